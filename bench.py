@@ -1,0 +1,168 @@
+#!/usr/bin/env python
+"""Headline benchmark: RAFT (full, raft-things config) training throughput on
+synthetic FlyingChairs-shaped pairs (368x496, 12 iterations, bf16, DDP over
+RCCL), plus Sintel-resolution (1088x436, padded 1088x440) 12-iteration
+inference FPS on rank 0.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched under torch.distributed.run (one rank per GPU).  W untimed
+steps, then exactly K timed steps bracketed by barrier + synchronize; the
+MAX time over ranks is reported; rank 0 prints ONE JSON line.
+
+value = total image pairs / s over all N GPUs (weak scaling: fixed per-GPU
+batch).  BASELINE.md publishes no training throughput (vs_baseline null for
+the training value); the inference FPS is compared against the paper's
+~10 fps (GTX 1080Ti, 1088x436) as ``inference.vs_baseline``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "train image-pairs/sec (node) + Sintel-res inference FPS, RAFT 12 iters"
+BASELINE_INFER_FPS = 10.0  # RAFT paper, GTX 1080Ti, 1088x436
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (reference mixed schedule: 8)")
+    ap.add_argument("--size", type=int, nargs=2, default=[368, 496])
+    ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--small", action="store_true")
+    ap.add_argument("--fp32", action="store_true", help="disable bf16 autocast")
+    ap.add_argument("--no-infer", action="store_true")
+    ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
+    ap.add_argument("--infer-reps", type=int, default=20)
+    ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from raft_stir_amd.config import make_args
+    from raft_stir_amd.models import RAFT
+    from raft_stir_amd.parallel import dist as rdist
+    from raft_stir_amd.train.loss import sequence_loss
+    from raft_stir_amd.train.optim import fetch_optimizer
+    from raft_stir_amd.data.synthetic import DevicePool
+
+    info = rdist.init_distributed()
+    dev = torch.device("cuda", info.local_rank)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(1234)
+
+    margs = make_args(small=a.small, mixed_precision=not a.fp32)
+    model = RAFT(margs).to(dev).to(memory_format=torch.channels_last)
+    model.train()
+    ddp = rdist.wrap_ddp(model, device=dev)
+    targs = argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
+    optimizer, scheduler = fetch_optimizer(targs, model)
+    H, W = a.size
+    pool = DevicePool(4, a.batch, H, W, dev, seed=info.rank * 97)
+
+    def step():
+        i1, i2, flow, valid = pool.next()
+        optimizer.zero_grad(set_to_none=True)
+        preds = ddp(i1, i2, iters=a.iters)
+        loss, _ = sequence_loss(preds, flow, valid, gamma=0.8, sync_metrics=False)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        optimizer.step()
+        scheduler.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    rdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    rdist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = rdist.all_reduce_max(elapsed, device=dev)
+    ms = 1000.0 * elapsed / max(a.steps, 1)
+    pairs_per_s = a.batch * info.world_size * a.steps / elapsed
+
+    infer = None
+    if info.is_main and not a.no_infer:
+        infer = bench_inference(model, dev, a)
+
+    if info.is_main:
+        out = {
+            "metric": METRIC,
+            "value": round(pairs_per_s, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": info.world_size,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if a.fp32 else "bf16",
+            "data": "synthetic (FlyingChairs-shaped 368x496 pairs, random-init weights)",
+            "config": {
+                "model": "RAFT-small" if a.small else "RAFT (raft-things config, 5.26M params)",
+                "global_batch": a.batch * info.world_size,
+                "per_gpu_batch": a.batch,
+                "seq_len": a.iters,
+                "image_size": [H, W],
+                "iters": a.iters,
+                "parallelism": f"dp{info.world_size}",
+            },
+            "final_loss": round(float(loss), 4),
+            "inference": infer,
+        }
+        print(json.dumps(out), flush=True)
+    rdist.shutdown()
+
+
+@torch.no_grad()
+def bench_inference(model, dev, a):
+    from raft_stir_amd.utils.padder import InputPadder
+    from raft_stir_amd.runtime.graph import GraphedInference
+    net = model
+    net.eval()
+    h, w = a.infer_size
+    g = torch.Generator(device=dev).manual_seed(0)
+    i1 = torch.rand(1, 3, h, w, device=dev, generator=g) * 255
+    i2 = torch.rand(1, 3, h, w, device=dev, generator=g) * 255
+    padder = InputPadder(i1.shape)
+    i1, i2 = padder.pad(i1, i2)
+    if a.no_graph:
+        run = lambda: net(i1, i2, iters=a.iters, test_mode=True)
+        mode = "eager"
+    else:
+        gi = GraphedInference(net, i1.shape, iters=a.iters)
+        run = lambda: gi(i1, i2)
+        mode = "hipgraph"
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.infer_reps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.infer_reps
+    net.train()
+    fps = 1.0 / dt
+    return {"fps": round(fps, 2), "ms_per_pair": round(1000 * dt, 3), "batch": 1,
+            "size": [h, w], "padded": list(i1.shape[-2:]), "iters": a.iters, "mode": mode,
+            "vs_baseline": round(fps / BASELINE_INFER_FPS, 2)}
+
+
+if __name__ == "__main__":
+    main()

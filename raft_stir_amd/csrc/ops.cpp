@@ -1,0 +1,418 @@
+// Operator registration: torch.ops.raft_stir.*  (TORCH_LIBRARY, no pybind).
+//
+// Replaces reference alt_cuda_corr/correlation.cpp (pybind module with
+// CHECK_CUDA/CHECK_CONTIGUOUS, launching on the legacy default stream).  Every
+// op here validates shapes/dtypes/devices on the host BEFORE launching (a bad
+// shape must never reach a kernel) and launches on PyTorch's current HIP
+// stream, so the ops compose with torch streams and hipGraph capture.
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include <cmath>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+namespace rs {
+void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1, int H2, int W2,
+                        int C, int levels, float* const* out, const int* Hs, const int* Ws,
+                        float scale, hipStream_t stream);
+void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* Ws, int levels,
+                            const float* coords, int B, int H1, int W1, int r, void* out,
+                            bool out_bf16, hipStream_t stream);
+void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
+                            const float* coords, int B, int H1, int W1, int r, const void* dout,
+                            bool dout_bf16, hipStream_t stream);
+void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
+                          float scale, hipStream_t stream);
+bool corr_otf_supported_channels(int C);
+void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
+                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int r, float scale, void* out, bool out_bf16, hipStream_t stream);
+void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
+                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int r, float scale, const void* dout, bool dout_bf16, float* df1,
+                         float* const* df2, hipStream_t stream);
+void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, int N, int H, int W,
+                          float* out, hipStream_t stream);
+void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
+                          bool dup_bf16, int N, int H, int W, void* dmask, float* dflow,
+                          float* partial, hipStream_t stream);
+void gru_gate_zr_launch(bool bf, const void* zr, const void* h, const void* x, long P, int hd,
+                        int cin, void* z, void* r, void* rhx, hipStream_t s);
+void gru_gate_q_launch(bool bf, const void* q, const void* z, const void* h, long P, int hd,
+                       void* hn, void* qt, hipStream_t s);
+void gru_bwd_q_launch(bool bf, const void* dhn, bool dhn_bf, const void* z, const void* h,
+                      const void* qt, long P, int hd, void* dq, void* dzr, float* dh,
+                      hipStream_t s);
+void gru_bwd_r_launch(bool bf, const void* drhx, const void* h, const void* r, long P, int hd,
+                      int cin, void* dzr, hipStream_t s);
+void gru_bwd_fin_launch(bool bf, const float* dhd, const void* drhx, const void* r,
+                        const void* dhx, long P, int hd, int cin, void* dh, void* dx,
+                        hipStream_t s);
+}  // namespace rs
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous (got strides ", t.strides(), ")");
+}
+void check_dtype(const Tensor& t, std::initializer_list<at::ScalarType> ok, const char* name) {
+  for (auto s : ok)
+    if (t.scalar_type() == s) return;
+  TORCH_CHECK(false, name, " has unsupported dtype ", t.scalar_type());
+}
+bool is_bf16(const Tensor& t) { return t.scalar_type() == at::kBFloat16; }
+
+// Pooled sizes with floor semantics (avg_pool2d(2,2) applied l times).
+void level_sizes(int H, int W, int levels, int* Hs, int* Ws) {
+  for (int l = 0; l < levels; ++l) {
+    Hs[l] = H;
+    Ws[l] = W;
+    H /= 2;
+    W /= 2;
+  }
+}
+
+// ---------------------------------------------------------------- corr volume
+std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t levels, double scale) {
+  check_gpu(f1, "f1");
+  check_gpu(f2, "f2");
+  check_dtype(f1, {at::kFloat, at::kBFloat16}, "f1");
+  TORCH_CHECK(f1.scalar_type() == f2.scalar_type(), "f1/f2 dtype mismatch");
+  TORCH_CHECK(f1.dim() == 3 && f2.dim() == 4, "f1 must be (B,N1,C), f2 (B,H2,W2,C)");
+  TORCH_CHECK(levels >= 1 && levels <= 4, "levels must be in [1,4]");
+  const int B = f1.size(0), N1 = f1.size(1), C = f1.size(2);
+  const int H2 = f2.size(1), W2 = f2.size(2);
+  TORCH_CHECK(f2.size(0) == B && f2.size(3) == C, "f1/f2 batch/channel mismatch");
+  TORCH_CHECK(C % (is_bf16(f1) ? 64 : 32) == 0, "channels must be a multiple of 64 (bf16) / 32");
+  c10::hip::HIPGuard guard(f1.device());
+  int Hs[4], Ws[4];
+  level_sizes(H2, W2, levels, Hs, Ws);
+  for (int l = 0; l < levels; ++l) TORCH_CHECK(Hs[l] > 0 && Ws[l] > 0, "pyramid level ", l, " is empty");
+  std::vector<Tensor> outs;
+  float* ptrs[4];
+  for (int l = 0; l < levels; ++l) {
+    outs.push_back(at::empty({B, N1, Hs[l], Ws[l]}, f1.options().dtype(at::kFloat)));
+    ptrs[l] = outs.back().data_ptr<float>();
+  }
+  rs::corr_volume_launch(f1.data_ptr(), f2.data_ptr(), is_bf16(f1), B, N1, H2, W2, C, levels, ptrs,
+                         Hs, Ws, (float)scale, cur_stream());
+  return outs;
+}
+
+void check_pyr(const std::vector<Tensor>& pyr, int B, int N1, int* Hs, int* Ws) {
+  TORCH_CHECK(!pyr.empty() && pyr.size() <= 4, "pyramid must have 1..4 levels");
+  for (size_t l = 0; l < pyr.size(); ++l) {
+    check_gpu(pyr[l], "pyramid level");
+    check_dtype(pyr[l], {at::kFloat}, "pyramid level");
+    TORCH_CHECK(pyr[l].dim() == 4 && pyr[l].size(0) == B && pyr[l].size(1) == N1,
+                "pyramid level ", l, " must be (B, H1*W1, H_l, W_l)");
+    Hs[l] = pyr[l].size(2);
+    Ws[l] = pyr[l].size(3);
+  }
+}
+
+void check_coords(const Tensor& coords) {
+  check_gpu(coords, "coords");
+  check_dtype(coords, {at::kFloat}, "coords");
+  TORCH_CHECK(coords.dim() == 4 && coords.size(1) == 2, "coords must be (B,2,H,W)");
+}
+
+// ---------------------------------------------------------------- lookup
+Tensor corr_lookup(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t radius,
+                   bool out_bf16) {
+  check_coords(coords);
+  const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
+  int Hs[4], Ws[4];
+  check_pyr(pyr, B, H1 * W1, Hs, Ws);
+  TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
+  c10::hip::HIPGuard guard(coords.device());
+  const int levels = pyr.size();
+  const int D = 2 * radius + 1;
+  Tensor out = at::empty({B, H1, W1, levels * D * D},
+                         coords.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  const float* ptrs[4];
+  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
+  rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
+                             out.data_ptr(), out_bf16, cur_stream());
+  return out;
+}
+
+void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords, int64_t radius,
+                          const Tensor& dout) {
+  check_coords(coords);
+  const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
+  int Hs[4], Ws[4];
+  check_pyr(gpyr, B, H1 * W1, Hs, Ws);
+  const int levels = gpyr.size();
+  const int D = 2 * radius + 1;
+  check_gpu(dout, "dout");
+  check_dtype(dout, {at::kFloat, at::kBFloat16}, "dout");
+  TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
+                  dout.size(3) == levels * D * D,
+              "dout must be (B,H1,W1,levels*(2r+1)^2)");
+  c10::hip::HIPGuard guard(coords.device());
+  float* ptrs[4];
+  for (int l = 0; l < levels; ++l) ptrs[l] = gpyr[l].data_ptr<float>();
+  rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
+                             dout.data_ptr(), is_bf16(dout), cur_stream());
+}
+
+void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
+  TORCH_CHECK(!gpyr.empty() && gpyr.size() <= 4, "pyramid must have 1..4 levels");
+  const int B = gpyr[0].size(0), N1 = gpyr[0].size(1);
+  int Hs[4], Ws[4];
+  check_pyr(gpyr, B, N1, Hs, Ws);
+  c10::hip::HIPGuard guard(gpyr[0].device());
+  float* ptrs[4];
+  for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
+}
+
+// ---------------------------------------------------------------- on-the-fly corr
+void check_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords, int* Hs,
+               int* Ws) {
+  check_gpu(f1, "f1");
+  check_dtype(f1, {at::kFloat, at::kBFloat16}, "f1");
+  check_coords(coords);
+  TORCH_CHECK(f1.dim() == 4, "f1 must be (B,H1,W1,C)");
+  const int B = f1.size(0), C = f1.size(3);
+  TORCH_CHECK(coords.size(0) == B && coords.size(2) == f1.size(1) && coords.size(3) == f1.size(2),
+              "coords/f1 shape mismatch");
+  TORCH_CHECK(rs::corr_otf_supported_channels(C), "on-the-fly corr: unsupported channel count ", C);
+  TORCH_CHECK(!f2.empty() && f2.size() <= 4, "f2 pyramid must have 1..4 levels");
+  for (size_t l = 0; l < f2.size(); ++l) {
+    check_gpu(f2[l], "f2 level");
+    TORCH_CHECK(f2[l].scalar_type() == f1.scalar_type(), "f2/f1 dtype mismatch");
+    TORCH_CHECK(f2[l].dim() == 4 && f2[l].size(0) == B && f2[l].size(3) == C,
+                "f2 level must be (B,H_l,W_l,C)");
+    Hs[l] = f2[l].size(1);
+    Ws[l] = f2[l].size(2);
+  }
+}
+
+Tensor corr_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
+                int64_t radius, double scale, bool out_bf16) {
+  int Hs[4], Ws[4];
+  check_otf(f1, f2, coords, Hs, Ws);
+  TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
+  c10::hip::HIPGuard guard(f1.device());
+  const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
+  const int levels = f2.size(), D = 2 * radius + 1;
+  Tensor out = at::empty({B, H1, W1, levels * D * D},
+                         f1.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  const void* p[4];
+  for (int l = 0; l < levels; ++l) p[l] = f2[l].data_ptr();
+  rs::corr_otf_fwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
+                          B, H1 * W1, C, radius, (float)scale, out.data_ptr(), out_bf16,
+                          cur_stream());
+  return out;
+}
+
+std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor>& f2,
+                                      const Tensor& coords, int64_t radius, double scale,
+                                      const Tensor& dout) {
+  int Hs[4], Ws[4];
+  check_otf(f1, f2, coords, Hs, Ws);
+  c10::hip::HIPGuard guard(f1.device());
+  const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
+  const int levels = f2.size(), D = 2 * radius + 1;
+  check_gpu(dout, "dout");
+  TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
+                  dout.size(3) == levels * D * D,
+              "dout must be (B,H1,W1,levels*(2r+1)^2)");
+  std::vector<Tensor> res;
+  Tensor df1 = at::empty({B, H1, W1, C}, f1.options().dtype(at::kFloat));
+  res.push_back(df1);
+  const void* p[4];
+  float* d[4];
+  for (int l = 0; l < levels; ++l) {
+    p[l] = f2[l].data_ptr();
+    res.push_back(at::zeros({B, Hs[l], Ws[l], C}, f1.options().dtype(at::kFloat)));
+    d[l] = res.back().data_ptr<float>();
+  }
+  rs::corr_otf_bwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
+                          B, H1 * W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
+                          df1.data_ptr<float>(), d, cur_stream());
+  return res;
+}
+
+// ---------------------------------------------------------------- convex upsample
+Tensor convex_upsample(const Tensor& flow, const Tensor& mask) {
+  check_gpu(flow, "flow");
+  check_dtype(flow, {at::kFloat}, "flow");
+  check_gpu(mask, "mask");
+  check_dtype(mask, {at::kFloat, at::kBFloat16}, "mask");
+  TORCH_CHECK(flow.dim() == 4 && flow.size(1) == 2, "flow must be (N,2,H,W)");
+  const int N = flow.size(0), H = flow.size(2), W = flow.size(3);
+  TORCH_CHECK(mask.dim() == 4 && mask.size(0) == N && mask.size(1) == H && mask.size(2) == W &&
+                  mask.size(3) == 576,
+              "mask must be channels-last (N,H,W,576)");
+  c10::hip::HIPGuard guard(flow.device());
+  Tensor out = at::empty({N, 2, 8 * H, 8 * W}, flow.options());
+  rs::convex_up_fwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), N, H, W,
+                           out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& mask,
+                                             const Tensor& dup) {
+  check_gpu(flow, "flow");
+  check_gpu(mask, "mask");
+  check_gpu(dup, "grad");
+  check_dtype(dup, {at::kFloat, at::kBFloat16}, "grad");
+  const int N = flow.size(0), H = flow.size(2), W = flow.size(3);
+  TORCH_CHECK(mask.dim() == 4 && mask.size(3) == 576, "mask must be (N,H,W,576)");
+  TORCH_CHECK(dup.dim() == 4 && dup.size(0) == N && dup.size(1) == 2 && dup.size(2) == 8 * H &&
+                  dup.size(3) == 8 * W,
+              "grad must be (N,2,8H,8W)");
+  c10::hip::HIPGuard guard(flow.device());
+  Tensor dflow = at::empty_like(flow);
+  Tensor dmask = at::empty_like(mask);
+  Tensor partial = at::empty({(int64_t)N * H * W * 18}, flow.options());
+  rs::convex_up_bwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), dup.data_ptr(),
+                           is_bf16(dup), N, H, W, dmask.data_ptr(), dflow.data_ptr<float>(),
+                           partial.data_ptr<float>(), cur_stream());
+  return {dflow, dmask};
+}
+
+// ---------------------------------------------------------------- GRU gates
+// All inputs are NHWC-contiguous, viewed as (P, channels).
+int64_t pixels(const Tensor& t) { return t.numel() / t.size(-1); }
+
+std::vector<Tensor> gru_gate_zr(const Tensor& zr, const Tensor& h, const Tensor& x) {
+  check_gpu(zr, "zr");
+  check_gpu(h, "h");
+  check_gpu(x, "x");
+  check_dtype(h, {at::kFloat, at::kBFloat16}, "h");
+  TORCH_CHECK(zr.scalar_type() == h.scalar_type() && x.scalar_type() == h.scalar_type(),
+              "gru_gate_zr: dtype mismatch");
+  const int hd = h.size(-1), cin = x.size(-1);
+  const int64_t P = pixels(h);
+  TORCH_CHECK(zr.size(-1) == 2 * hd && pixels(zr) == P && pixels(x) == P, "gru_gate_zr: shapes");
+  c10::hip::HIPGuard guard(h.device());
+  auto sz = h.sizes().vec();
+  Tensor z = at::empty_like(h), r = at::empty_like(h);
+  sz.back() = hd + cin;
+  Tensor rhx = at::empty(sz, h.options());
+  rs::gru_gate_zr_launch(is_bf16(h), zr.data_ptr(), h.data_ptr(), x.data_ptr(), P, hd, cin,
+                         z.data_ptr(), r.data_ptr(), rhx.data_ptr(), cur_stream());
+  return {z, r, rhx};
+}
+
+std::vector<Tensor> gru_gate_q(const Tensor& q, const Tensor& z, const Tensor& h) {
+  check_gpu(q, "q");
+  check_gpu(z, "z");
+  check_gpu(h, "h");
+  TORCH_CHECK(q.sizes() == h.sizes() && z.sizes() == h.sizes(), "gru_gate_q: shapes");
+  TORCH_CHECK(q.scalar_type() == h.scalar_type() && z.scalar_type() == h.scalar_type(),
+              "gru_gate_q: dtype mismatch");
+  c10::hip::HIPGuard guard(h.device());
+  Tensor hn = at::empty_like(h), qt = at::empty_like(h);
+  rs::gru_gate_q_launch(is_bf16(h), q.data_ptr(), z.data_ptr(), h.data_ptr(), pixels(h),
+                        h.size(-1), hn.data_ptr(), qt.data_ptr(), cur_stream());
+  return {hn, qt};
+}
+
+std::vector<Tensor> gru_bwd_q(const Tensor& dhn, const Tensor& z, const Tensor& h,
+                              const Tensor& qt) {
+  check_gpu(dhn, "dhn");
+  check_gpu(z, "z");
+  check_gpu(h, "h");
+  check_gpu(qt, "qt");
+  TORCH_CHECK(dhn.sizes() == h.sizes() && z.sizes() == h.sizes() && qt.sizes() == h.sizes(),
+              "gru_bwd_q: shapes");
+  c10::hip::HIPGuard guard(h.device());
+  const int hd = h.size(-1);
+  const int64_t P = pixels(h);
+  auto sz = h.sizes().vec();
+  Tensor dq = at::empty_like(h);
+  sz.back() = 2 * hd;
+  Tensor dzr = at::empty(sz, h.options());
+  Tensor dh = at::empty(h.sizes(), h.options().dtype(at::kFloat));
+  rs::gru_bwd_q_launch(is_bf16(h), dhn.data_ptr(), is_bf16(dhn), z.data_ptr(), h.data_ptr(),
+                       qt.data_ptr(), P, hd, dq.data_ptr(), dzr.data_ptr(), dh.data_ptr<float>(),
+                       cur_stream());
+  return {dq, dzr, dh};
+}
+
+void gru_bwd_r(const Tensor& drhx, const Tensor& h, const Tensor& r, const Tensor& dzr) {
+  check_gpu(drhx, "drhx");
+  check_gpu(h, "h");
+  check_gpu(r, "r");
+  check_gpu(dzr, "dzr");
+  const int hd = h.size(-1), cin = drhx.size(-1) - hd;
+  const int64_t P = pixels(h);
+  TORCH_CHECK(pixels(drhx) == P && dzr.size(-1) == 2 * hd && pixels(dzr) == P, "gru_bwd_r: shapes");
+  TORCH_CHECK(drhx.scalar_type() == h.scalar_type() && dzr.scalar_type() == h.scalar_type(),
+              "gru_bwd_r: dtype mismatch");
+  c10::hip::HIPGuard guard(h.device());
+  rs::gru_bwd_r_launch(is_bf16(h), drhx.data_ptr(), h.data_ptr(), r.data_ptr(), P, hd, cin,
+                       dzr.data_ptr(), cur_stream());
+}
+
+std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Tensor& r,
+                                const Tensor& dhx) {
+  check_gpu(dhd, "dhd");
+  check_gpu(drhx, "drhx");
+  check_gpu(r, "r");
+  check_gpu(dhx, "dhx");
+  check_dtype(dhd, {at::kFloat}, "dhd");
+  const int hd = r.size(-1), cin = drhx.size(-1) - hd;
+  const int64_t P = pixels(r);
+  TORCH_CHECK(pixels(drhx) == P && dhx.sizes() == drhx.sizes() && dhd.sizes() == r.sizes(),
+              "gru_bwd_fin: shapes");
+  TORCH_CHECK(drhx.scalar_type() == r.scalar_type() && dhx.scalar_type() == r.scalar_type(),
+              "gru_bwd_fin: dtype mismatch");
+  c10::hip::HIPGuard guard(r.device());
+  auto sz = r.sizes().vec();
+  Tensor dh = at::empty_like(r);
+  sz.back() = cin;
+  Tensor dx = at::empty(sz, r.options());
+  rs::gru_bwd_fin_launch(is_bf16(r), dhd.data_ptr<float>(), drhx.data_ptr(), r.data_ptr(),
+                         dhx.data_ptr(), P, hd, cin, dh.data_ptr(), dx.data_ptr(), cur_stream());
+  return {dh, dx};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(raft_stir, m) {
+  m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale) -> Tensor[]");
+  m.def("corr_lookup(Tensor[] pyr, Tensor coords, int radius, bool out_bf16) -> Tensor");
+  m.def("corr_lookup_backward(Tensor(a!)[] gpyr, Tensor coords, int radius, Tensor dout) -> ()");
+  m.def("pyr_grad_fold(Tensor(a!)[] gpyr, float scale) -> ()");
+  m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
+  m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
+  m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
+  m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> Tensor[]");
+  m.def("gru_gate_zr(Tensor zr, Tensor h, Tensor x) -> Tensor[]");
+  m.def("gru_gate_q(Tensor q, Tensor z, Tensor h) -> Tensor[]");
+  m.def("gru_bwd_q(Tensor dhn, Tensor z, Tensor h, Tensor qt) -> Tensor[]");
+  m.def("gru_bwd_r(Tensor drhx, Tensor h, Tensor r, Tensor(a!) dzr) -> ()");
+  m.def("gru_bwd_fin(Tensor dhd, Tensor drhx, Tensor r, Tensor dhx) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
+  m.impl("corr_volume", &corr_volume);
+  m.impl("corr_lookup", &corr_lookup);
+  m.impl("corr_lookup_backward", &corr_lookup_backward);
+  m.impl("pyr_grad_fold", &pyr_grad_fold);
+  m.impl("corr_otf", &corr_otf);
+  m.impl("corr_otf_backward", &corr_otf_backward);
+  m.impl("convex_upsample", &convex_upsample);
+  m.impl("convex_upsample_backward", &convex_upsample_backward);
+  m.impl("gru_gate_zr", &gru_gate_zr);
+  m.impl("gru_gate_q", &gru_gate_q);
+  m.impl("gru_bwd_q", &gru_bwd_q);
+  m.impl("gru_bwd_r", &gru_bwd_r);
+  m.impl("gru_bwd_fin", &gru_bwd_fin);
+}

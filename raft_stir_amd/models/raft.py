@@ -1,0 +1,136 @@
+"""RAFT: Recurrent All-Pairs Field Transforms, MI355X engine.
+
+Public API identical to reference core/raft.py:24-144:
+    model = RAFT(args)             # args: Namespace with .small, .mixed_precision, ...
+    flow_predictions = model(image1, image2, iters=12)                  # training
+    flow_low, flow_up = model(image1, image2, iters=12, test_mode=True)  # inference
+    model.freeze_bn()
+and the same ``state_dict`` keys (fnet/cnet/update_block...), so reference
+``.pth`` checkpoints (with or without the DataParallel ``module.`` prefix, see
+raft_stir_amd.train.checkpoint) load unchanged.
+
+Engine differences (outputs unchanged):
+  * GPU: channels_last activations, bf16 autocast when ``mixed_precision``
+    (the reference used fp16 AMP), all-pairs volume + pyramid from one MFMA
+    kernel, HIP pyramid lookup, fused ConvGRU gates, HIP convex upsampler.
+  * test_mode computes the mask head and the convex upsampling only on the
+    last iteration -- the only one whose output is returned (reference B7).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..config import RAFTConfig, resolve_config
+from ..ops import _ext
+from ..ops import reference as ref
+from ..ops.upsample import convex_upsample, upflow8
+from .corr import CorrBlock, AlternateCorrBlock
+from .extractor import BasicEncoder, SmallEncoder
+from .update import BasicUpdateBlock, SmallUpdateBlock
+
+
+class RAFT(nn.Module):
+    def __init__(self, args=None, **overrides):
+        super().__init__()
+        cfg = args if isinstance(args, RAFTConfig) else resolve_config(args, **overrides)
+        self.cfg = cfg
+        self.args = args if args is not None else cfg
+        self.hidden_dim = hdim = cfg.hidden_dim
+        self.context_dim = cdim = cfg.context_dim
+        if cfg.small:
+            self.fnet = SmallEncoder(output_dim=cfg.fnet_dim, norm_fn="instance", dropout=cfg.dropout)
+            self.cnet = SmallEncoder(output_dim=hdim + cdim, norm_fn="none", dropout=cfg.dropout)
+            self.update_block = SmallUpdateBlock(cfg, hidden_dim=hdim)
+        else:
+            self.fnet = BasicEncoder(output_dim=cfg.fnet_dim, norm_fn="instance", dropout=cfg.dropout)
+            self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch", dropout=cfg.dropout)
+            self.update_block = BasicUpdateBlock(cfg, hidden_dim=hdim)
+        self.set_fused_gru(cfg.fused_gru)
+
+    # ------------------------------------------------------------------ utils
+    def set_fused_gru(self, enabled: bool):
+        for m in self.modules():
+            if hasattr(m, "fused") and m is not self:
+                m.fused = enabled
+
+    def freeze_bn(self):
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    def initialize_flow(self, img):
+        N, _, H, W = img.shape
+        c0 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
+        c1 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
+        return c0, c1
+
+    def upsample_flow(self, flow, mask):
+        return convex_upsample(flow, mask)
+
+    def _autocast(self, device):
+        enabled = bool(self.cfg.mixed_precision) and device.type == "cuda"
+        return torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=enabled)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
+        dev = image1.device
+        gpu = dev.type == "cuda"
+        image1 = 2 * (image1 / 255.0) - 1.0
+        image2 = 2 * (image2 / 255.0) - 1.0
+        fmt = torch.channels_last if gpu else torch.contiguous_format
+        image1 = image1.contiguous(memory_format=fmt)
+        image2 = image2.contiguous(memory_format=fmt)
+        hdim, cdim = self.hidden_dim, self.context_dim
+        mixed = bool(self.cfg.mixed_precision) and gpu
+
+        with self._autocast(dev):
+            fmap1, fmap2 = self.fnet([image1, image2])
+        # The reference casts the features to fp32 (core/raft.py:102-103).  Under
+        # bf16 autocast they are exactly representable in bf16, so the MFMA
+        # volume kernel consumes them in bf16 with fp32 accumulation (exact
+        # products); in fp32 mode it runs the exact fp32 MFMA variant.
+        if not (mixed and _ext.use_hip(fmap1)):
+            fmap1, fmap2 = fmap1.float(), fmap2.float()
+        corr_dtype = torch.bfloat16 if mixed else torch.float32
+        block = AlternateCorrBlock if self.cfg.alternate_corr else CorrBlock
+        corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
+                        radius=self.cfg.corr_radius, out_dtype=corr_dtype)
+
+        with self._autocast(dev):
+            cnet = self.cnet(image1)
+            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+            net = torch.tanh(net)
+            inp = torch.relu(inp)
+
+        coords0, coords1 = self.initialize_flow(image1)
+        if flow_init is not None:
+            coords1 = coords1 + flow_init
+
+        small = self.cfg.small
+        preds = []
+        flow_up = None
+        for itr in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn(coords1)
+            flow = coords1 - coords0
+            last = itr == iters - 1
+            want_up = (not test_mode) or last
+            with self._autocast(dev):
+                if small:
+                    net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
+                else:
+                    net, up_mask, delta_flow = self.update_block(net, inp, corr, flow,
+                                                                 upsample=want_up)
+            coords1 = coords1 + delta_flow.float()
+            if not want_up:
+                continue
+            if up_mask is None:
+                flow_up = upflow8(coords1 - coords0)
+            else:
+                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+            preds.append(flow_up)
+
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return preds

@@ -1,0 +1,186 @@
+"""Correlation ops: all-pairs volume + pyramid, window lookup, on-the-fly.
+
+GPU tensors run the hand-written HIP kernels (csrc/corr_volume.hip,
+csrc/corr_lookup.hip, csrc/corr_onthefly.hip); CPU tensors and export run
+the ATen oracles of ops/reference.py.
+
+Autograd design for the all-pairs path (training).  The reference
+differentiates through ``grid_sample`` per level per iteration (a dense,
+zero-filled pyramid gradient each time) and then through
+``avg_pool2d`` and ``bmm``.  Here:
+
+* :class:`_CorrVolume` builds the whole pyramid in one kernel and returns a
+  0-d *token*; the pyramid itself lives in a :class:`CorrState` that the
+  lookups read.
+* every :class:`_CorrLookup` backward accumulates its cell gradients straight
+  into ONE pyramid-shaped fp32 buffer owned by the state (own-row writes, no
+  atomics) and returns a zero token gradient;
+* when autograd reaches the volume node (after all lookups, by topology) it
+  folds the pyramid gradient into level 0 (avg-pool backward + 1/sqrt(C)) and
+  issues the two GEMMs  df1 = G f2,  df2 = G^T f1  once per step.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from . import reference as ref
+
+
+class CorrState:
+    __slots__ = ("pyr", "gpyr", "levels", "radius", "scale", "shape")
+
+    def __init__(self, levels: int, radius: int):
+        self.pyr: Optional[List[torch.Tensor]] = None
+        self.gpyr: Optional[List[torch.Tensor]] = None
+        self.levels = levels
+        self.radius = radius
+        self.scale = 1.0
+        self.shape = None
+
+
+def to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """(B,C,H,W) -> contiguous (B,H,W,C) (free when x is channels_last)."""
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def from_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """contiguous (B,H,W,C) -> (B,C,H,W) view with channels_last strides."""
+    return x.permute(0, 3, 1, 2)
+
+
+class _CorrVolume(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f1, f2, state: CorrState):
+        # f1: (B,N1,C), f2: (B,H2,W2,C) contiguous, fp32 or bf16
+        state.scale = 1.0 / math.sqrt(f1.shape[-1])
+        state.pyr = list(torch.ops.raft_stir.corr_volume(f1, f2, state.levels, state.scale))
+        state.shape = (f1.shape, f2.shape)
+        ctx.state = state
+        ctx.save_for_backward(f1, f2)
+        return f1.new_zeros((), dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, _dtoken):
+        state: CorrState = ctx.state
+        f1, f2 = ctx.saved_tensors
+        if state.gpyr is None:
+            return None, None, None
+        B, N1, C = f1.shape
+        _, H2, W2, _ = f2.shape
+        torch.ops.raft_stir.pyr_grad_fold(state.gpyr, state.scale)
+        G = state.gpyr[0].view(B, N1, H2 * W2)
+        df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C).float())
+        df2 = torch.bmm(G.transpose(1, 2), f1.float())
+        state.gpyr = None
+        state.pyr = None
+        return df1.to(f1.dtype), df2.view(B, H2, W2, C).to(f2.dtype), None
+
+
+class _CorrLookup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, coords, state: CorrState, out_bf16: bool):
+        ctx.state = state
+        ctx.save_for_backward(coords)
+        return torch.ops.raft_stir.corr_lookup(state.pyr, coords, state.radius, out_bf16)
+
+    @staticmethod
+    def backward(ctx, dout):
+        state: CorrState = ctx.state
+        (coords,) = ctx.saved_tensors
+        if state.gpyr is None:
+            state.gpyr = [torch.zeros_like(p) for p in state.pyr]
+        torch.ops.raft_stir.corr_lookup_backward(state.gpyr, coords, state.radius,
+                                                 dout.contiguous())
+        return coords.new_zeros(()), None, None, None
+
+
+class AllPairsCorr:
+    """All-pairs correlation pyramid + lookup (reference CorrBlock semantics).
+
+    Built from NCHW (ideally channels_last) feature maps. ``__call__(coords)``
+    returns (B, levels*(2r+1)^2, H, W); on GPU the result is a channels_last
+    view in ``out_dtype``.
+    """
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32):
+        self.num_levels = num_levels
+        self.radius = radius
+        self.out_dtype = out_dtype
+        self.hip = _ext.use_hip(fmap1)
+        if self.hip:
+            f1 = to_nhwc(fmap1)
+            B, H, W, C = f1.shape
+            f2 = to_nhwc(fmap2.to(f1.dtype))
+            if f1.dtype not in (torch.float32, torch.bfloat16):
+                f1, f2 = f1.float(), f2.float()
+            self.state = CorrState(num_levels, radius)
+            self.token = _CorrVolume.apply(f1.view(B, H * W, C), f2, self.state)
+        else:
+            self.pyramid = ref.corr_pyramid(fmap1, fmap2, num_levels)
+
+    @property
+    def corr_pyramid(self):
+        if self.hip:
+            B = self.state.shape[0][0]
+            return [p.reshape(-1, 1, p.shape[2], p.shape[3]) for p in self.state.pyr]
+        return self.pyramid
+
+    def __call__(self, coords):
+        if self.hip:
+            out = _CorrLookup.apply(self.token, coords.float().contiguous(), self.state,
+                                    self.out_dtype == torch.bfloat16)
+            return from_nhwc(out)
+        return ref.corr_lookup(self.pyramid, coords, self.radius).to(self.out_dtype)
+
+
+class _CorrOTF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, coords, radius, scale, out_bf16, f1, *f2s):
+        ctx.radius, ctx.scale = radius, scale
+        ctx.save_for_backward(coords, f1, *f2s)
+        return torch.ops.raft_stir.corr_otf(f1, list(f2s), coords, radius, scale, out_bf16)
+
+    @staticmethod
+    def backward(ctx, dout):
+        coords, f1, *f2s = ctx.saved_tensors
+        grads = torch.ops.raft_stir.corr_otf_backward(f1, list(f2s), coords, ctx.radius,
+                                                      ctx.scale, dout.contiguous())
+        df1 = grads[0].to(f1.dtype)
+        df2 = [g.to(f.dtype) for g, f in zip(grads[1:], f2s)]
+        return (None, None, None, None, df1, *df2)
+
+
+class OnTheFlyCorr:
+    """Memory-efficient correlation (reference AlternateCorrBlock semantics,
+    core/corr.py:63-91) -- O(HW*C) memory, recomputed every iteration, and
+    (unlike the reference) differentiable."""
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32):
+        self.num_levels = num_levels
+        self.radius = radius
+        self.out_dtype = out_dtype
+        self.hip = _ext.use_hip(fmap1)
+        self.fmap1, self.fmap2 = fmap1, fmap2
+        if self.hip:
+            dt = torch.bfloat16 if fmap1.dtype == torch.bfloat16 else torch.float32
+            f1 = fmap1.to(dt).contiguous(memory_format=torch.channels_last)
+            f2 = fmap2.to(dt).contiguous(memory_format=torch.channels_last)
+            levels = [f2]
+            for _ in range(num_levels - 1):
+                levels.append(F.avg_pool2d(levels[-1], 2, stride=2))
+            self.f1 = to_nhwc(f1)
+            self.f2s = [to_nhwc(t) for t in levels]
+            self.scale = 1.0 / math.sqrt(fmap1.shape[1])
+
+    def __call__(self, coords):
+        if self.hip:
+            out = _CorrOTF.apply(coords.float().contiguous(), self.radius, self.scale,
+                                 self.out_dtype == torch.bfloat16, self.f1, *self.f2s)
+            return from_nhwc(out)
+        return ref.corr_onthefly(self.fmap1, self.fmap2, coords, self.radius,
+                                 self.num_levels).to(self.out_dtype)

@@ -1,0 +1,179 @@
+"""HIP kernel numerics vs the plain-PyTorch fp32 references (ops/reference.py).
+
+Odd sizes on purpose (h % 4, w % 8 != 0; pooled levels with floor sizes), both
+radii (3: RAFT-small, 4: RAFT), both channel counts (128, 256), B > 1.
+"""
+import math
+
+import pytest
+import torch
+
+from raft_stir_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _fmaps(B, C, H, W, dev, dtype=torch.float32, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    f1 = torch.randn(B, C, H, W, generator=g)
+    f2 = torch.randn(B, C, H, W, generator=g)
+    return f1.to(dev, dtype), f2.to(dev, dtype)
+
+
+def _coords(B, H, W, dev, spread=6.0, seed=1):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    base = ref.coords_grid(B, H, W)
+    return (base + spread * torch.randn(B, 2, H, W, generator=g)).to(dev)
+
+
+@pytest.mark.parametrize("C", [128, 256])
+@pytest.mark.parametrize("HW", [(11, 37), (46, 62), (8, 8)])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_corr_volume_pyramid(cuda, C, HW, bf16):
+    H, W = HW
+    B = 2
+    dt = torch.bfloat16 if bf16 else torch.float32
+    f1, f2 = _fmaps(B, C, H, W, cuda, dt)
+    levels = 4 if min(H, W) >= 8 else 3
+    pyr = torch.ops.raft_stir.corr_volume(
+        f1.permute(0, 2, 3, 1).reshape(B, H * W, C).contiguous(),
+        f2.permute(0, 2, 3, 1).contiguous(), levels, 1.0 / math.sqrt(C))
+    want = ref.corr_pyramid(f1.float(), f2.float(), levels)
+    for l in range(levels):
+        got = pyr[l].reshape(want[l].shape)
+        tol = 2e-3 if bf16 else 1e-4
+        torch.testing.assert_close(got, want[l], atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("r", [3, 4])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_corr_lookup_forward(cuda, r, out_bf16):
+    B, C, H, W = 2, 64, 23, 29
+    f1, f2 = _fmaps(B, C, H, W, "cpu")
+    pyr = ref.corr_pyramid(f1, f2, 4)
+    coords = _coords(B, H, W, "cpu")
+    want = ref.corr_lookup(pyr, coords, r)
+    gp = [p.reshape(B, H * W, p.shape[-2], p.shape[-1]).contiguous().to(cuda) for p in pyr]
+    got = torch.ops.raft_stir.corr_lookup(gp, coords.to(cuda), r, out_bf16)
+    got = got.permute(0, 3, 1, 2).float().cpu()
+    tol = 2e-2 if out_bf16 else 1e-5
+    torch.testing.assert_close(got, want, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_allpairs_corr_autograd(cuda, small):
+    """Full chain (volume -> 3 lookups -> loss) gradient vs ATen autograd."""
+    from raft_stir_amd.ops.corr import AllPairsCorr
+    B, C, H, W = 2, (128 if small else 256), 13, 21
+    r = 3 if small else 4
+    f1, f2 = _fmaps(B, C, H, W, "cpu", seed=3)
+    coords = [_coords(B, H, W, "cpu", seed=s) for s in range(3)]
+    g = torch.Generator().manual_seed(7)
+    wts = [torch.randn(B, 4 * (2 * r + 1) ** 2, H, W, generator=g) for _ in coords]
+
+    a1, a2 = f1.clone().requires_grad_(), f2.clone().requires_grad_()
+    pyr = ref.corr_pyramid(a1, a2, 4)
+    loss_ref = sum((ref.corr_lookup(pyr, c, r) * w).sum() for c, w in zip(coords, wts))
+    loss_ref.backward()
+
+    b1 = f1.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    b2 = f2.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    blk = AllPairsCorr(b1, b2, 4, r)
+    loss = sum((blk(c.to(cuda)) * w.to(cuda)).sum() for c, w in zip(coords, wts))
+    loss.backward()
+    torch.testing.assert_close(loss.cpu(), loss_ref.detach(), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(b1.grad.cpu(), a1.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(b2.grad.cpu(), a2.grad, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("C", [128, 256])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_onthefly_corr_fwd_bwd(cuda, C, bf16):
+    from raft_stir_amd.ops.corr import OnTheFlyCorr
+    B, H, W, r = 2, 17, 27, 4
+    f1, f2 = _fmaps(B, C, H, W, "cpu", seed=5)
+    if bf16:
+        f1, f2 = f1.bfloat16().float(), f2.bfloat16().float()
+    coords = _coords(B, H, W, "cpu", seed=9)
+    a1, a2 = f1.clone().requires_grad_(), f2.clone().requires_grad_()
+    want = ref.corr_onthefly(a1, a2, coords, r)
+    g = torch.randn_like(want)
+    (want * g).sum().backward()
+
+    dt = torch.bfloat16 if bf16 else torch.float32
+    b1 = f1.to(cuda, dt).contiguous(memory_format=torch.channels_last).requires_grad_()
+    b2 = f2.to(cuda, dt).contiguous(memory_format=torch.channels_last).requires_grad_()
+    blk = OnTheFlyCorr(b1, b2, 4, r)
+    got = blk(coords.to(cuda))
+    torch.testing.assert_close(got.float().cpu(), want.detach(), rtol=1e-4, atol=1e-3)
+    (got * g.to(cuda)).sum().backward()
+    tol = 2e-2 if bf16 else 1e-3
+    torch.testing.assert_close(b1.grad.float().cpu(), a1.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(b2.grad.float().cpu(), a2.grad, rtol=tol, atol=tol)
+
+
+def test_onthefly_matches_allpairs(cuda):
+    """pyramid[l] == corr(f1, avgpool^l f2): both paths agree."""
+    from raft_stir_amd.ops.corr import OnTheFlyCorr, AllPairsCorr
+    B, C, H, W = 1, 256, 24, 32
+    f1, f2 = _fmaps(B, C, H, W, cuda, seed=11)
+    coords = _coords(B, H, W, cuda, seed=12)
+    a = AllPairsCorr(f1, f2, 4, 4)(coords)
+    b = OnTheFlyCorr(f1, f2, 4, 4)(coords)
+    torch.testing.assert_close(a.float(), b.float(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("mask_bf16", [False, True])
+def test_convex_upsample(cuda, mask_bf16):
+    from raft_stir_amd.ops.upsample import convex_upsample
+    N, H, W = 2, 7, 11
+    g = torch.Generator().manual_seed(0)
+    flow = torch.randn(N, 2, H, W, generator=g) * 3
+    mask = torch.randn(N, 576, H, W, generator=g)
+    if mask_bf16:
+        mask = mask.bfloat16().float()
+    fa, ma = flow.clone().requires_grad_(), mask.clone().requires_grad_()
+    want = ref.convex_upsample(fa, ma)
+    gout = torch.randn_like(want)
+    (want * gout).sum().backward()
+
+    dt = torch.bfloat16 if mask_bf16 else torch.float32
+    fb = flow.to(cuda).requires_grad_()
+    mb = mask.to(cuda, dt).contiguous(memory_format=torch.channels_last).requires_grad_()
+    got = convex_upsample(fb, mb)
+    torch.testing.assert_close(got.cpu(), want.detach(), rtol=1e-4, atol=1e-4)
+    (got * gout.to(cuda)).sum().backward()
+    torch.testing.assert_close(fb.grad.cpu(), fa.grad, rtol=1e-4, atol=1e-3)
+    tol = 3e-2 if mask_bf16 else 1e-4
+    torch.testing.assert_close(mb.grad.float().cpu(), ma.grad, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("sep", [True, False])
+def test_fused_gru_pass(cuda, sep):
+    from raft_stir_amd.models.update import ConvGRU, SepConvGRU, _gru_step_reference
+    torch.manual_seed(0)
+    hd, cin = (128, 256) if sep else (96, 146)
+    mod = (SepConvGRU if sep else ConvGRU)(hidden_dim=hd, input_dim=cin)
+    B, H, W = 2, 9, 13
+    h = torch.tanh(torch.randn(B, hd, H, W))
+    x = torch.randn(B, cin, H, W)
+
+    ha, xa = h.clone().requires_grad_(), x.clone().requires_grad_()
+    mod.fused = False
+    out_ref = mod(ha, xa)
+    gout = torch.randn_like(out_ref)
+    (out_ref * gout).sum().backward()
+    ref_grads = {n: p.grad.clone() for n, p in mod.named_parameters()}
+    mod.zero_grad()
+
+    m2 = mod.to(cuda).to(memory_format=torch.channels_last)
+    m2.fused = True
+    hb = h.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    xb = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    out = m2(hb, xb)
+    torch.testing.assert_close(out.cpu(), out_ref.detach(), rtol=1e-4, atol=1e-4)
+    (out * gout.to(cuda)).sum().backward()
+    torch.testing.assert_close(hb.grad.cpu(), ha.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(xb.grad.cpu(), xa.grad, rtol=1e-3, atol=1e-3)
+    for n, p in m2.named_parameters():
+        torch.testing.assert_close(p.grad.cpu(), ref_grads[n], rtol=1e-3, atol=2e-3)

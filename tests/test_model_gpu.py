@@ -1,0 +1,84 @@
+"""End-to-end model on the GPU (HIP path) vs the CPU ATen oracle."""
+import copy
+
+import pytest
+import torch
+
+from raft_stir_amd.config import make_args
+from raft_stir_amd.models import RAFT
+
+pytestmark = pytest.mark.gpu
+
+
+def _imgs(B, H, W, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, 3, H, W, generator=g) * 255, torch.rand(B, 3, H, W, generator=g) * 255
+
+
+@pytest.mark.parametrize("small", [False, True])
+@pytest.mark.parametrize("alt", [False, True])
+def test_inference_fp32_matches_cpu(cuda, small, alt):
+    torch.manual_seed(0)
+    cpu = RAFT(make_args(small=small, alternate_corr=alt)).eval()
+    gpu = copy.deepcopy(cpu).to(cuda).to(memory_format=torch.channels_last).eval()
+    i1, i2 = _imgs(1, 128, 192)
+    with torch.no_grad():
+        lo_c, up_c = cpu(i1, i2, iters=6, test_mode=True)
+        lo_g, up_g = gpu(i1.to(cuda), i2.to(cuda), iters=6, test_mode=True)
+    # MIOpen conv algorithms differ from CPU in summation order; the recurrent
+    # loop amplifies fp32 noise a little.
+    torch.testing.assert_close(lo_g.cpu(), lo_c, atol=2e-2, rtol=1e-3)
+    torch.testing.assert_close(up_g.cpu(), up_c, atol=5e-2, rtol=1e-3)
+
+
+def test_bf16_inference_close_to_fp32(cuda):
+    torch.manual_seed(0)
+    m32 = RAFT(make_args()).to(cuda).to(memory_format=torch.channels_last).eval()
+    mbf = copy.deepcopy(m32)
+    mbf.cfg = mbf.cfg.__class__(**{**mbf.cfg.to_dict(), "mixed_precision": True})
+    i1, i2 = _imgs(1, 192, 256, seed=1)
+    i1, i2 = i1.to(cuda), i2.to(cuda)
+    with torch.no_grad():
+        _, a = m32(i1, i2, iters=12, test_mode=True)
+        _, b = mbf(i1, i2, iters=12, test_mode=True)
+    err = (a - b).norm(dim=1).mean().item()
+    mag = a.norm(dim=1).mean().item()
+    assert err < 0.05 * max(mag, 1.0), (err, mag)
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_training_grads_match_cpu(cuda, small):
+    torch.manual_seed(0)
+    cpu = RAFT(make_args(small=small)).train()
+    gpu = copy.deepcopy(cpu).to(cuda).to(memory_format=torch.channels_last).train()
+    i1, i2 = _imgs(2, 96, 128, seed=2)
+    gt = torch.randn(2, 2, 96, 128) * 4
+    preds = cpu(i1, i2, iters=3)
+    loss_c = sum((p - gt).abs().mean() for p in preds)
+    loss_c.backward()
+    preds_g = gpu(i1.to(cuda), i2.to(cuda), iters=3)
+    loss_g = sum((p - gt.to(cuda)).abs().mean() for p in preds_g)
+    loss_g.backward()
+    torch.testing.assert_close(loss_g.cpu(), loss_c.detach(), rtol=1e-3, atol=1e-3)
+    gc = torch.cat([p.grad.flatten() for p in cpu.parameters()])
+    gg = torch.cat([p.grad.flatten().cpu() for p in gpu.parameters()])
+    cos = torch.nn.functional.cosine_similarity(gc, gg, dim=0).item()
+    assert cos > 0.999, cos
+    assert (gc - gg).norm() / gc.norm() < 2e-2
+
+
+def test_graphed_inference_matches_eager(cuda):
+    from raft_stir_amd.runtime.graph import GraphedInference
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).eval()
+    i1, i2 = _imgs(1, 128, 256, seed=3)
+    i1, i2 = i1.to(cuda), i2.to(cuda)
+    with torch.no_grad():
+        lo, up = m(i1, i2, iters=8, test_mode=True)
+    g = GraphedInference(m, i1.shape, iters=8)
+    lo2, up2 = g(i1, i2)
+    torch.testing.assert_close(up2, up, atol=1e-3, rtol=1e-3)
+    lo3, up3 = g(i2, i1)  # replay with new inputs
+    with torch.no_grad():
+        _, upe = m(i2, i1, iters=8, test_mode=True)
+    torch.testing.assert_close(up3, upe, atol=1e-3, rtol=1e-3)
