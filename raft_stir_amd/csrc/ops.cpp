@@ -7,8 +7,8 @@
 // stream, so the ops compose with torch streams and hipGraph capture.
 
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include <cmath>
@@ -59,7 +59,7 @@ namespace {
 
 using at::Tensor;
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 void check_gpu(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -94,7 +94,7 @@ std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t leve
   const int H2 = f2.size(1), W2 = f2.size(2);
   TORCH_CHECK(f2.size(0) == B && f2.size(3) == C, "f1/f2 batch/channel mismatch");
   TORCH_CHECK(C % (is_bf16(f1) ? 64 : 32) == 0, "channels must be a multiple of 64 (bf16) / 32");
-  c10::hip::HIPGuard guard(f1.device());
+  const c10::DeviceGuard guard(f1.device());
   int Hs[4], Ws[4];
   level_sizes(H2, W2, levels, Hs, Ws);
   for (int l = 0; l < levels; ++l) TORCH_CHECK(Hs[l] > 0 && Ws[l] > 0, "pyramid level ", l, " is empty");
@@ -135,7 +135,7 @@ Tensor corr_lookup(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t
   int Hs[4], Ws[4];
   check_pyr(pyr, B, H1 * W1, Hs, Ws);
   TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
-  c10::hip::HIPGuard guard(coords.device());
+  const c10::DeviceGuard guard(coords.device());
   const int levels = pyr.size();
   const int D = 2 * radius + 1;
   Tensor out = at::empty({B, H1, W1, levels * D * D},
@@ -160,7 +160,7 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
   TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
                   dout.size(3) == levels * D * D,
               "dout must be (B,H1,W1,levels*(2r+1)^2)");
-  c10::hip::HIPGuard guard(coords.device());
+  const c10::DeviceGuard guard(coords.device());
   float* ptrs[4];
   for (int l = 0; l < levels; ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
@@ -172,7 +172,7 @@ void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
   const int B = gpyr[0].size(0), N1 = gpyr[0].size(1);
   int Hs[4], Ws[4];
   check_pyr(gpyr, B, N1, Hs, Ws);
-  c10::hip::HIPGuard guard(gpyr[0].device());
+  const c10::DeviceGuard guard(gpyr[0].device());
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
@@ -205,7 +205,7 @@ Tensor corr_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& c
   int Hs[4], Ws[4];
   check_otf(f1, f2, coords, Hs, Ws);
   TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
-  c10::hip::HIPGuard guard(f1.device());
+  const c10::DeviceGuard guard(f1.device());
   const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
   const int levels = f2.size(), D = 2 * radius + 1;
   Tensor out = at::empty({B, H1, W1, levels * D * D},
@@ -223,7 +223,7 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
                                       const Tensor& dout) {
   int Hs[4], Ws[4];
   check_otf(f1, f2, coords, Hs, Ws);
-  c10::hip::HIPGuard guard(f1.device());
+  const c10::DeviceGuard guard(f1.device());
   const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
   const int levels = f2.size(), D = 2 * radius + 1;
   check_gpu(dout, "dout");
@@ -257,7 +257,7 @@ Tensor convex_upsample(const Tensor& flow, const Tensor& mask) {
   TORCH_CHECK(mask.dim() == 4 && mask.size(0) == N && mask.size(1) == H && mask.size(2) == W &&
                   mask.size(3) == 576,
               "mask must be channels-last (N,H,W,576)");
-  c10::hip::HIPGuard guard(flow.device());
+  const c10::DeviceGuard guard(flow.device());
   Tensor out = at::empty({N, 2, 8 * H, 8 * W}, flow.options());
   rs::convex_up_fwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), N, H, W,
                            out.data_ptr<float>(), cur_stream());
@@ -275,7 +275,7 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
   TORCH_CHECK(dup.dim() == 4 && dup.size(0) == N && dup.size(1) == 2 && dup.size(2) == 8 * H &&
                   dup.size(3) == 8 * W,
               "grad must be (N,2,8H,8W)");
-  c10::hip::HIPGuard guard(flow.device());
+  const c10::DeviceGuard guard(flow.device());
   Tensor dflow = at::empty_like(flow);
   Tensor dmask = at::empty_like(mask);
   Tensor partial = at::empty({(int64_t)N * H * W * 18}, flow.options());
@@ -299,7 +299,7 @@ std::vector<Tensor> gru_gate_zr(const Tensor& zr, const Tensor& h, const Tensor&
   const int hd = h.size(-1), cin = x.size(-1);
   const int64_t P = pixels(h);
   TORCH_CHECK(zr.size(-1) == 2 * hd && pixels(zr) == P && pixels(x) == P, "gru_gate_zr: shapes");
-  c10::hip::HIPGuard guard(h.device());
+  const c10::DeviceGuard guard(h.device());
   auto sz = h.sizes().vec();
   Tensor z = at::empty_like(h), r = at::empty_like(h);
   sz.back() = hd + cin;
@@ -316,7 +316,7 @@ std::vector<Tensor> gru_gate_q(const Tensor& q, const Tensor& z, const Tensor& h
   TORCH_CHECK(q.sizes() == h.sizes() && z.sizes() == h.sizes(), "gru_gate_q: shapes");
   TORCH_CHECK(q.scalar_type() == h.scalar_type() && z.scalar_type() == h.scalar_type(),
               "gru_gate_q: dtype mismatch");
-  c10::hip::HIPGuard guard(h.device());
+  const c10::DeviceGuard guard(h.device());
   Tensor hn = at::empty_like(h), qt = at::empty_like(h);
   rs::gru_gate_q_launch(is_bf16(h), q.data_ptr(), z.data_ptr(), h.data_ptr(), pixels(h),
                         h.size(-1), hn.data_ptr(), qt.data_ptr(), cur_stream());
@@ -331,7 +331,7 @@ std::vector<Tensor> gru_bwd_q(const Tensor& dhn, const Tensor& z, const Tensor& 
   check_gpu(qt, "qt");
   TORCH_CHECK(dhn.sizes() == h.sizes() && z.sizes() == h.sizes() && qt.sizes() == h.sizes(),
               "gru_bwd_q: shapes");
-  c10::hip::HIPGuard guard(h.device());
+  const c10::DeviceGuard guard(h.device());
   const int hd = h.size(-1);
   const int64_t P = pixels(h);
   auto sz = h.sizes().vec();
@@ -355,7 +355,7 @@ void gru_bwd_r(const Tensor& drhx, const Tensor& h, const Tensor& r, const Tenso
   TORCH_CHECK(pixels(drhx) == P && dzr.size(-1) == 2 * hd && pixels(dzr) == P, "gru_bwd_r: shapes");
   TORCH_CHECK(drhx.scalar_type() == h.scalar_type() && dzr.scalar_type() == h.scalar_type(),
               "gru_bwd_r: dtype mismatch");
-  c10::hip::HIPGuard guard(h.device());
+  const c10::DeviceGuard guard(h.device());
   rs::gru_bwd_r_launch(is_bf16(h), drhx.data_ptr(), h.data_ptr(), r.data_ptr(), P, hd, cin,
                        dzr.data_ptr(), cur_stream());
 }
@@ -373,7 +373,7 @@ std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Ten
               "gru_bwd_fin: shapes");
   TORCH_CHECK(drhx.scalar_type() == r.scalar_type() && dhx.scalar_type() == r.scalar_type(),
               "gru_bwd_fin: dtype mismatch");
-  c10::hip::HIPGuard guard(r.device());
+  const c10::DeviceGuard guard(r.device());
   auto sz = r.sizes().vec();
   Tensor dh = at::empty_like(r);
   sz.back() = cin;

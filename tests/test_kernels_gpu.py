@@ -64,7 +64,7 @@ def test_corr_lookup_forward(cuda, r, out_bf16):
 def test_allpairs_corr_autograd(cuda, small):
     """Full chain (volume -> 3 lookups -> loss) gradient vs ATen autograd."""
     from raft_stir_amd.ops.corr import AllPairsCorr
-    B, C, H, W = 2, (128 if small else 256), 13, 21
+    B, C, H, W = 2, (128 if small else 256), 17, 21
     r = 3 if small else 4
     f1, f2 = _fmaps(B, C, H, W, "cpu", seed=3)
     coords = [_coords(B, H, W, "cpu", seed=s) for s in range(3)]
@@ -105,7 +105,9 @@ def test_onthefly_corr_fwd_bwd(cuda, C, bf16):
     b2 = f2.to(cuda, dt).contiguous(memory_format=torch.channels_last).requires_grad_()
     blk = OnTheFlyCorr(b1, b2, 4, r)
     got = blk(coords.to(cuda))
-    torch.testing.assert_close(got.float().cpu(), want.detach(), rtol=1e-4, atol=1e-3)
+    # bf16: the pooled f2 levels are stored in bf16 (rounding ~2^-9 relative)
+    ftol = 1e-2 if bf16 else 1e-4
+    torch.testing.assert_close(got.float().cpu(), want.detach(), rtol=ftol, atol=ftol)
     (got * g.to(cuda)).sum().backward()
     tol = 2e-2 if bf16 else 1e-3
     torch.testing.assert_close(b1.grad.float().cpu(), a1.grad, rtol=tol, atol=tol)
