@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--infer-reps", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
+    ap.add_argument("--reference-ops", action="store_true",
+                    help="A/B baseline: run the model on stock PyTorch-ROCm ops only "
+                         "(reference semantics: matmul volume, grid_sample lookup, unfused GRU)")
     return ap.parse_args()
 
 
@@ -57,6 +60,9 @@ def main():
     from raft_stir_amd.train.optim import fetch_optimizer
     from raft_stir_amd.data.synthetic import DevicePool
 
+    if a.reference_ops:
+        from raft_stir_amd.ops import _ext
+        _ext.reference_mode().__enter__()
     info = rdist.init_distributed()
     dev = torch.device("cuda", info.local_rank)
     torch.cuda.set_device(dev)
@@ -122,6 +128,7 @@ def main():
                 "image_size": [H, W],
                 "iters": a.iters,
                 "parallelism": f"dp{info.world_size}",
+                "ops": "stock-pytorch (reference semantics)" if a.reference_ops else "hip-kernels",
             },
             "final_loss": round(float(loss), 4),
             "inference": infer,

@@ -26,6 +26,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(os.path.dirname(PKG), "build", "hip")
 OUT = os.path.join(PKG, "_C.so")
+HOST_CSRC = os.path.join(PKG, "csrc_host")
+HOST_OUT = os.path.join(PKG, "_host.so")
 ARCH = os.environ.get("RAFT_STIR_ARCH", "gfx950")
 
 
@@ -120,6 +122,42 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
     return OUT
 
 
+def build_host(force: bool = False, debug: bool = False, verbose: bool = False) -> str:
+    """Build the CPU-only data-pipeline library ``_host.so`` (g++, zlib)."""
+    inc, lib, abi = _torch_paths()
+    srcs = sorted(os.path.join(HOST_CSRC, f) for f in os.listdir(HOST_CSRC) if f.endswith(".cpp"))
+    flags = ["-std=c++17", "-fPIC", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+             "-Wno-deprecated-declarations"] + (["-O0", "-g"] if debug else ["-O3"])
+    flags += [f"-I{p}" for p in inc]
+    h = hashlib.sha1(json.dumps(flags).encode())
+    for s in srcs:
+        with open(s, "rb") as f:
+            h.update(f.read())
+    stamp = os.path.join(BUILD, "_host.sha1")
+    os.makedirs(BUILD, exist_ok=True)
+    if not force and os.path.exists(HOST_OUT) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == h.hexdigest():
+                return HOST_OUT
+    cxx = shutil.which("g++") or shutil.which("c++")
+    tmp = HOST_OUT + ".tmp"
+    cmd = [cxx] + flags + srcs + [f"-L{lib}", "-ltorch_cpu", "-lc10", f"-Wl,-rpath,{lib}", "-lz",
+                                  "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"host build failed\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, HOST_OUT)
+    with open(stamp, "w") as f:
+        f.write(h.hexdigest())
+    return HOST_OUT
+
+
+def build_all(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = False):
+    return build(force, jobs, debug, verbose), build_host(force, debug, verbose)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
@@ -127,8 +165,7 @@ def main(argv=None):
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    path = build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose)
-    print(path)
+    print(build_all(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose))
 
 
 if __name__ == "__main__":
