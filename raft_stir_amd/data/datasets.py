@@ -15,8 +15,8 @@ Engine additions:
     defect B10 made the default split empty);
   * ``fetch_dataloader`` adds the ``synthetic`` stage (FlyingChairs-shaped
     generated pairs, used by benchmarks/tests since no dataset ships offline),
-    a DistributedSampler per rank under torch.distributed, pinned memory and
-    persistent workers for GPU training.
+    a rank-sharded resumable sampler (exact mid-epoch resume) and pinned
+    memory for GPU training.
 """
 from __future__ import annotations
 
@@ -253,6 +253,41 @@ def build_train_dataset(args, TRAIN_DS="C+T+K+S+H"):
     raise ValueError(f"unknown stage {args.stage!r}")
 
 
+class ResumableSampler(data.Sampler):
+    """Shuffled, rank-sharded, *resumable* sampler.
+
+    The permutation of epoch ``e`` is drawn from ``Generator(seed + e)``, so it
+    is identical on every rank and after a restart; rank ``r`` takes every
+    ``world_size``-th index (drop_last semantics), and :meth:`set_position`
+    skips the batches already consumed in the current epoch -- a resumed run
+    sees exactly the samples the uninterrupted run would have.
+    """
+
+    def __init__(self, dataset, rank=0, world_size=1, seed=0, batch_size=1):
+        self.n = len(dataset)
+        self.rank, self.world_size, self.seed = rank, world_size, seed
+        self.batch_size = batch_size
+        self.per_rank = self.n // world_size
+        self.epoch = 0
+        self.skip = 0
+
+    def set_epoch(self, epoch):
+        self.epoch = epoch
+
+    def set_position(self, epoch, batches_done):
+        self.epoch, self.skip = epoch, batches_done * self.batch_size
+
+    def __iter__(self):
+        g = torch.Generator().manual_seed(self.seed + self.epoch)
+        perm = torch.randperm(self.n, generator=g)[: self.per_rank * self.world_size]
+        mine = perm[self.rank::self.world_size].tolist()
+        skip, self.skip = self.skip, 0
+        return iter(mine[skip:])
+
+    def __len__(self):
+        return self.per_rank
+
+
 def fetch_dataloader(args, TRAIN_DS="C+T+K+S+H", rank=None, world_size=None, pin_memory=None):
     """Per-stage DataLoader (reference core/datasets.py:199-234).
 
@@ -265,16 +300,14 @@ def fetch_dataloader(args, TRAIN_DS="C+T+K+S+H", rank=None, world_size=None, pin
     if rank is None:
         rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
     per_rank = max(1, args.batch_size // world_size)
-    sampler = None
-    if world_size > 1:
-        sampler = data.distributed.DistributedSampler(train_dataset, num_replicas=world_size,
-                                                      rank=rank, shuffle=True, drop_last=True)
+    sampler = ResumableSampler(train_dataset, rank=rank, world_size=world_size,
+                               seed=int(getattr(args, "seed", 1234)), batch_size=per_rank)
     workers = int(getattr(args, "num_workers", 4))
     if pin_memory is None:
         pin_memory = torch.cuda.is_available()
     loader = data.DataLoader(train_dataset, batch_size=per_rank, pin_memory=pin_memory,
-                             shuffle=sampler is None, sampler=sampler, num_workers=workers,
-                             drop_last=True, persistent_workers=workers > 0)
+                             sampler=sampler, num_workers=workers, drop_last=True,
+                             persistent_workers=False)
     if rank == 0:
         print("Training with %d image pairs" % len(train_dataset))
     return loader

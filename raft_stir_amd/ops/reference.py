@@ -83,7 +83,7 @@ def corr_lookup(pyramid: List[torch.Tensor], coords, radius: int):
         # sampled: (BHW, 1, 2r+1 [rows of grid = dx], 2r+1 [cols = dy])
         outs.append(sampled.reshape(B, H, W, -1))
     out = torch.cat(outs, dim=-1)
-    return out.permute(0, 3, 1, 2).contiguous().float()
+    return out.permute(0, 3, 1, 2).contiguous()
 
 
 def corr_onthefly(fmap1, fmap2, coords, radius: int, num_levels: int = 4):

@@ -1,0 +1,100 @@
+"""Training runtime on CPU: the full train() loop (synthetic stage), reference
+checkpoint names, exact resume after an injected fault, non-finite skipping,
+optimizer/schedule parity with the reference hyper-parameters."""
+import os
+
+import pytest
+import torch
+
+from raft_stir_amd.train import checkpoint as ckpt
+from raft_stir_amd.train import trainer
+
+BASE = ["--device", "cpu", "--stage", "synthetic", "--small", "--iters", "2", "--image_size", "128", "128",
+        "--batch_size", "2", "--num_workers", "0", "--lr", "0.0004", "--wdecay", "0.0001",
+        "--synthetic_length", "6", "--sum_freq", "2", "--val_freq", "3"]
+
+
+def _run(tmp_path, name, extra):
+    argv = BASE + ["--name", name, "--ckpt_dir", str(tmp_path / "ck"), "--log_dir", str(tmp_path / "logs")] + extra
+    return trainer.main(argv)
+
+
+def test_train_loop_checkpoints_and_logs(tmp_path):
+    path = _run(tmp_path, "t1", ["--num_steps", "4"])
+    ck = tmp_path / "ck"
+    assert os.path.exists(path) and (ck / "3_t1.pth").exists() and (ck / "t1_resume_3.pt").exists()
+    sd = torch.load(path, weights_only=True)
+    assert all(k.startswith("module.") for k in sd) and len(sd) == 106
+    lines = open(tmp_path / "logs" / "metrics.jsonl").read().strip().splitlines()
+    assert lines and '"epe"' in lines[0] and '"pairs_per_s"' in lines[0]
+
+
+def test_resume_after_fault_is_exact(tmp_path):
+    ref_path = _run(tmp_path / "a", "run", ["--num_steps", "5"])
+    with pytest.raises(trainer.InjectedFault):
+        _run(tmp_path / "b", "run", ["--num_steps", "5", "--fault_at_step", "4"])
+    assert ckpt.latest_resume(str(tmp_path / "b" / "ck"), "run").endswith("run_resume_3.pt")
+    res_path = _run(tmp_path / "b", "run", ["--num_steps", "5", "--resume", "auto"])
+    a = torch.load(ref_path, weights_only=True)
+    b = torch.load(res_path, weights_only=True)
+    for k in a:
+        torch.testing.assert_close(b[k], a[k], atol=0, rtol=0, msg=k)
+
+
+def test_resume_file_contents(tmp_path):
+    from raft_stir_amd.config import make_args
+    from raft_stir_amd.models import RAFT
+    from raft_stir_amd.train.optim import fetch_optimizer
+    import argparse
+    m = RAFT(make_args(small=True))
+    opt, sch = fetch_optimizer(argparse.Namespace(lr=1e-3, wdecay=1e-4, epsilon=1e-8, num_steps=50), m)
+    for _ in range(3):
+        opt.zero_grad()
+        sum(p.sum() for p in m.parameters()).backward()
+        opt.step()
+        sch.step()
+    p = str(tmp_path / "x_resume_3.pt")
+    ckpt.save_resume(p, m, opt, sch, step=3, extra={"epoch": 1, "batch": 2})
+    m2 = RAFT(make_args(small=True))
+    opt2, sch2 = fetch_optimizer(argparse.Namespace(lr=1e-3, wdecay=1e-4, epsilon=1e-8, num_steps=50), m2)
+    obj = ckpt.load_resume(p, m2, opt2, sch2)
+    assert obj["step"] == 3 and obj["extra"] == {"epoch": 1, "batch": 2}
+    assert sch2.get_last_lr() == sch.get_last_lr()
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+
+
+def test_onecycle_matches_reference_schedule():
+    import argparse
+    from raft_stir_amd.config import make_args
+    from raft_stir_amd.models import RAFT
+    from raft_stir_amd.train.optim import fetch_optimizer
+    m = RAFT(make_args(small=True))
+    args = argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=1000)
+    opt, sch = fetch_optimizer(args, m)
+    ref_opt = torch.optim.AdamW(m.parameters(), lr=4e-4, weight_decay=1e-4, eps=1e-8)
+    ref = torch.optim.lr_scheduler.OneCycleLR(ref_opt, 4e-4, 1100, pct_start=0.05,
+                                              cycle_momentum=False, anneal_strategy="linear")
+    for _ in range(200):
+        assert abs(sch.get_last_lr()[0] - ref.get_last_lr()[0]) < 1e-12
+        opt.step(); sch.step(); ref_opt.step(); ref.step()
+    assert opt.param_groups[0]["weight_decay"] == 1e-4 and opt.param_groups[0]["eps"] == 1e-8
+
+
+def test_nonfinite_step_skipped_on_cpu(tmp_path, monkeypatch):
+    """A NaN loss must not corrupt the weights: the optimizer step is skipped."""
+    from raft_stir_amd.train import loss as loss_mod
+    calls = {"n": 0}
+    real = loss_mod.sequence_loss
+
+    def poisoned(*a, **k):
+        l, m = real(*a, **k)
+        calls["n"] += 1
+        return (l * float("nan") if calls["n"] == 2 else l), m
+
+    monkeypatch.setattr(trainer, "sequence_loss", poisoned)
+    path = _run(tmp_path, "nan", ["--num_steps", "3", "--max_skips", "5"])
+    sd = torch.load(path, weights_only=True)
+    assert all(torch.isfinite(v).all() for v in sd.values() if v.is_floating_point())
+    lines = open(tmp_path / "logs" / "metrics.jsonl").read()
+    assert '"skipped": 1.0' in lines
