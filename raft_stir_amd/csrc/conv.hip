@@ -1,0 +1,371 @@
+// Fused implicit-GEMM convolution for the RAFT update block (bf16 MFMA, NHWC).
+//
+// The reference update operator (core/update.py:6-136) is ~13 small
+// convolutions per refinement iteration glued together by cat / sigmoid /
+// tanh / relu / mul / add kernels.  Here every one of them is ONE launch of
+// this kernel:
+//
+//   out[p, co] = epilogue( bias[co] + sum_{tap, ci} X[p + tap, ci] * W[co, tap, ci] )
+//
+// * GEMM orientation: M = output channels (A = packed weights), N = pixels
+//   (B = implicit im2col of the NHWC input), K = taps x input channels.
+//   mfma_f32_16x16x32_bf16 fragments are 16-byte K-runs for both operands:
+//   A: W[co][tap][k0 + 8*(lane>>4) .. +7], B: X[pixel'][k0 + 8*(lane>>4) .. +7]
+//   -- channels-last rows, so no im2col buffer and no LDS transpose.
+// * The input is up to 3 channel SEGMENTS, each a (base, channel count,
+//   row stride) view, so concatenations (cat[h, x], cat[r*h, x],
+//   cat[inp, motion, flow]) are never materialised: the producer kernels
+//   write straight into slices of shared NHWC buffers.
+// * Zero padding ("same" convolutions, stride 1) by predicated loads.
+// * Epilogues fuse what the reference does in separate kernels:
+//   bias, ReLU, scale (mask x0.25), the ConvGRU gates (z, r*h) and the GRU
+//   update h' = (1-z) h + z tanh(q), and the coords update coords += delta.
+// * Register double-buffered fragment loads (step k+1 issued before the
+//   MFMAs of step k); weights are tiny and L1/L2-resident.
+//
+// Weights are packed on the host (ops/conv.py) into [Cout_pad][taps][Ktot]
+// bf16, Ktot = sum of the segment channel counts (each a multiple of 32),
+// with zeros for padding channels, so the K loop needs no bounds checks.
+#include "common.h"
+
+namespace rs {
+namespace conv {
+
+enum Epi : int {
+  EPI_BIAS = 0,
+  EPI_RELU = 1,
+  EPI_SCALE = 2,   // (acc + b) * scale
+  EPI_GRU_ZR = 3,  // co < hd: z -> out ; co >= hd: r*h -> out2 (r -> out3 if set)
+  EPI_GRU_Q = 4,   // h' = (1-z) h + z tanh(acc + b) -> out (q~ -> out2 if set)
+  EPI_FLOW = 5,    // coords (fp32 NCHW) += acc + b   (co < 2)
+};
+
+struct Seg {
+  const bf16_t* ptr;
+  int C;       // channels read (multiple of 32)
+  int stride;  // row stride in elements (multiple of 8)
+};
+
+struct Args {
+  Seg seg[3];
+  int nseg;
+  const bf16_t* w;  // [Cout_pad][taps][Ktot]
+  const float* bias;
+  int B, H, W, P;
+  int KH, KW, PH, PW;
+  int Cout, Ktot;
+  int epi;
+  float scale;
+  int hd;
+  // outputs (element strides/offsets)
+  void* out;
+  int ostr, ooff;
+  void* out2;
+  int o2str, o2off;
+  void* out3;
+  int o3str, o3off;
+  // aux inputs (bf16 NHWC)
+  const bf16_t* aux1;  // h
+  int a1str, a1off;
+  const bf16_t* aux2;  // z
+  int a2str, a2off;
+};
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+template <int WM, int WN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_kernel(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int m0 = (blockIdx.y * WAVES_M + wm) * WM * 16;  // first output channel of this wave
+  const int n0 = (blockIdx.x * WAVES_N + wn) * WN * 16;  // first pixel of this wave
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int taps = a.KH * a.KW;
+  const int HW = a.H * a.W;
+
+  // pixel coordinates of this lane's B columns
+  int pb[WN], py[WN], px[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int p = n0 + nt * 16 + lr;
+    if (p < a.P) {
+      pb[nt] = p / HW;
+      const int q = p - pb[nt] * HW;
+      py[nt] = q / a.W;
+      px[nt] = q - py[nt] * a.W;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = 0;
+    }
+  }
+  // weight row pointers of this lane's A rows
+  const bf16_t* wrow[WM];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+    wrow[mt] = a.w + (size_t)(m0 + mt * 16 + lr) * taps * a.Ktot + lk;
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // flattened K steps: (segment, tap, 32-channel chunk).  Segment fields are
+  // selected with wave-uniform compares (no dynamic indexing of the kernarg
+  // array, which would go through scratch).
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const int e1 = taps * (s0.C >> 5);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 5) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 5) : 0);
+
+  // plain locals: a lambda capturing the byval kernarg struct by reference
+  // would force a copy of it into scratch.
+  const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+#define RS_CONV_LOAD(STEP, FA, FB)                                                           \
+  do {                                                                                       \
+    const int step_ = (STEP);                                                                \
+    const int si = (step_ >= e1) + (step_ >= e2);                                            \
+    const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);                       \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                 \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                 \
+    const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);                           \
+    const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                          \
+    const int chunks = sC >> 5;                                                              \
+    const int tap = local / chunks;                                                          \
+    const int c0 = (local - tap * chunks) * 32;                                              \
+    const int dy = tap / KW - PH, dx = tap % KW - PW;                                        \
+    _Pragma("unroll") for (int mt = 0; mt < WM; ++mt)                                        \
+      FA[mt] = ld16(wrow[mt] + (size_t)tap * Ktot + kseg + c0);                              \
+    _Pragma("unroll") for (int nt = 0; nt < WN; ++nt) {                                      \
+      const int yy = py[nt] + dy, xx = px[nt] + dx;                                          \
+      const bool ok = pb[nt] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;                 \
+      FB[nt] = ok ? ld16(sp + ((size_t)(pb[nt] * H + yy) * W + xx) * sst + c0 + lk) : zero;  \
+    }                                                                                        \
+  } while (0)
+
+#define RS_CONV_MMA(FA, FB)                                                                       \
+  _Pragma("unroll") for (int mt = 0; mt < WM; ++mt)                                               \
+    _Pragma("unroll") for (int nt = 0; nt < WN; ++nt)                                             \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                                      \
+          __builtin_bit_cast(bf16x8_t, FA[mt]), __builtin_bit_cast(bf16x8_t, FB[nt]), acc[mt][nt], \
+          0, 0, 0)
+
+  uint4 fa0[WM], fb0[WN], fa1[WM], fb1[WN];
+  RS_CONV_LOAD(0, fa0, fb0);
+  int step = 0;
+  for (; step + 2 <= nsteps; step += 2) {
+    RS_CONV_LOAD(step + 1, fa1, fb1);
+    RS_CONV_MMA(fa0, fb0);
+    if (step + 2 < nsteps) RS_CONV_LOAD(step + 2, fa0, fb0);
+    RS_CONV_MMA(fa1, fb1);
+  }
+  if (step < nsteps) {
+    RS_CONV_MMA(fa0, fb0);
+  }
+#undef RS_CONV_LOAD
+#undef RS_CONV_MMA
+
+  // ------------------------------------------------------------ epilogue
+  const int cq = (lane >> 4) * 4;
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    if (pb[nt] < 0) continue;
+    const int p = n0 + nt * 16 + lr;
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt) {
+      const int cb = m0 + mt * 16 + cq;
+      if (cb >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
+      const bool full = cb + 3 < a.Cout;
+      switch (a.epi) {
+        case EPI_FLOW: {
+          float* crd = static_cast<float*>(a.out);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = cb + j;
+            if (co < a.Cout && co < 2) {
+              float* d = crd + ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
+              *d += v[j];
+            }
+          }
+          break;
+        }
+        case EPI_GRU_ZR: {
+          if (cb < a.hd) {
+            bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
+          } else {
+            const int c = cb - a.hd;
+            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
+            bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
+            bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float r = sigmoidf_(v[j]);
+              rh[j] = f2bf(r * bf2f(h[j]));
+              if (rs_) rs_[j] = f2bf(r);
+            }
+          }
+          break;
+        }
+        case EPI_GRU_Q: {
+          const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+          const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+          bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+          bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
+          float hv[4], zv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hv[j] = bf2f(h[j]);
+            zv[j] = bf2f(z[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float q = tanhf_(v[j]);
+            hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
+            if (qs) qs[j] = f2bf(q);
+          }
+          break;
+        }
+        default: {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (a.epi == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+            else if (a.epi == EPI_SCALE) v[j] *= a.scale;
+          }
+          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+          if (full && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
+            uint2 pk;
+            pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+            pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+            *reinterpret_cast<uint2*>(o) = pk;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (cb + j < a.Cout) o[j] = f2bf(v[j]);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ flow encoder
+// convf1 of the motion encoder (reference core/update.py:67,84): a 7x7 conv
+// of the 2-channel flow (= coords1 - coords0, computed here from coords1)
+// with ReLU, written as bf16 NHWC.  K = 98, so it is a VALU kernel: one
+// thread per (pixel, 8 output channels), the 7x7x2 flow window in registers.
+// It also writes the flow itself (bf16) into its slot of the GRU input
+// buffer (reference: cat([out, flow]) in the motion encoder).
+__global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__ coords, int B, int H,
+                                                       int W, const float* __restrict__ w,  // [49][2][Cout]
+                                                       const float* __restrict__ bias, int Cout,
+                                                       bf16_t* __restrict__ out, int ostr, int ooff,
+                                                       bf16_t* __restrict__ fout, int fstr, int foff) {
+  const int groups = Cout / 8;
+  const int HW = H * W;
+  const long total = (long)B * HW * groups;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % groups);
+    const long p = i / groups;
+    const int b = (int)(p / HW), q = (int)(p % HW), y = q / W, x = q % W;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = bias[g * 8 + j];
+    const float* cx = coords + (size_t)b * 2 * HW;
+    const float* cy = cx + HW;
+    for (int ky = 0; ky < 7; ++ky) {
+      const int yy = y + ky - 3;
+      if (yy < 0 || yy >= H) continue;
+      for (int kx = 0; kx < 7; ++kx) {
+        const int xx = x + kx - 3;
+        if (xx < 0 || xx >= W) continue;
+        const float fu = cx[yy * W + xx] - (float)xx;
+        const float fv = cy[yy * W + xx] - (float)yy;
+        const float* wt = w + ((ky * 7 + kx) * 2) * Cout + g * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += fu * wt[j] + fv * wt[Cout + j];
+      }
+    }
+    uint4 pk;
+    uint32_t u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      u[j] = uint32_t(f2bf(fmaxf(acc[2 * j], 0.f))) | (uint32_t(f2bf(fmaxf(acc[2 * j + 1], 0.f))) << 16);
+    pk = make_uint4(u[0], u[1], u[2], u[3]);
+    *reinterpret_cast<uint4*>(out + (size_t)p * ostr + ooff + g * 8) = pk;
+    if (g == 0 && fout) {
+      fout[(size_t)p * fstr + foff] = f2bf(cx[q] - (float)x);
+      fout[(size_t)p * fstr + foff + 1] = f2bf(cy[q] - (float)y);
+    }
+  }
+}
+
+}  // namespace conv
+
+// ------------------------------------------------------------------ launchers
+struct ConvLaunch {
+  const void* seg_ptr[3];
+  int seg_C[3], seg_stride[3];
+  int nseg;
+  const void* w;
+  const float* bias;
+  int B, H, W, KH, KW, PH, PW, Cout, Cout_pad, Ktot;
+  int epi;
+  float scale;
+  int hd;
+  void* out; int ostr, ooff;
+  void* out2; int o2str, o2off;
+  void* out3; int o3str, o3off;
+  const void* aux1; int a1str, a1off;
+  const void* aux2; int a2str, a2off;
+  int tile;  // 0: 32co x 32px per wave (2x2 waves); 1: 64co x 32px per wave
+};
+
+void conv_launch(const ConvLaunch& L, hipStream_t stream) {
+  conv::Args a{};
+  for (int s = 0; s < 3; ++s) {
+    a.seg[s].ptr = static_cast<const bf16_t*>(L.seg_ptr[s]);
+    a.seg[s].C = L.seg_C[s];
+    a.seg[s].stride = L.seg_stride[s];
+  }
+  a.nseg = L.nseg;
+  a.w = static_cast<const bf16_t*>(L.w);
+  a.bias = L.bias;
+  a.B = L.B; a.H = L.H; a.W = L.W; a.P = L.B * L.H * L.W;
+  a.KH = L.KH; a.KW = L.KW; a.PH = L.PH; a.PW = L.PW;
+  a.Cout = L.Cout; a.Ktot = L.Ktot;
+  a.epi = L.epi; a.scale = L.scale; a.hd = L.hd;
+  a.out = L.out; a.ostr = L.ostr; a.ooff = L.ooff;
+  a.out2 = L.out2; a.o2str = L.o2str; a.o2off = L.o2off;
+  a.out3 = L.out3; a.o3str = L.o3str; a.o3off = L.o3off;
+  a.aux1 = static_cast<const bf16_t*>(L.aux1); a.a1str = L.a1str; a.a1off = L.a1off;
+  a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
+  if (L.tile == 1) {
+    constexpr int WM = 4, WN = 2, WAVES_M = 1, WAVES_N = 4;
+    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout_pad, WM * 16 * WAVES_M));
+    hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
+                       0, stream, a);
+  } else {
+    constexpr int WM = 2, WN = 2, WAVES_M = 1, WAVES_N = 4;
+    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout_pad, WM * 16 * WAVES_M));
+    hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
+                       0, stream, a);
+  }
+}
+
+void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
+                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
+                     hipStream_t stream) {
+  const long total = (long)B * H * W * (Cout / 8);
+  const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
+  hipLaunchKernelGGL(conv::flow_enc_kernel, dim3(grid), dim3(256), 0, stream, coords, B, H, W, w, bias,
+                     Cout, static_cast<bf16_t*>(out), ostr, ooff, static_cast<bf16_t*>(fout), fstr, foff);
+}
+
+}  // namespace rs

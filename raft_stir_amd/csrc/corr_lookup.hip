@@ -45,13 +45,18 @@ template <typename OutT>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(Pyr pyr, int levels,
                                                          const float* __restrict__ coords, int B,
                                                          int H1, int W1, int r,
-                                                         OutT* __restrict__ out, long total) {
+                                                         OutT* __restrict__ out, long total,
+                                                         int ostride) {
   const int D = 2 * r + 1, K2 = D * D, CH = levels * K2;
   const int N1 = H1 * W1;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int ch = (int)(idx % CH);
-    const long pix = idx / CH;  // b * N1 + n
+    const int ch = (int)(idx % ostride);
+    const long pix = idx / ostride;  // b * N1 + n
+    if (ch >= CH) {  // zero the channel padding of a padded (K-aligned) output row
+      io<OutT>::st(out + idx, 0.f);
+      continue;
+    }
     const int b = (int)(pix / N1), n = (int)(pix % N1);
     const int l = ch / K2, k = ch % K2;
     const int i = k / D, j = k % D;  // i: dx index, j: dy index
@@ -159,22 +164,24 @@ inline int grid_for(long total) {
 
 void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* Ws, int levels,
                             const float* coords, int B, int H1, int W1, int r, void* out,
-                            bool out_bf16, hipStream_t stream) {
+                            bool out_bf16, hipStream_t stream, int ostride) {
   lookup::Pyr p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? pyr[l] : nullptr;
     p.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = l < levels ? Ws[l] : 0;
   }
-  const long total = (long)B * H1 * W1 * levels * (2 * r + 1) * (2 * r + 1);
+  const int CH = levels * (2 * r + 1) * (2 * r + 1);
+  if (ostride <= 0) ostride = CH;
+  const long total = (long)B * H1 * W1 * ostride;
   if (total == 0) return;
   const int grid = lookup::grid_for(total);
   if (out_bf16)
     hipLaunchKernelGGL(lookup::lookup_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<bf16_t*>(out), total);
+                       levels, coords, B, H1, W1, r, static_cast<bf16_t*>(out), total, ostride);
   else
     hipLaunchKernelGGL(lookup::lookup_fwd_kernel<float>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<float*>(out), total);
+                       levels, coords, B, H1, W1, r, static_cast<float*>(out), total, ostride);
 }
 
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,

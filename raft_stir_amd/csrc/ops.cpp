@@ -22,7 +22,7 @@ void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1
                         float scale, hipStream_t stream);
 void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* Ws, int levels,
                             const float* coords, int B, int H1, int W1, int r, void* out,
-                            bool out_bf16, hipStream_t stream);
+                            bool out_bf16, hipStream_t stream, int ostride);
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream);
@@ -143,8 +143,31 @@ Tensor corr_lookup(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t
   const float* ptrs[4];
   for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
   rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
-                             out.data_ptr(), out_bf16, cur_stream());
+                             out.data_ptr(), out_bf16, cur_stream(), 0);
   return out;
+}
+
+// Lookup into a preallocated channels-last buffer whose rows may be wider than
+// levels*(2r+1)^2 (K-aligned for the fused conv); the padding is zeroed.
+void corr_lookup_into(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t radius,
+                      const Tensor& out) {
+  check_coords(coords);
+  const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
+  int Hs[4], Ws[4];
+  check_pyr(pyr, B, H1 * W1, Hs, Ws);
+  TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
+  const int levels = pyr.size();
+  const int D = 2 * radius + 1;
+  check_gpu(out, "out");
+  check_dtype(out, {at::kFloat, at::kBFloat16}, "out");
+  TORCH_CHECK(out.dim() == 4 && out.size(0) == B && out.size(1) == H1 && out.size(2) == W1 &&
+                  out.size(3) >= levels * D * D,
+              "out must be (B,H1,W1,>=levels*(2r+1)^2)");
+  const c10::DeviceGuard guard(coords.device());
+  const float* ptrs[4];
+  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
+  rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
+                             out.data_ptr(), is_bf16(out), cur_stream(), out.size(3));
 }
 
 void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords, int64_t radius,
@@ -388,6 +411,7 @@ std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Ten
 TORCH_LIBRARY(raft_stir, m) {
   m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale) -> Tensor[]");
   m.def("corr_lookup(Tensor[] pyr, Tensor coords, int radius, bool out_bf16) -> Tensor");
+  m.def("corr_lookup_into(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_lookup_backward(Tensor(a!)[] gpyr, Tensor coords, int radius, Tensor dout) -> ()");
   m.def("pyr_grad_fold(Tensor(a!)[] gpyr, float scale) -> ()");
   m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
@@ -404,6 +428,7 @@ TORCH_LIBRARY(raft_stir, m) {
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("corr_volume", &corr_volume);
   m.impl("corr_lookup", &corr_lookup);
+  m.impl("corr_lookup_into", &corr_lookup_into);
   m.impl("corr_lookup_backward", &corr_lookup_backward);
   m.impl("pyr_grad_fold", &pyr_grad_fold);
   m.impl("corr_otf", &corr_otf);

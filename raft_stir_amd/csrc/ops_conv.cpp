@@ -1,0 +1,169 @@
+// torch.ops.raft_stir.conv_fused / flow_encode: the fused update-block
+// convolution (csrc/conv.hip).  All shape, alignment and bounds checks happen
+// here on the host; the kernel assumes them.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+
+namespace rs {
+struct ConvLaunch {
+  const void* seg_ptr[3];
+  int seg_C[3], seg_stride[3];
+  int nseg;
+  const void* w;
+  const float* bias;
+  int B, H, W, KH, KW, PH, PW, Cout, Cout_pad, Ktot;
+  int epi;
+  float scale;
+  int hd;
+  void* out; int ostr, ooff;
+  void* out2; int o2str, o2off;
+  void* out3; int o3str, o3off;
+  const void* aux1; int a1str, a1off;
+  const void* aux2; int a2str, a2off;
+  int tile;
+};
+void conv_launch(const ConvLaunch& L, hipStream_t stream);
+void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
+                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
+                     hipStream_t stream);
+}  // namespace rs
+
+namespace {
+using at::Tensor;
+
+constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_nhwc(const Tensor& t, int B, int H, int W, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, n, ": contiguous NHWC GPU tensor required");
+  TORCH_CHECK(t.size(0) == B && t.size(1) == H && t.size(2) == W, n, ": spatial shape mismatch");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, ": bf16 required");
+}
+
+void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C,
+                const Tensor& w, const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t Cout,
+                int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
+                const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
+                int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
+                const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile) {
+  TORCH_CHECK(!segs.empty() && segs.size() <= 3, "conv_fused: 1..3 input segments");
+  TORCH_CHECK(seg_off.size() == segs.size() && seg_C.size() == segs.size(), "conv_fused: segment spec");
+  const int B = segs[0].size(0), H = segs[0].size(1), W = segs[0].size(2);
+  const c10::DeviceGuard guard(segs[0].device());
+  rs::ConvLaunch L{};
+  int Ktot = 0;
+  for (size_t s = 0; s < 3; ++s) {
+    if (s < segs.size()) {
+      check_nhwc(segs[s], B, H, W, "segment");
+      const int C = seg_C[s], off = seg_off[s], Cb = segs[s].size(3);
+      TORCH_CHECK(C > 0 && C % 32 == 0, "conv_fused: segment channels must be a positive multiple of 32");
+      TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb,
+                  "conv_fused: segment window out of bounds or misaligned");
+      L.seg_ptr[s] = static_cast<const at::BFloat16*>(segs[s].data_ptr()) + off;
+      L.seg_C[s] = C;
+      L.seg_stride[s] = Cb;
+      Ktot += C;
+    } else {
+      L.seg_ptr[s] = L.seg_ptr[0];
+      L.seg_C[s] = 32;
+      L.seg_stride[s] = L.seg_stride[0];
+    }
+  }
+  L.nseg = segs.size();
+  TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
+  const int tileM = tile == 1 ? 64 : 32;
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
+              "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
+  TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == Ktot, "conv_fused: packed weight K mismatch");
+  TORCH_CHECK(w.size(0) >= Cout && w.size(0) % tileM == 0, "conv_fused: Cout_pad must be a multiple of ", tileM);
+  if (bias) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() >= Cout &&
+                    bias->is_contiguous(),
+                "conv_fused: bias must be fp32 (Cout,)");
+  }
+  L.w = w.data_ptr();
+  L.bias = bias ? bias->data_ptr<float>() : nullptr;
+  L.B = B; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.PH = KH / 2; L.PW = KW / 2;
+  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;
+  L.epi = epi; L.scale = scale; L.hd = hd; L.tile = tile;
+  if (epi == EPI_FLOW) {
+    TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kFloat && out.dim() == 4 &&
+                    out.size(0) == B && out.size(1) == 2 && out.size(2) == H && out.size(3) == W,
+                "conv_fused(flow): out must be fp32 coords (B,2,H,W)");
+    TORCH_CHECK(Cout == 2, "conv_fused(flow): Cout must be 2");
+    L.out = out.data_ptr(); L.ostr = 0; L.ooff = 0;
+  } else {
+    check_nhwc(out, B, H, W, "out");
+    const int cw = epi == EPI_GRU_ZR ? hd : Cout;
+    TORCH_CHECK(ooff >= 0 && ooff + cw <= out.size(3), "conv_fused: output window out of bounds");
+    L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = ooff;
+  }
+  auto opt_nhwc = [&](const c10::optional<Tensor>& t, int64_t off, int width, const char* n, void** p,
+                      int* str, int* o) {
+    if (!t) { *p = nullptr; *str = 0; *o = 0; return; }
+    check_nhwc(*t, B, H, W, n);
+    TORCH_CHECK(off >= 0 && off + width <= t->size(3), "conv_fused: ", n, " window out of bounds");
+    *p = t->data_ptr(); *str = t->size(3); *o = off;
+  };
+  void* p;
+  if (epi == EPI_GRU_ZR) {
+    TORCH_CHECK(Cout == 2 * hd && hd % 4 == 0 && out2 && aux1, "conv_fused(gru_zr): needs Cout=2*hd, out2 (r*h), aux1 (h)");
+    opt_nhwc(out2, o2off, hd, "out2", &L.out2, &L.o2str, &L.o2off);
+    opt_nhwc(out3, o3off, hd, "out3", &L.out3, &L.o3str, &L.o3off);
+    opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
+  } else if (epi == EPI_GRU_Q) {
+    TORCH_CHECK(Cout % 4 == 0 && aux1 && aux2, "conv_fused(gru_q): needs aux1 (h) and aux2 (z)");
+    opt_nhwc(out2, o2off, Cout, "out2", &L.out2, &L.o2str, &L.o2off);
+    opt_nhwc(aux1, a1off, Cout, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
+    opt_nhwc(aux2, a2off, Cout, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
+  }
+  rs::conv_launch(L, stream());
+}
+
+// convf1 of the motion encoder from coords1 (flow = coords1 - grid), ReLU, bf16
+// NHWC into out[..., ooff:ooff+Cout]; the flow itself (bf16) into fout[..., foff:foff+2].
+void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, const Tensor& out, int64_t ooff,
+                 const c10::optional<Tensor>& fout, int64_t foff) {
+  TORCH_CHECK(coords.is_cuda() && coords.is_contiguous() && coords.scalar_type() == at::kFloat &&
+                  coords.dim() == 4 && coords.size(1) == 2,
+              "flow_encode: coords must be fp32 (B,2,H,W)");
+  const int B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  const int Cout = bias.numel();
+  TORCH_CHECK(Cout % 8 == 0, "flow_encode: Cout must be a multiple of 8");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.numel() == 98 * Cout,
+              "flow_encode: w must be fp32 [49][2][Cout]");
+  TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.is_contiguous(), "flow_encode: bias fp32");
+  check_nhwc(out, B, H, W, "out");
+  TORCH_CHECK(ooff % 8 == 0 && out.size(3) % 8 == 0 && ooff + Cout <= out.size(3), "flow_encode: out window");
+  void* fp = nullptr;
+  int fstr = 0;
+  if (fout) {
+    check_nhwc(*fout, B, H, W, "fout");
+    TORCH_CHECK(foff >= 0 && foff + 2 <= fout->size(3), "flow_encode: fout window");
+    fp = fout->data_ptr();
+    fstr = fout->size(3);
+  }
+  const c10::DeviceGuard guard(coords.device());
+  rs::flow_enc_launch(coords.data_ptr<float>(), B, H, W, w.data_ptr<float>(), bias.data_ptr<float>(), Cout,
+                      out.data_ptr(), out.size(3), ooff, fp, fstr, foff, stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("conv_fused(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, "
+        "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
+        "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile) -> ()");
+  m.def("flow_encode(Tensor coords, Tensor w, Tensor bias, Tensor(a!) out, int ooff, Tensor(b!)? fout, "
+        "int foff) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
+  m.impl("conv_fused", &conv_fused);
+  m.impl("flow_encode", &flow_encode);
+}

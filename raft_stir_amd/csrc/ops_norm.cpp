@@ -1,0 +1,128 @@
+// torch.ops.raft_stir.norm_* : fused NHWC normalisation + activation (csrc/norm.hip).
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+
+namespace rs {
+int norm_ws_floats(int B, int P, int C, bool bf16);
+void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, float eps, float* ws,
+                       float* mean, float* rstd, hipStream_t s);
+void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mean,
+                     const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
+                     int G, bool relu, void* y, hipStream_t s);
+void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, const float* mean,
+                     const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
+                     int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
+                     void* dres, hipStream_t s);
+}  // namespace rs
+
+namespace {
+using at::Tensor;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+// x: (B, H, W, C) contiguous (an NCHW-shaped channels_last tensor is passed as
+// its NHWC permute by the Python side).
+void check_x(const Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "norm: x must be contiguous (B,H,W,C) on GPU");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "norm: x must be fp32/bf16");
+  const int64_t C = x.size(3);
+  const int vn = x.scalar_type() == at::kBFloat16 ? 8 : 4;
+  TORCH_CHECK(C % vn == 0 && C / vn <= 256, "norm: channel count ", C, " unsupported");
+}
+
+void check_like(const c10::optional<Tensor>& t, const Tensor& x, const char* n) {
+  if (!t) return;
+  TORCH_CHECK(t->sizes() == x.sizes() && t->scalar_type() == x.scalar_type() && t->is_contiguous(),
+              "norm: ", n, " must match x");
+}
+
+void check_param(const c10::optional<Tensor>& t, int64_t C, const char* n) {
+  if (!t) return;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+              "norm: ", n, " must be fp32 (C,)");
+}
+
+const float* fptr(const c10::optional<Tensor>& t) { return t ? t->data_ptr<float>() : nullptr; }
+
+std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps) {
+  check_x(x);
+  const c10::DeviceGuard g(x.device());
+  const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
+  const int G = per_sample ? B : 1;
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
+  Tensor mean = at::empty({G, C}, fo), rstd = at::empty({G, C}, fo);
+  rs::norm_stats_launch(bf, x.data_ptr(), B, P, C, G, (float)eps, ws.data_ptr<float>(),
+                        mean.data_ptr<float>(), rstd.data_ptr<float>(), stream());
+  return {mean, rstd};
+}
+
+Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
+                const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+                const c10::optional<Tensor>& res, bool relu) {
+  check_x(x);
+  const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
+  const int G = mean.size(0);
+  TORCH_CHECK(mean.is_contiguous() && rstd.is_contiguous() && mean.numel() == (int64_t)G * C &&
+                  rstd.numel() == (int64_t)G * C && (G == 1 || G == B),
+              "norm_act: stats shape");
+  check_param(gamma, C, "gamma");
+  check_param(beta, C, "beta");
+  check_like(res, x, "residual");
+  const c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  rs::norm_fwd_launch(x.scalar_type() == at::kBFloat16, x.data_ptr(), res ? res->data_ptr() : nullptr,
+                      mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
+                      G, relu, y.data_ptr(), stream());
+  return y;
+}
+
+// returns dx, dres (empty if no residual), s1 (= dbeta per group), s2 (= dgamma per group).
+// batch_stats=false: the statistics were constants (BatchNorm in eval mode), so
+// dx = gamma * rstd * g without the mean/variance terms.
+std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const Tensor& mean,
+                                      const Tensor& rstd, const c10::optional<Tensor>& gamma,
+                                      const c10::optional<Tensor>& beta,
+                                      const c10::optional<Tensor>& res, bool relu,
+                                      bool batch_stats) {
+  check_x(x);
+  check_like(dy, x, "grad");
+  check_like(res, x, "residual");
+  const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
+  const int G = mean.size(0);
+  TORCH_CHECK(mean.numel() == (int64_t)G * C && rstd.numel() == (int64_t)G * C && (G == 1 || G == B),
+              "norm_act_backward: stats shape");
+  check_param(gamma, C, "gamma");
+  check_param(beta, C, "beta");
+  const c10::DeviceGuard g(x.device());
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
+  Tensor s1 = at::empty({G, C}, fo), s2 = at::empty({G, C}, fo);
+  Tensor dx = at::empty_like(x);
+  Tensor dres = res ? at::empty_like(x) : at::empty({0}, x.options());
+  rs::norm_bwd_launch(bf, x.data_ptr(), dy.data_ptr(), res ? res->data_ptr() : nullptr,
+                      mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
+                      G, relu, batch_stats, ws.data_ptr<float>(), s1.data_ptr<float>(),
+                      s2.data_ptr<float>(), dx.data_ptr(), res ? dres.data_ptr() : nullptr, stream());
+  return {dx, dres, s1, s2};
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("norm_stats(Tensor x, bool per_sample, float eps) -> Tensor[]");
+  m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu) -> Tensor");
+  m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, bool batch_stats) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
+  m.impl("norm_stats", &norm_stats);
+  m.impl("norm_act", &norm_act);
+  m.impl("norm_act_backward", &norm_act_backward);
+}

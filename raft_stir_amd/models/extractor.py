@@ -13,8 +13,11 @@ Parameter/buffer names are kept identical so reference ``.pth`` files load
 unchanged (including the aliased ``normK`` / ``downsample.1`` pair that the
 reference creates by registering the same norm module twice).
 
-MI355X notes: the encoders run once per image pair, so they go through
-MIOpen in channels_last (NHWC) bf16 under autocast; NHWC keeps the 1x1
+MI355X notes: the encoders run once per image pair; their convolutions go
+through MIOpen in channels_last (NHWC) bf16 under autocast, and every
+norm -> ReLU (-> residual add -> ReLU) chain is one fused NHWC pass of
+csrc/norm.hip (ops/norm.py) instead of PyTorch's instance_norm, which would
+copy each channels_last map to NCHW and back.  NHWC also keeps the 1x1
 projection's output directly usable as the K-contiguous operand of the
 correlation MFMA GEMM (csrc/corr_volume.hip).
 """
@@ -22,6 +25,8 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
+
+from ..ops.norm import norm_act
 
 
 def make_norm(kind: str, channels: int, groups: int) -> nn.Module:
@@ -54,10 +59,10 @@ class ResidualBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm3)
 
     def forward(self, x):
-        y = self.relu(self.norm1(self.conv1(x)))
-        y = self.relu(self.norm2(self.conv2(y)))
-        skip = x if self.downsample is None else self.downsample(x)
-        return self.relu(skip + y)
+        y = norm_act(self.norm1, self.conv1(x))
+        skip = x if self.downsample is None else norm_act(self.norm3, self.downsample[0](x), relu=False)
+        # relu(skip + relu(norm2(conv2(y)))) as one fused pass on GPU
+        return norm_act(self.norm2, self.conv2(y), relu=True, residual=skip)
 
 
 class BottleneckBlock(nn.Module):
@@ -81,11 +86,10 @@ class BottleneckBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm4)
 
     def forward(self, x):
-        y = self.relu(self.norm1(self.conv1(x)))
-        y = self.relu(self.norm2(self.conv2(y)))
-        y = self.relu(self.norm3(self.conv3(y)))
-        skip = x if self.downsample is None else self.downsample(x)
-        return self.relu(skip + y)
+        y = norm_act(self.norm1, self.conv1(x))
+        y = norm_act(self.norm2, self.conv2(y))
+        skip = x if self.downsample is None else norm_act(self.norm4, self.downsample[0](x), relu=False)
+        return norm_act(self.norm3, self.conv3(y), relu=True, residual=skip)
 
 
 class _Encoder(nn.Module):
@@ -133,7 +137,7 @@ class _Encoder(nn.Module):
         if pair:
             n = x[0].shape[0]
             x = torch.cat(list(x), dim=0)
-        x = self.relu1(self.norm1(self.conv1(x)))
+        x = norm_act(self.norm1, self.conv1(x))
         x = self.layer3(self.layer2(self.layer1(x)))
         x = self.conv2(x)
         if self.training and self.dropout is not None:

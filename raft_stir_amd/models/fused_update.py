@@ -1,0 +1,229 @@
+"""Fused inference engine for the RAFT refinement loop (bf16, MI355X).
+
+Replaces, for inference (no autograd, bf16 autocast), the per-iteration
+module graph of reference core/raft.py:122-139 + core/update.py (motion
+encoder, ConvGRU / SepConvGRU, flow head, mask head, ~40 kernels and
+several concatenations per iteration) with a fixed sequence of hand-written
+HIP launches over persistent channels-last buffers:
+
+  full RAFT, per iteration (12 launches, +2 on iterations that upsample):
+    corr_lookup_into   pyramid window lookup -> corr[., 352]   (324 + zero pad)
+    flow_encode        convf1 7x7 of (coords1 - grid), ReLU   -> f1[., 128];
+                       flow (bf16) -> hx[., 382:384]
+    conv convc1 1x1    corr -> c1 (ReLU)
+    conv convc2 3x3    c1 -> mot[., 0:192] (ReLU)
+    conv convf2 3x3    f1 -> mot[., 192:256] (ReLU)
+    conv conv   3x3    mot -> hx[., 256:382] (ReLU)          (= cat[out, flow])
+    conv z|r 1x5       hx -> z, r*h          (GRU gate epilogue)
+    conv q   1x5       [r*h | hx[128:]] -> hx[., 0:128] = (1-z)h + z tanh(q)
+    conv z|r, q 5x1    (second SepConvGRU pass)
+    conv head 3x3      h -> [flow-head hidden | mask hidden] (ReLU; one GEMM,
+                       the mask half only on iterations that upsample)
+    conv flow 3x3      -> coords1 += delta   (coords update epilogue)
+    conv mask 1x1      -> mask x 0.25        (upsampling iterations only)
+    convex_upsample    (upsampling iterations only)
+
+  hx = [h | inp | motion | flow] is ONE buffer, so cat[h, x] and
+  cat[r*h, x] are just different segment views of it.
+
+RAFT-small uses the same machinery (ConvGRU 3x3, hidden 96, context 64,
+corr radius 3 -> 196 channels, bilinear x8 upsampling).
+
+Packed weights are cached per (parameter versions) and rebuilt after any
+in-place update, so an optimizer step between evaluations is picked up.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import _ext
+from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, conv_fused, pack_bias,
+                        pack_weight, pad_to)
+from ..ops.upsample import convex_upsample
+
+
+class _Conv:
+    """One packed convolution: weight [Cout_pad][taps][Ktot] bf16 + fp32 bias."""
+
+    def __init__(self, convs, segs, cout_pad_mult=32):
+        convs = convs if isinstance(convs, (list, tuple)) else [convs]
+        weight = torch.cat([c.weight for c in convs], 0)
+        bias = torch.cat([c.bias for c in convs], 0)
+        self.cout = weight.shape[0]
+        self.kh, self.kw = weight.shape[2], weight.shape[3]
+        self.w = pack_weight(weight, segs, pad_to(self.cout, 64))
+        self.b = pack_bias(bias)
+
+
+class FusedUpdate:
+    def __init__(self, model):
+        self.model = model
+        self.key = None
+        self.bufs = {}
+
+    # ------------------------------------------------------------ eligibility
+    @staticmethod
+    def eligible(model, image, corr_fn) -> bool:
+        if image.device.type != "cuda" or torch.is_grad_enabled():
+            return False
+        if not model.cfg.mixed_precision or not model.cfg.fused_gru:
+            return False
+        if not _ext.use_hip(image):
+            return False
+        return getattr(corr_fn, "hip", False)
+
+    # ------------------------------------------------------------ weights
+    def _version_key(self):
+        return tuple((p.data_ptr(), p._version) for p in self.model.update_block.parameters())
+
+    @torch.no_grad()
+    def _pack(self):
+        ub = self.model.update_block
+        small = self.model.cfg.small
+        if small:
+            hd, cd, corr_c = 96, 64, 4 * 49
+            self.corr_pad = pad_to(corr_c, 32)   # 224
+            enc = ub.encoder
+            # hx = [h 96 | inp 64 | mot 80 | flow 2 | pad 14] = 256
+            self.hx_c, self.off_inp, self.off_mot, self.off_flow = 256, 96, 160, 240
+            self.mot_c = 128                    # [c1 96 | f2 32]
+            self.convc1 = _Conv(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
+            self.convf2 = _Conv(enc.convf2, [(64, [(0, 64, 0)])])
+            self.conv = _Conv(enc.conv, [(128, [(0, 128, 0)])])
+            self.f1_c = 64
+            gru = ub.gru
+            self.gru = [(
+                _Conv([gru.convz, gru.convr], [(256, [(0, hd, 0), (hd, cd + 82, hd)])]),
+                _Conv(gru.convq, [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]),
+            )]
+            self.head = _Conv(ub.flow_head.conv1, [(96, [(0, hd, 0)])])
+            self.head_c = 128
+            self.flow = _Conv(ub.flow_head.conv2, [(128, [(0, 128, 0)])])
+            self.mask0 = self.mask2 = None
+        else:
+            hd, cd, corr_c = 128, 128, 4 * 81
+            self.corr_pad = pad_to(corr_c, 32)   # 352
+            enc = ub.encoder
+            # hx = [h 128 | inp 128 | mot 126 | flow 2] = 384
+            self.hx_c, self.off_inp, self.off_mot, self.off_flow = 384, 128, 256, 382
+            self.mot_c = 256                    # [c2 192 | f2 64]
+            self.convc1 = _Conv(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
+            self.convc2 = _Conv(enc.convc2, [(256, [(0, 256, 0)])])
+            self.convf2 = _Conv(enc.convf2, [(128, [(0, 128, 0)])])
+            self.conv = _Conv(enc.conv, [(256, [(0, 256, 0)])])
+            self.f1_c = 128
+            g = ub.gru
+            self.gru = []
+            for zc, rc, qc in ((g.convz1, g.convr1, g.convq1), (g.convz2, g.convr2, g.convq2)):
+                self.gru.append((
+                    _Conv([zc, rc], [(384, [(0, 384, 0)])]),
+                    _Conv(qc, [(128, [(0, hd, 0)]), (256, [(hd, 256, 0)])]),
+                ))
+            self.head = _Conv([ub.flow_head.conv1, ub.mask[0]], [(128, [(0, hd, 0)])])
+            self.head_c = 512
+            self.flow = _Conv(ub.flow_head.conv2, [(256, [(0, 256, 0)])])
+            self.mask2 = _Conv(ub.mask[2], [(256, [(0, 256, 0)])])
+        self.hd, self.cd = hd, cd
+        f1 = ub.encoder.convf1
+        self.f1_w = f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()  # [7][7][2][Cout]
+        self.f1_b = f1.bias.detach().float().contiguous()
+
+    def _reuse_storage(self, old):
+        """Copy freshly packed weights into the previous tensors (same shapes),
+        so hipGraphs captured against them stay valid after a weight update."""
+        for name, new in list(self.__dict__.items()):
+            prev = old.get(name)
+            if isinstance(new, _Conv) and isinstance(prev, _Conv) and prev.w.shape == new.w.shape:
+                prev.w.copy_(new.w)
+                prev.b.copy_(new.b)
+                self.__dict__[name] = prev
+            elif name == "gru" and isinstance(prev, list) and len(prev) == len(new):
+                for (pz, pq), (nz, nq) in zip(prev, new):
+                    for p_, n_ in ((pz, nz), (pq, nq)):
+                        p_.w.copy_(n_.w)
+                        p_.b.copy_(n_.b)
+                self.gru = prev
+            elif name in ("f1_w", "f1_b") and isinstance(prev, torch.Tensor) and prev.shape == new.shape:
+                prev.copy_(new)
+                self.__dict__[name] = prev
+
+    def _buffers(self, B, H, W, dev):
+        key = (B, H, W, dev)
+        bufs = self.bufs.get(key)
+        if bufs is None:
+            e = lambda c: torch.empty(B, H, W, c, device=dev, dtype=torch.bfloat16)
+            z = lambda c: torch.zeros(B, H, W, c, device=dev, dtype=torch.bfloat16)
+            bufs = dict(corr=e(self.corr_pad), f1=e(self.f1_c), mot=e(self.mot_c), hx=z(self.hx_c),
+                        z=e(self.hd), rh=z(pad_to(self.hd, 32)), head=e(self.head_c))
+            if not self.model.cfg.small:
+                bufs["c1"] = e(256)
+                bufs["mask"] = e(576)
+            # kept for every shape seen: a captured hipGraph references them
+            self.bufs[key] = bufs
+        return bufs
+
+    # ------------------------------------------------------------ run
+    @torch.no_grad()
+    def run(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        k = self._version_key()
+        if k != self.key:
+            old = self.__dict__.copy()
+            self._pack()
+            self._reuse_storage(old)
+            self.key = k
+        B, _, H, W = coords1.shape
+        bufs = self._buffers(B, H, W, coords1.device)
+        hx = bufs["hx"]
+        hd = self.hd
+        hx[..., :hd].copy_(net.permute(0, 2, 3, 1))
+        hx[..., self.off_inp:self.off_inp + self.cd].copy_(inp.permute(0, 2, 3, 1))
+        coords1 = coords1.float().contiguous().clone()
+        st = corr_fn.state
+        small = self.model.cfg.small
+        preds, flow_up = [], None
+        for itr in range(iters):
+            want_up = (not test_mode) or itr == iters - 1
+            torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
+            torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
+            cp = self.corr_pad
+            if small:
+                conv_fused([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
+                           bufs["mot"], 0)
+                conv_fused([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
+                           bufs["mot"], 96)
+                conv_fused([(bufs["mot"], 0, 128)], self.conv.w, self.conv.b, 3, 3, 80, EPI_RELU,
+                           hx, self.off_mot)
+            else:
+                conv_fused([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 256, EPI_RELU,
+                           bufs["c1"], 0)
+                conv_fused([(bufs["c1"], 0, 256)], self.convc2.w, self.convc2.b, 3, 3, 192, EPI_RELU,
+                           bufs["mot"], 0)
+                conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                           bufs["mot"], 192)
+                conv_fused([(bufs["mot"], 0, 256)], self.conv.w, self.conv.b, 3, 3, 126, EPI_RELU,
+                           hx, self.off_mot)
+            for zr, q in self.gru:
+                rhc = bufs["rh"].shape[-1]
+                conv_fused([(hx, 0, self.hx_c)], zr.w, zr.b, zr.kh, zr.kw, 2 * hd, EPI_GRU_ZR,
+                           bufs["z"], 0, hd=hd, out2=bufs["rh"], o2off=0, aux1=hx, a1off=0)
+                conv_fused([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
+                           EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0)
+            if small:
+                conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0)
+                conv_fused([(bufs["head"], 0, 128)], self.flow.w, self.flow.b, 3, 3, 2, EPI_FLOW, coords1)
+            else:
+                conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
+                           bufs["head"], 0)
+                conv_fused([(bufs["head"], 0, 256)], self.flow.w, self.flow.b, 3, 3, 2, EPI_FLOW, coords1)
+            if not want_up:
+                continue
+            flow = coords1 - coords0
+            if small:
+                flow_up = 8 * F.interpolate(flow, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)
+            else:
+                conv_fused([(bufs["head"], 256, 256)], self.mask2.w, self.mask2.b, 1, 1, 576, EPI_SCALE,
+                           bufs["mask"], 0, scale=0.25)
+                flow_up = convex_upsample(flow, bufs["mask"].permute(0, 3, 1, 2))
+            preds.append(flow_up)
+        return coords1, preds, flow_up

@@ -15,6 +15,9 @@ Engine differences (outputs unchanged):
     kernel, HIP pyramid lookup, fused ConvGRU gates, HIP convex upsampler.
   * test_mode computes the mask head and the convex upsampling only on the
     last iteration -- the only one whose output is returned (reference B7).
+  * GPU inference (no autograd, bf16) runs the refinement loop through the
+    fused engine of models/fused_update.py: ~12 hand-written HIP launches per
+    iteration over persistent NHWC buffers instead of the module graph.
 """
 from __future__ import annotations
 
@@ -23,10 +26,12 @@ import torch.nn as nn
 
 from ..config import RAFTConfig, resolve_config
 from ..ops import _ext
+from ..ops import gru as gru_ops
 from ..ops import reference as ref
 from ..ops.upsample import convex_upsample, upflow8
 from .corr import CorrBlock, AlternateCorrBlock
 from .extractor import BasicEncoder, SmallEncoder
+from .fused_update import FusedUpdate
 from .update import BasicUpdateBlock, SmallUpdateBlock
 
 
@@ -53,6 +58,13 @@ class RAFT(nn.Module):
         for m in self.modules():
             if hasattr(m, "fused") and m is not self:
                 m.fused = enabled
+
+    def _fused_engine(self):
+        eng = self.__dict__.get("_fused")
+        if eng is None or eng.model is not self:
+            eng = FusedUpdate(self)
+            self.__dict__["_fused"] = eng
+        return eng
 
     def freeze_bn(self):
         for m in self.modules():
@@ -84,52 +96,62 @@ class RAFT(nn.Module):
         hdim, cdim = self.hidden_dim, self.context_dim
         mixed = bool(self.cfg.mixed_precision) and gpu
 
+        # ONE autocast region for the whole forward: autocast caches the bf16
+        # copy of every weight for the region, so each conv weight is cast
+        # once per forward instead of once per iteration (and its gradient
+        # accumulates over the 12 iterations before a single cast back).
+        gru_ops.begin_forward()
         with self._autocast(dev):
             fmap1, fmap2 = self.fnet([image1, image2])
-        # The reference casts the features to fp32 (core/raft.py:102-103).  Under
-        # bf16 autocast they are exactly representable in bf16, so the MFMA
-        # volume kernel consumes them in bf16 with fp32 accumulation (exact
-        # products); in fp32 mode it runs the exact fp32 MFMA variant.
-        if not (mixed and _ext.use_hip(fmap1)):
-            fmap1, fmap2 = fmap1.float(), fmap2.float()
-        corr_dtype = torch.bfloat16 if mixed else torch.float32
-        block = AlternateCorrBlock if self.cfg.alternate_corr else CorrBlock
-        corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
-                        radius=self.cfg.corr_radius, out_dtype=corr_dtype)
+            # The reference casts the features to fp32 (core/raft.py:102-103).
+            # Under bf16 autocast they are exactly representable in bf16, so the
+            # MFMA volume kernel consumes them in bf16 with fp32 accumulation
+            # (exact products); in fp32 mode it runs the exact fp32 MFMA variant.
+            if not (mixed and _ext.use_hip(fmap1)):
+                fmap1, fmap2 = fmap1.float(), fmap2.float()
+            corr_dtype = torch.bfloat16 if mixed else torch.float32
+            block = AlternateCorrBlock if self.cfg.alternate_corr else CorrBlock
+            corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
+                            radius=self.cfg.corr_radius, out_dtype=corr_dtype)
 
-        with self._autocast(dev):
             cnet = self.cnet(image1)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)
 
-        coords0, coords1 = self.initialize_flow(image1)
-        if flow_init is not None:
-            coords1 = coords1 + flow_init
+            coords0, coords1 = self.initialize_flow(image1)
+            if flow_init is not None:
+                coords1 = coords1 + flow_init
 
-        small = self.cfg.small
-        preds = []
-        flow_up = None
-        for itr in range(iters):
-            coords1 = coords1.detach()
-            corr = corr_fn(coords1)
-            flow = coords1 - coords0
-            last = itr == iters - 1
-            want_up = (not test_mode) or last
-            with self._autocast(dev):
+            if FusedUpdate.eligible(self, image1, corr_fn):
+                eng = self._fused_engine()
+                coords1, preds, flow_up = eng.run(net, inp, corr_fn, coords0, coords1, iters, test_mode)
+                if test_mode:
+                    return coords1 - coords0, flow_up
+                return preds
+
+            small = self.cfg.small
+            preds = []
+            flow_up = None
+            for itr in range(iters):
+                coords1 = coords1.detach()
+                corr = corr_fn(coords1)
+                flow = coords1 - coords0
+                last = itr == iters - 1
+                want_up = (not test_mode) or last
                 if small:
                     net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
                 else:
                     net, up_mask, delta_flow = self.update_block(net, inp, corr, flow,
                                                                  upsample=want_up)
-            coords1 = coords1 + delta_flow.float()
-            if not want_up:
-                continue
-            if up_mask is None:
-                flow_up = upflow8(coords1 - coords0)
-            else:
-                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
-            preds.append(flow_up)
+                coords1 = coords1 + delta_flow.float()
+                if not want_up:
+                    continue
+                if up_mask is None:
+                    flow_up = upflow8(coords1 - coords0)
+                else:
+                    flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+                preds.append(flow_up)
 
         if test_mode:
             return coords1 - coords0, flow_up

@@ -1,0 +1,60 @@
+"""Host side of the fused update-block convolution (csrc/conv.hip).
+
+* :func:`pack_weight` turns a PyTorch conv weight (Cout, Cin, KH, KW) into the
+  kernel's [Cout_pad][taps][Ktot] bf16 layout for a given channel-SEGMENT
+  layout of its input: each segment is a (padded channel count, pieces) pair
+  where a piece maps weight input channels [w0, w0+n) to segment channels
+  [s0, s0+n).  Unmapped (padding) channels get zero weights, so the kernel's
+  K loop runs over 32-channel chunks with no bounds checks.
+* :func:`conv_fused` is a thin, checked wrapper over torch.ops.raft_stir.conv_fused.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_GRU_ZR, EPI_GRU_Q, EPI_FLOW = range(6)
+
+Piece = Tuple[int, int, int]          # (weight in-channel start, length, segment channel offset)
+SegSpec = Tuple[int, Sequence[Piece]]  # (segment channels read (multiple of 32), pieces)
+
+
+def pad_to(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+@torch.no_grad()
+def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int) -> torch.Tensor:
+    cout, cin, kh, kw = weight.shape
+    taps = kh * kw
+    wt = weight.detach().float().permute(0, 2, 3, 1).reshape(cout, taps, cin)
+    ktot = sum(c for c, _ in segs)
+    out = torch.zeros(cout_pad, taps, ktot, device=weight.device, dtype=torch.float32)
+    kb = 0
+    for c, pieces in segs:
+        assert c % 32 == 0
+        for w0, n, s0 in pieces:
+            assert s0 + n <= c and w0 + n <= cin
+            out[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
+        kb += c
+    return out.to(torch.bfloat16).contiguous()
+
+
+@torch.no_grad()
+def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
+    b = bias.detach().float()
+    if n is not None and n > b.numel():
+        b = torch.cat([b, b.new_zeros(n - b.numel())])
+    return b.contiguous()
+
+
+def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
+               scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
+               aux2=None, a2off=0, tile=0):
+    """segs: list of (NHWC bf16 buffer, channel offset, channels read)."""
+    tensors = [s[0] for s in segs]
+    offs = [int(s[1]) for s in segs]
+    chans = [int(s[2]) for s in segs]
+    torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
+                                   out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

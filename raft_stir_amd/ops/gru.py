@@ -68,12 +68,31 @@ def _compute_dtype(h):
     return h.dtype if h.dtype in (torch.float32, torch.bfloat16) else torch.float32
 
 
+_WCACHE = {}
+
+
+def begin_forward():
+    """Called once per RAFT forward: the fused/cast GRU weights are built once
+    per forward (they are nodes of this forward's autograd graph, so their
+    gradients accumulate over the iterations and flow back once)."""
+    _WCACHE.clear()
+
+
+def _weights(convz, convr, convq, dt):
+    key = (id(convz), dt)
+    w = _WCACHE.get(key)
+    if w is None:
+        wzr = torch.cat([convz.weight, convr.weight], dim=0).to(dt).contiguous(memory_format=_CL)
+        bzr = torch.cat([convz.bias, convr.bias], dim=0).to(dt)
+        wq = convq.weight.to(dt).contiguous(memory_format=_CL)
+        bq = convq.bias.to(dt)
+        w = _WCACHE[key] = (wzr, bzr, wq, bq)
+    return w
+
+
 def gru_pass(h, x, convz, convr, convq):
     dt = _compute_dtype(h)
-    wzr = torch.cat([convz.weight, convr.weight], dim=0).to(dt).contiguous(memory_format=_CL)
-    bzr = torch.cat([convz.bias, convr.bias], dim=0).to(dt)
-    wq = convq.weight.to(dt).contiguous(memory_format=_CL)
-    bq = convq.bias.to(dt)
+    wzr, bzr, wq, bq = _weights(convz, convr, convq, dt)
     h = h.to(dt).contiguous(memory_format=_CL)
     x = x.to(dt).contiguous(memory_format=_CL)
     with torch.autocast("cuda", enabled=False):

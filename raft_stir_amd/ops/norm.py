@@ -1,0 +1,105 @@
+"""Fused channels-last normalisation + activation for the encoders.
+
+``norm_act(norm, x, relu=True, residual=None)`` computes, with the semantics of
+reference core/extractor.py (``relu(norm(x))``; residual blocks
+``relu(skip + relu(norm(conv(y))))``):
+
+    y = norm(x); if relu: y = relu(y); if residual is not None: y = relu(residual + y)
+
+On GPU tensors with an InstanceNorm2d (no affine, no running stats -- the
+reference fnet) or BatchNorm2d (the reference cnet; training mode uses batch
+statistics and updates the running buffers exactly like nn.BatchNorm2d, eval
+mode uses the running buffers) it runs csrc/norm.hip directly on the NHWC
+memory of a channels_last activation: no NCHW round-trip copies, one stats
+pass + one fused apply pass forward, one reduction + one apply pass backward.
+Everything else (CPU, export, GroupNorm, identity) takes the composite path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+
+_CL = torch.channels_last
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+class _NormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, mean, rstd, relu, batch_stats):
+        xn = _nhwc(x)
+        rn = _nhwc(res) if res is not None else None
+        y = torch.ops.raft_stir.norm_act(xn, mean, rstd, gamma, beta, rn, relu)
+        ctx.save_for_backward(x, gamma, beta, res, mean, rstd)
+        ctx.relu, ctx.batch_stats = relu, batch_stats
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, res, mean, rstd = ctx.saved_tensors
+        dyn = _nhwc(dy.contiguous(memory_format=_CL)).to(x.dtype)
+        rn = _nhwc(res) if res is not None else None
+        dx, dres, s1, s2 = torch.ops.raft_stir.norm_act_backward(
+            dyn, _nhwc(x), mean, rstd, gamma, beta, rn, ctx.relu, ctx.batch_stats)
+        dgamma = s2.sum(0) if gamma is not None and ctx.needs_input_grad[1] else None
+        dbeta = s1.sum(0) if beta is not None and ctx.needs_input_grad[2] else None
+        dres_out = dres.permute(0, 3, 1, 2) if res is not None else None
+        return dx.permute(0, 3, 1, 2), dgamma, dbeta, dres_out, None, None, None, None
+
+
+def _hip_ok(norm, x, residual):
+    if not _ext.use_hip(x) or x.dim() != 4:
+        return False
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        return False
+    if not x.is_contiguous(memory_format=_CL):
+        return False
+    if residual is not None and (residual.dtype != x.dtype or residual.shape != x.shape):
+        return False
+    C = x.shape[1]
+    vn = 8 if x.dtype == torch.bfloat16 else 4
+    if C % vn or C // vn > 256:
+        return False
+    if isinstance(norm, nn.InstanceNorm2d):
+        return not norm.affine and not norm.track_running_stats
+    if isinstance(norm, nn.BatchNorm2d):
+        return norm.affine and norm.track_running_stats and norm.momentum is not None
+    return False
+
+
+def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None):
+    if not _hip_ok(norm, x, residual):
+        y = norm(x)
+        if relu:
+            y = F.relu(y)
+        if residual is not None:
+            y = F.relu(residual + y)
+        return y
+    if residual is not None:
+        residual = residual.contiguous(memory_format=_CL)
+    xn = _nhwc(x)
+    if isinstance(norm, nn.InstanceNorm2d):
+        mean, rstd = torch.ops.raft_stir.norm_stats(xn, True, norm.eps)
+        return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True)
+    # BatchNorm2d
+    batch_stats = norm.training
+    if batch_stats:
+        mean, rstd = torch.ops.raft_stir.norm_stats(xn, False, norm.eps)
+        with torch.no_grad():
+            n = x.numel() // x.shape[1]
+            var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
+            unbiased = var * (n / max(n - 1, 1))
+            m = norm.momentum
+            norm.running_mean.mul_(1 - m).add_(mean.reshape(-1), alpha=m)
+            norm.running_var.mul_(1 - m).add_(unbiased, alpha=m)
+            norm.num_batches_tracked.add_(1)
+    else:
+        mean = norm.running_mean.float().reshape(1, -1)
+        rstd = torch.rsqrt(norm.running_var.float() + norm.eps).reshape(1, -1)
+    return _NormAct.apply(x, norm.weight, norm.bias, residual, mean.contiguous(), rstd.contiguous(),
+                          relu, batch_stats)

@@ -1,0 +1,82 @@
+#!/usr/bin/env python
+"""Microbenchmark of the fused update-block convolution (csrc/conv.hip) on
+every conv shape of the RAFT update block, vs MIOpen (F.conv2d, bf16,
+channels_last) on the same shape.  Prints one line per (shape, variant).
+
+    python scripts/bench_conv.py [--hw 55 136] [--batch 1] [--reps 50] [--tiles 0 1]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+# name, cin, cout, kh, kw
+SHAPES = [
+    ("convc1", 352, 256, 1, 1),
+    ("convc2", 256, 192, 3, 3),
+    ("convf2", 128, 64, 3, 3),
+    ("conv", 256, 126, 3, 3),
+    ("gru_zr", 384, 256, 1, 5),
+    ("gru_q", 384, 128, 1, 5),
+    ("head", 128, 512, 3, 3),
+    ("flow", 256, 2, 3, 3),
+    ("mask2", 256, 576, 1, 1),
+]
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000.0 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hw", type=int, nargs=2, default=[55, 136])
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--tiles", type=int, nargs="+", default=[0, 1])
+    a = ap.parse_args()
+    from raft_stir_amd.ops import _ext
+    from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
+    _ext.load(raise_on_error=True)
+    dev = torch.device("cuda", 0)
+    B, (H, W) = a.batch, a.hw
+    P = B * H * W
+    tot = {}
+    for name, cin, cout, kh, kw in SHAPES:
+        x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
+        w = torch.randn(cout, cin, kh, kw, device=dev) * 0.05
+        b = torch.randn(cout, device=dev)
+        out = torch.empty(B, H, W, pad_to(cout, 8), device=dev, dtype=torch.bfloat16)
+        wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 64))
+        bp = pack_bias(b)
+        flop = 2.0 * P * cout * cin * kh * kw
+        line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"
+        for t in a.tiles:
+            us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
+            line += f" tile{t} {us:7.1f}us {flop / us / 1e6:6.1f}TF |"
+            tot.setdefault(f"tile{t}", 0.0)
+            tot[f"tile{t}"] += us
+        xc = x.permute(0, 3, 1, 2)
+        wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        us = timeit(lambda: F.relu(F.conv2d(xc, wb, b.to(torch.bfloat16), padding=(kh // 2, kw // 2))), a.reps)
+        line += f" miopen {us:7.1f}us {flop / us / 1e6:6.1f}TF"
+        tot["miopen"] = tot.get("miopen", 0.0) + us
+        print(line, flush=True)
+    print("sum per iteration-set:", {k: round(v, 1) for k, v in tot.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+#!/usr/bin/env python
+"""torch.profiler breakdown (aten op level, with input shapes) of one training
+step and one inference forward -- finds the glue ops (copies, casts, cats)
+around the HIP kernels.  Writes gpurun_out/torch_prof_{train,infer}.txt.
+
+    python scripts/torch_prof.py [--batch 8] [--small] [--mode train|infer|both]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--small", action="store_true")
+    ap.add_argument("--mode", default="both")
+    ap.add_argument("--out", default="gpurun_out")
+    a = ap.parse_args()
+    from raft_stir_amd.config import make_args
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.models import RAFT
+    from raft_stir_amd.train.loss import sequence_loss
+    from raft_stir_amd.train.optim import fetch_optimizer
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = RAFT(make_args(small=a.small, mixed_precision=True)).to(dev).to(memory_format=torch.channels_last)
+    os.makedirs(a.out, exist_ok=True)
+    if a.mode in ("train", "both"):
+        model.train()
+        opt, sch = fetch_optimizer(argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=1000), model)
+        i1, i2, fl, v = make_batch(a.batch, 368, 496, device=dev)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss, _ = sequence_loss(model(i1, i2, iters=12), fl, v, 0.8, sync_metrics=False)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
+            sch.step()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            step()
+            torch.cuda.synchronize()
+        with open(os.path.join(a.out, "torch_prof_train.txt"), "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
+                                                                       max_name_column_width=60,
+                                                                       max_shapes_column_width=90))
+            f.write("\n\n")
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=60))
+    if a.mode in ("infer", "both"):
+        model.eval()
+        from raft_stir_amd.utils.padder import InputPadder
+        i1 = torch.rand(1, 3, 436, 1088, device=dev) * 255
+        i2 = torch.rand(1, 3, 436, 1088, device=dev) * 255
+        i1, i2 = InputPadder(i1.shape).pad(i1, i2)
+        with torch.no_grad():
+            for _ in range(3):
+                model(i1, i2, iters=12, test_mode=True)
+            torch.cuda.synchronize()
+            with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+                model(i1, i2, iters=12, test_mode=True)
+                torch.cuda.synchronize()
+        with open(os.path.join(a.out, "torch_prof_infer.txt"), "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=80,
+                                                                       max_name_column_width=60,
+                                                                       max_shapes_column_width=90))
+            f.write("\n\n")
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=60))
+    print("ok")
+
+
+if __name__ == "__main__":
+    main()

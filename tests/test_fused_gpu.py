@@ -1,0 +1,153 @@
+"""Fused update-block convolution (csrc/conv.hip) and the fused inference
+engine (models/fused_update.py) vs plain fp32 PyTorch."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from raft_stir_amd.config import make_args
+from raft_stir_amd.models import RAFT
+from raft_stir_amd.ops.conv import (EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE,
+                                    conv_fused, pack_bias, pack_weight, pad_to)
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5), (5, 1)])
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
+def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
+    torch.manual_seed(0)
+    B, H, W = 2, 11, 19
+    kh, kw = k
+    # input = cat[a (40 ch, stored in a 64-wide buffer at offset 8), b (32 ch)]
+    a_buf = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
+    b_buf = torch.randn(B, H, W, 32, device=cuda).to(torch.bfloat16)
+    x = torch.cat([a_buf[..., 8:48], b_buf], -1).float().permute(0, 3, 1, 2)
+    cout = 70
+    w = torch.randn(cout, 72, kh, kw, device=cuda) * 0.1
+    b = torch.randn(cout, device=cuda)
+    # segment 0 reads 64 channels from a_buf at offset 0: weights for [8,48) only
+    wp = pack_weight(w, [(64, [(0, 40, 8)]), (32, [(40, 32, 0)])], pad_to(cout, 64))
+    out = torch.full((B, H, W, 80), 7.0, device=cuda, dtype=torch.bfloat16)
+    conv_fused([(a_buf, 0, 64), (b_buf, 0, 32)], wp, pack_bias(b), kh, kw, cout, epi, out, 4,
+               scale=0.25, tile=tile)
+    ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2))
+    if epi == EPI_RELU:
+        ref = ref.relu()
+    if epi == EPI_SCALE:
+        ref = ref * 0.25
+    got = out[..., 4:4 + cout].float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
+    assert (out[..., :4] == 7).all() and (out[..., 4 + cout:] == 7).all()  # no writes outside the window
+
+
+def test_gru_epilogues(cuda):
+    torch.manual_seed(1)
+    B, H, W, hd = 1, 9, 13, 64
+    hx = torch.randn(B, H, W, 3 * hd, device=cuda).to(torch.bfloat16)   # [h | x(2hd)]
+    wz = torch.randn(hd, 3 * hd, 1, 5, device=cuda) * 0.05
+    wr = torch.randn(hd, 3 * hd, 1, 5, device=cuda) * 0.05
+    wq = torch.randn(hd, 3 * hd, 1, 5, device=cuda) * 0.05
+    bz, br, bq = (torch.randn(hd, device=cuda) * 0.1 for _ in range(3))
+    wzr = pack_weight(torch.cat([wz, wr]), [(3 * hd, [(0, 3 * hd, 0)])], 2 * hd)
+    z = torch.empty(B, H, W, hd, device=cuda, dtype=torch.bfloat16)
+    rh = torch.empty_like(z)
+    rs = torch.empty_like(z)
+    conv_fused([(hx, 0, 3 * hd)], wzr, pack_bias(torch.cat([bz, br])), 1, 5, 2 * hd, EPI_GRU_ZR, z, 0,
+               hd=hd, out2=rh, out3=rs, aux1=hx, a1off=0)
+    xin = hx.float().permute(0, 3, 1, 2)
+    h = xin[:, :hd]
+    zr_ = torch.sigmoid(F.conv2d(xin, _bf(wz), bz, padding=(0, 2)))
+    r_ = torch.sigmoid(F.conv2d(xin, _bf(wr), br, padding=(0, 2)))
+    torch.testing.assert_close(z.float().permute(0, 3, 1, 2), zr_, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(rs.float().permute(0, 3, 1, 2), r_, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(rh.float().permute(0, 3, 1, 2), r_ * h, atol=3e-2, rtol=3e-2)
+    wqp = pack_weight(wq, [(hd, [(0, hd, 0)]), (2 * hd, [(hd, 2 * hd, 0)])], hd)
+    hx2 = hx.clone()
+    conv_fused([(rh, 0, hd), (hx2, hd, 2 * hd)], wqp, pack_bias(bq), 1, 5, hd, EPI_GRU_Q, hx2, 0,
+               aux1=hx2, a1off=0, aux2=z, a2off=0)
+    qin = torch.cat([rh.float().permute(0, 3, 1, 2), xin[:, hd:]], 1)
+    q = torch.tanh(F.conv2d(qin, _bf(wq), bq, padding=(0, 2)))
+    zz = z.float().permute(0, 3, 1, 2)
+    hn = (1 - zz) * h + zz * q
+    torch.testing.assert_close(hx2[..., :hd].float().permute(0, 3, 1, 2), hn, atol=3e-2, rtol=3e-2)
+    assert torch.equal(hx2[..., hd:], hx[..., hd:])
+
+
+def test_flow_epilogue_and_flow_encode(cuda):
+    torch.manual_seed(2)
+    B, H, W = 2, 10, 12
+    feat = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
+    w = torch.randn(2, 64, 3, 3, device=cuda) * 0.1
+    b = torch.randn(2, device=cuda)
+    coords = torch.randn(B, 2, H, W, device=cuda) * 3
+    c0 = coords.clone()
+    conv_fused([(feat, 0, 64)], pack_weight(w, [(64, [(0, 64, 0)])], 64), pack_bias(b), 3, 3, 2, EPI_FLOW,
+               coords)
+    delta = F.conv2d(feat.float().permute(0, 3, 1, 2), _bf(w), b, padding=1)
+    torch.testing.assert_close(coords, c0 + delta, atol=2e-2, rtol=2e-2)
+    # flow encoder: relu(conv7x7(coords - grid)) and the flow itself into a slot
+    from raft_stir_amd.ops.reference import coords_grid
+    grid = coords_grid(B, H, W, device=cuda)
+    crd = grid + torch.randn(B, 2, H, W, device=cuda) * 4
+    wf = torch.randn(128, 2, 7, 7, device=cuda) * 0.1
+    bf = torch.randn(128, device=cuda)
+    out = torch.zeros(B, H, W, 128, device=cuda, dtype=torch.bfloat16)
+    slot = torch.zeros(B, H, W, 8, device=cuda, dtype=torch.bfloat16)
+    torch.ops.raft_stir.flow_encode(crd, wf.permute(2, 3, 1, 0).contiguous(), bf, out, 0, slot, 6)
+    ref = F.conv2d(crd - grid, wf, bf, padding=3).relu()
+    torch.testing.assert_close(out.float().permute(0, 3, 1, 2), ref, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(slot[..., 6:8].float().permute(0, 3, 1, 2), crd - grid, atol=5e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_fused_inference_matches_unfused(cuda, small):
+    """Fused engine vs the module graph (same bf16 autocast), and vs fp32."""
+    from raft_stir_amd.data.synthetic import make_batch
+    torch.manual_seed(0)
+    m = RAFT(make_args(small=small, mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).eval()
+    unf = copy.deepcopy(m)
+    unf.set_fused_gru(False)
+    unf.cfg = unf.cfg.__class__(**{**unf.cfg.to_dict(), "fused_gru": False})
+    f32 = copy.deepcopy(m)
+    f32.cfg = f32.cfg.__class__(**{**f32.cfg.to_dict(), "mixed_precision": False})
+    i1, i2, _, _ = make_batch(1, 256, 320, seed=1, device=cuda)
+    with torch.no_grad():
+        lo_f, up_f = m(i1, i2, iters=12, test_mode=True)
+        lo_u, up_u = unf(i1, i2, iters=12, test_mode=True)
+        lo_r, up_r = f32(i1, i2, iters=12, test_mode=True)
+        preds = m(i1, i2, iters=3, test_mode=False)
+    assert len(preds) == 3 and preds[-1].shape == up_f.shape
+    err_fused = (up_f - up_r).norm(dim=1).mean().item()
+    err_unfused = (up_u - up_r).norm(dim=1).mean().item()
+    # the fused engine must be as close to fp32 as the bf16 module graph is
+    assert err_fused < 1.5 * err_unfused + 2e-2, (err_fused, err_unfused)
+    assert torch.isfinite(up_f).all()
+
+
+def test_fused_graph_replay(cuda):
+    from raft_stir_amd.runtime.graph import GraphedInference
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).eval()
+    g = torch.Generator().manual_seed(3)
+    i1 = (torch.rand(1, 3, 128, 256, generator=g) * 255).to(cuda)
+    i2 = (torch.rand(1, 3, 128, 256, generator=g) * 255).to(cuda)
+    with torch.no_grad():
+        _, up = m(i1, i2, iters=8, test_mode=True)
+    gi = GraphedInference(m, i1.shape, iters=8)
+    _, up2 = gi(i1, i2)
+    torch.testing.assert_close(up2, up, atol=3e-2, rtol=3e-2)  # MIOpen may pick other algos under capture
+    _, up3 = gi(i2, i1)
+    with torch.no_grad():
+        _, upe = m(i2, i1, iters=8, test_mode=True)
+    torch.testing.assert_close(up3, upe, atol=3e-2, rtol=3e-2)

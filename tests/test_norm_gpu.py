@@ -1,0 +1,76 @@
+"""csrc/norm.hip (fused NHWC norm + ReLU [+ residual + ReLU]) vs the fp32 PyTorch composite."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from raft_stir_amd.ops.norm import norm_act
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(norm, x, relu, res):
+    y = norm(x)
+    if relu:
+        y = F.relu(y)
+    if res is not None:
+        y = F.relu(res + y)
+    return y
+
+
+@pytest.mark.parametrize("kind", ["instance", "batch_train", "batch_eval"])
+@pytest.mark.parametrize("C", [32, 64, 96])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,use_res", [(True, False), (False, False), (True, True)])
+def test_norm_act_fwd_bwd(cuda, kind, C, dtype, relu, use_res):
+    torch.manual_seed(0)
+    B, H, W = 3, 13, 21
+    if kind == "instance":
+        norm = nn.InstanceNorm2d(C)
+    else:
+        norm = nn.BatchNorm2d(C)
+        with torch.no_grad():
+            norm.weight.uniform_(0.5, 1.5)
+            norm.bias.uniform_(-0.3, 0.3)
+            norm.running_mean.uniform_(-0.2, 0.2)
+            norm.running_var.uniform_(0.5, 2.0)
+        norm.train(kind == "batch_train")
+    norm = norm.to(cuda)
+    ref_norm = copy.deepcopy(norm)
+    x0 = (torch.randn(B, C, H, W, device=cuda) * 2 + 0.5)
+    x = x0.to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    res = None
+    if use_res:
+        res = torch.randn(B, C, H, W, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+        res.requires_grad_(True)
+    y = norm_act(norm, x, relu=relu, residual=res)
+    xr = x.detach().float().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True) if use_res else None
+    yr = _ref(ref_norm, xr, relu, rr)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g.to(dtype).float())
+    gtol = 2e-4 if dtype == torch.float32 else 6e-2
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=gtol, rtol=gtol)
+    if use_res:
+        torch.testing.assert_close(res.grad.float(), rr.grad, atol=gtol, rtol=gtol)
+    if kind != "instance":
+        torch.testing.assert_close(norm.weight.grad, ref_norm.weight.grad, atol=gtol * 10, rtol=gtol)
+        torch.testing.assert_close(norm.bias.grad, ref_norm.bias.grad, atol=gtol * 10, rtol=gtol)
+        torch.testing.assert_close(norm.running_mean, ref_norm.running_mean, atol=1e-4, rtol=1e-3)
+        torch.testing.assert_close(norm.running_var, ref_norm.running_var, atol=1e-3, rtol=1e-3)
+
+
+def test_norm_act_large_spatial(cuda):
+    """Encoder-stem sized map (many split blocks, fp64 finalize)."""
+    torch.manual_seed(1)
+    x = (torch.randn(4, 64, 92, 124, device=cuda) * 3 + 1).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    norm = nn.InstanceNorm2d(64)
+    y = norm_act(norm, x)
+    yr = F.relu(norm(x.float()))
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
