@@ -73,6 +73,101 @@ struct Args {
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
+// Shared epilogue: acc[mt][nt][j] holds output channel m0 + mt*16 + 4*(lane>>4) + j
+// of pixel n0 + nt*16 + (lane&15).
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int n0,
+                                         int lane, const int (&pb)[WN], const int (&py)[WN],
+                                         const int (&px)[WN]) {
+  const int lr = lane & 15;
+  const int HW = a.H * a.W;
+  const int cq = (lane >> 4) * 4;
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    if (pb[nt] < 0) continue;
+    const int p = n0 + nt * 16 + lr;
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt) {
+      const int cb = m0 + mt * 16 + cq;
+      if (cb >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
+      const bool full = cb + 3 < a.Cout;
+      switch (a.epi) {
+        case EPI_FLOW: {
+          float* crd = static_cast<float*>(a.out);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = cb + j;
+            if (co < a.Cout && co < 2) {
+              float* d = crd + ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
+              *d += v[j];
+            }
+          }
+          break;
+        }
+        case EPI_GRU_ZR: {
+          if (cb < a.hd) {
+            bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
+          } else {
+            const int c = cb - a.hd;
+            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
+            bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
+            bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float r = sigmoidf_(v[j]);
+              rh[j] = f2bf(r * bf2f(h[j]));
+              if (rs_) rs_[j] = f2bf(r);
+            }
+          }
+          break;
+        }
+        case EPI_GRU_Q: {
+          const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+          const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+          bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+          bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
+          float hv[4], zv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hv[j] = bf2f(h[j]);
+            zv[j] = bf2f(z[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float q = tanhf_(v[j]);
+            hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
+            if (qs) qs[j] = f2bf(q);
+          }
+          break;
+        }
+        default: {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (a.epi == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+            else if (a.epi == EPI_SCALE) v[j] *= a.scale;
+          }
+          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+          if (full && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
+            uint2 pk;
+            pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+            pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+            *reinterpret_cast<uint2*>(o) = pk;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (cb + j < a.Cout) o[j] = f2bf(v[j]);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int WM, int WN, int WAVES_M, int WAVES_N>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_kernel(Args a) {
   const int lane = threadIdx.x & 63;
@@ -167,91 +262,219 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_kernel(Args a) {
 #undef RS_CONV_LOAD
 #undef RS_CONV_MMA
 
-  // ------------------------------------------------------------ epilogue
-  const int cq = (lane >> 4) * 4;
+  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
+// ------------------------------------------------------------------ LDS-staged variant
+// Block tile BM output channels x BN pixels, 256 threads (WAVES_M x WAVES_N
+// waves).  Per 32-deep K step the block stages the A (weights) and B (pixel
+// rows) tiles once in LDS -- XOR-swizzled 64-B rows so the 16 rows a
+// ds_read_b128 lane group reads land on 16 distinct bank slots -- and every
+// wave reads its fragments from there: each global byte is fetched once per
+// block instead of once per wave.  Global loads for step k+1 are in flight
+// while the MFMAs of step k run (register prefetch, LDS double buffer, one
+// barrier per step).
+// rows of CPR 16-byte chunks; XOR so the 16 rows of a ds_read_b128 lane group
+// hit 16 distinct 16-B bank slots (256-B bank rows hold 4 (BK=32) / 2 (BK=64) rows)
+template <int CPR>
+__device__ __forceinline__ int swz(int r, int c) {
+  return CPR == 4 ? r * 4 + (c ^ ((r >> 2) & 3)) : r * 8 + (c ^ ((r >> 1) & 7));
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK>
+__global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(BK == 32 || BK == 64, "BK");
+  constexpr int CPR = BK / 8;  // 16-byte chunks per staged row
+  constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
+  constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
+  static_assert(NA >= 1 && NB >= 1, "BM, BN must be multiples of 64");
+  __shared__ uint4 lds[2][(BM + BN) * CPR];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int bm0 = blockIdx.y * BM, bn0 = blockIdx.x * BN;
+  const int m0 = bm0 + wm * WM * 16, n0 = bn0 + wn * WN * 16;
+  const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
+  const int taps = a.KH * KW;
+  const int HW = H * W;
+
+  // this thread's staging rows
+  const bf16_t* arow[NA];
+  int acol[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = t + 256 * i;
+    arow[i] = a.w + (size_t)(bm0 + id / CPR) * taps * Ktot + (id % CPR) * 8;
+    acol[i] = id % CPR;
+  }
+  int sb[NB], sy[NB], sx[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int id = t + 256 * i;
+    const int p = bn0 + id / CPR;
+    if (p < a.P) {
+      sb[i] = p / HW;
+      const int q = p - sb[i] * HW;
+      sy[i] = q / W;
+      sx[i] = q - sy[i] * W;
+    } else {
+      sb[i] = -1;
+      sy[i] = sx[i] = 0;
+    }
+  }
+
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  constexpr int SH = BK == 32 ? 5 : 6;
+  const int e1 = taps * (s0.C >> SH);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> SH) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> SH) : 0);
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+
+  uint4 ra[NA], rb[NB];
+#define RS_GLOAD(STEP)                                                                          \
+  do {                                                                                          \
+    const int step_ = (STEP);                                                                   \
+    const int si = (step_ >= e1) + (step_ >= e2);                                               \
+    const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);                          \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                    \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
+    const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);                              \
+    const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                             \
+    const int chunks = sC >> SH;                                                                \
+    const int tap = local / chunks;                                                             \
+    const int c0 = (local - tap * chunks) * BK;                                                 \
+    const int dy = tap / KW - PH, dx = tap % KW - PW;                                           \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                              \
+      ra[i] = ld16(arow[i] + (size_t)tap * Ktot + kseg + c0);                                   \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int yy = sy[i] + dy, xx = sx[i] + dx;                                               \
+      const bool ok = sb[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;                    \
+      rb[i] = ok ? ld16(sp + ((size_t)(sb[i] * H + yy) * W + xx) * sst + c0 + ((t + 256 * i) % CPR) * 8) \
+                 : zero;                                                                        \
+    }                                                                                           \
+  } while (0)
+#define RS_LSTORE(BUF)                                                                          \
+  do {                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                            \
+      const int id = t + 256 * i;                                                               \
+      lds[BUF][swz<CPR>(id / CPR, acol[i])] = ra[i];                                            \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int id = t + 256 * i;                                                               \
+      lds[BUF][BM * CPR + swz<CPR>(id / CPR, id % CPR)] = rb[i];                                \
+    }                                                                                           \
+  } while (0)
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lc = lane >> 4;
+  RS_GLOAD(0);
+  RS_LSTORE(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    if (step + 1 < nsteps) RS_GLOAD(step + 1);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      uint4 fa[WM], fb[WN];
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) fa[mt] = lds[buf][swz<CPR>(wm * WM * 16 + mt * 16 + lr, kk * 4 + lc)];
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+        fb[nt] = lds[buf][BM * CPR + swz<CPR>(wn * WN * 16 + nt * 16 + lr, kk * 4 + lc)];
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[mt]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[nt]),
+                                                                acc[mt][nt], 0, 0, 0);
+    }
+    if (step + 1 < nsteps) RS_LSTORE(buf ^ 1);
+    __syncthreads();
+  }
+#undef RS_GLOAD
+#undef RS_LSTORE
+
+  int pb[WN], py[WN], px[WN];
 #pragma unroll
   for (int nt = 0; nt < WN; ++nt) {
-    if (pb[nt] < 0) continue;
     const int p = n0 + nt * 16 + lr;
-#pragma unroll
-    for (int mt = 0; mt < WM; ++mt) {
-      const int cb = m0 + mt * 16 + cq;
-      if (cb >= a.Cout) continue;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
-      const bool full = cb + 3 < a.Cout;
-      switch (a.epi) {
-        case EPI_FLOW: {
-          float* crd = static_cast<float*>(a.out);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int co = cb + j;
-            if (co < a.Cout && co < 2) {
-              float* d = crd + ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
-              *d += v[j];
-            }
-          }
-          break;
-        }
-        case EPI_GRU_ZR: {
-          if (cb < a.hd) {
-            bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
-          } else {
-            const int c = cb - a.hd;
-            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
-            bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
-            bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float r = sigmoidf_(v[j]);
-              rh[j] = f2bf(r * bf2f(h[j]));
-              if (rs_) rs_[j] = f2bf(r);
-            }
-          }
-          break;
-        }
-        case EPI_GRU_Q: {
-          const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
-          const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
-          bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-          bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
-          float hv[4], zv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            hv[j] = bf2f(h[j]);
-            zv[j] = bf2f(z[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float q = tanhf_(v[j]);
-            hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
-            if (qs) qs[j] = f2bf(q);
-          }
-          break;
-        }
-        default: {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (a.epi == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
-            else if (a.epi == EPI_SCALE) v[j] *= a.scale;
-          }
-          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-          if (full && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
-            uint2 pk;
-            pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-            pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-            *reinterpret_cast<uint2*>(o) = pk;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (cb + j < a.Cout) o[j] = f2bf(v[j]);
-          }
-        }
-      }
+    if (p < a.P) {
+      pb[nt] = p / HW;
+      const int q = p - pb[nt] * HW;
+      py[nt] = q / W;
+      px[nt] = q - py[nt] * W;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = 0;
     }
+  }
+  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
+// ------------------------------------------------------------------ small-N variant
+// Cout <= 16 (the flow head's 256 -> 2 conv): one 16x16 output tile per block
+// (16 pixels), the K steps split over the 4 waves (step = wave mod 4), partial
+// accumulators reduced through LDS, epilogue by wave 0.  Without the K split
+// such a conv is one long dependent MFMA chain per 16 pixels.
+__global__ __launch_bounds__(256) void conv_smalln_kernel(Args a) {
+  __shared__ f32x4_t red[4][64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
+  const int taps = a.KH * KW;
+  const int HW = H * W;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  int pb[1], py[1], px[1];
+  {
+    const int p = n0 + lr;
+    if (p < a.P) {
+      pb[0] = p / HW;
+      const int q = p - pb[0] * HW;
+      py[0] = q / W;
+      px[0] = q - py[0] * W;
+    } else {
+      pb[0] = -1;
+      py[0] = px[0] = 0;
+    }
+  }
+  const bf16_t* wrow = a.w + (size_t)lr * taps * Ktot + lk;
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const int e1 = taps * (s0.C >> 5);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 5) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 5) : 0);
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  f32x4_t acc[1][1];
+  acc[0][0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int step = wave; step < nsteps; step += 4) {
+    const int si = (step >= e1) + (step >= e2);
+    const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);
+    const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);
+    const int local = step - (si == 0 ? 0 : (si == 1 ? e1 : e2));
+    const int chunks = sC >> 5;
+    const int tap = local / chunks;
+    const int c0 = (local - tap * chunks) * 32;
+    const int dy = tap / KW - PH, dx = tap % KW - PW;
+    const uint4 fa = ld16(wrow + (size_t)tap * Ktot + kseg + c0);
+    const int yy = py[0] + dy, xx = px[0] + dx;
+    const bool ok = pb[0] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const uint4 fb = ok ? ld16(sp + ((size_t)(pb[0] * H + yy) * W + xx) * sst + c0 + lk) : zero;
+    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa),
+                                                        __builtin_bit_cast(bf16x8_t, fb), acc[0][0], 0, 0, 0);
+  }
+  red[wave][lane] = acc[0][0];
+  __syncthreads();
+  if (wave == 0) {
+    acc[0][0] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    epilogue<1, 1>(a, acc, 0, n0, lane, pb, py, px);
   }
 }
 
@@ -346,14 +569,33 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.out3 = L.out3; a.o3str = L.o3str; a.o3off = L.o3off;
   a.aux1 = static_cast<const bf16_t*>(L.aux1); a.a1str = L.a1str; a.a1off = L.a1off;
   a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
-  if (L.tile == 1) {
+  if (L.tile == 5) {
+    hipLaunchKernelGGL(conv::conv_smalln_kernel, dim3(cdiv(a.P, 16)), dim3(256), 0, stream, a);
+  } else if (L.tile >= 2) {
+    if (L.tile == 2) {  // 64 co x 128 px, waves 1 x 4 (wave 64 x 32)
+      dim3 grid(cdiv(a.P, 128), cdiv(L.Cout, 64));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<64, 128, 1, 4, 32>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 3) {  // 64 co x 64 px, waves 2 x 2 (wave 32 x 32)
+      dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 64));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<64, 64, 2, 2, 32>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 4) {  // 128 co x 64 px, waves 2 x 2 (wave 64 x 32)
+      dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 128));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<128, 64, 2, 2, 32>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 6) {  // tile 3 with 64-deep K steps
+      dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 64));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<64, 64, 2, 2, 64>), grid, dim3(256), 0, stream, a);
+    } else {  // 7: tile 4 with 64-deep K steps
+      dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 128));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<128, 64, 2, 2, 64>), grid, dim3(256), 0, stream, a);
+    }
+  } else if (L.tile == 1) {
     constexpr int WM = 4, WN = 2, WAVES_M = 1, WAVES_N = 4;
-    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout_pad, WM * 16 * WAVES_M));
+    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout, WM * 16 * WAVES_M));
     hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
                        0, stream, a);
   } else {
     constexpr int WM = 2, WN = 2, WAVES_M = 1, WAVES_N = 4;
-    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout_pad, WM * 16 * WAVES_M));
+    dim3 grid(cdiv(a.P, WN * 16 * WAVES_N), cdiv(L.Cout, WM * 16 * WAVES_M));
     hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
                        0, stream, a);
   }

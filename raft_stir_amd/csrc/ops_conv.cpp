@@ -76,11 +76,17 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  const int tileM = tile == 1 ? 64 : 32;
+  TORCH_CHECK(tile >= 0 && tile <= 7, "conv_fused: tile must be in [0,7]");
+  TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
+  const int tileM = tile == 0 ? 32 : ((tile == 4 || tile == 7) ? 128 : (tile == 5 ? 16 : 64));
+  if (tile == 6 || tile == 7)
+    for (size_t s = 0; s < segs.size(); ++s)
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 6/7 (64-deep K) need segment channels % 64 == 0");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
               "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
   TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == Ktot, "conv_fused: packed weight K mismatch");
-  TORCH_CHECK(w.size(0) >= Cout && w.size(0) % tileM == 0, "conv_fused: Cout_pad must be a multiple of ", tileM);
+  TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
+              "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
   if (bias) {
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() >= Cout &&
                     bias->is_contiguous(),

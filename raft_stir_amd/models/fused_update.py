@@ -7,7 +7,7 @@ several concatenations per iteration) with a fixed sequence of hand-written
 HIP launches over persistent channels-last buffers:
 
   full RAFT, per iteration (12 launches, +2 on iterations that upsample):
-    corr_lookup_into   pyramid window lookup -> corr[., 352]   (324 + zero pad)
+    corr_lookup_into   pyramid window lookup -> corr[., 384]   (324 + zero pad)
     flow_encode        convf1 7x7 of (coords1 - grid), ReLU   -> f1[., 128];
                        flow (bf16) -> hx[., 382:384]
     conv convc1 1x1    corr -> c1 (ReLU)
@@ -52,7 +52,7 @@ class _Conv:
         bias = torch.cat([c.bias for c in convs], 0)
         self.cout = weight.shape[0]
         self.kh, self.kw = weight.shape[2], weight.shape[3]
-        self.w = pack_weight(weight, segs, pad_to(self.cout, 64))
+        self.w = pack_weight(weight, segs, pad_to(self.cout, 128))
         self.b = pack_bias(bias)
 
 
@@ -83,7 +83,7 @@ class FusedUpdate:
         small = self.model.cfg.small
         if small:
             hd, cd, corr_c = 96, 64, 4 * 49
-            self.corr_pad = pad_to(corr_c, 32)   # 224
+            self.corr_pad = pad_to(corr_c, 64)   # 256 (64-deep K steps)
             enc = ub.encoder
             # hx = [h 96 | inp 64 | mot 80 | flow 2 | pad 14] = 256
             self.hx_c, self.off_inp, self.off_mot, self.off_flow = 256, 96, 160, 240
@@ -103,7 +103,7 @@ class FusedUpdate:
             self.mask0 = self.mask2 = None
         else:
             hd, cd, corr_c = 128, 128, 4 * 81
-            self.corr_pad = pad_to(corr_c, 32)   # 352
+            self.corr_pad = pad_to(corr_c, 64)   # 384 (64-deep K steps)
             enc = ub.encoder
             # hx = [h 128 | inp 128 | mot 126 | flow 2] = 384
             self.hx_c, self.off_inp, self.off_mot, self.off_flow = 384, 128, 256, 382

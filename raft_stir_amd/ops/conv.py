@@ -49,12 +49,28 @@ def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
     return b.contiguous()
 
 
+def choose_tile(P: int, cout: int, seg_chans) -> int:
+    """Kernel variant for a conv (measured on MI355X, scripts/bench_conv.py):
+    5 = split-K small-N (Cout <= 16); 6/7 = LDS-staged 64x64 / 128x64 tiles
+    with 64-deep K steps (all segments % 64 == 0); 3/4 = the same with 32-deep
+    K steps."""
+    if cout <= 16:
+        return 5
+    big = cout >= 192 or (cout >= 126 and P >= 16384)
+    if all(c % 64 == 0 for c in seg_chans):
+        return 7 if big else 6
+    return 4 if big else 3
+
+
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=0):
+               aux2=None, a2off=0, tile=None):
     """segs: list of (NHWC bf16 buffer, channel offset, channels read)."""
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
+    if tile is None:
+        t0 = tensors[0]
+        tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans)
     torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                    out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

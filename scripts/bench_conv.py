@@ -17,6 +17,7 @@ import torch.nn.functional as F  # noqa: E402
 # name, cin, cout, kh, kw
 SHAPES = [
     ("convc1", 352, 256, 1, 1),
+    ("convc1p", 384, 256, 1, 1),
     ("convc2", 256, 192, 3, 3),
     ("convf2", 128, 64, 3, 3),
     ("conv", 256, 126, 3, 3),
@@ -46,7 +47,7 @@ def main():
     ap.add_argument("--hw", type=int, nargs=2, default=[55, 136])
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--tiles", type=int, nargs="+", default=[0, 1])
+    ap.add_argument("--tiles", type=int, nargs="+", default=[3, 4, 5, 6, 7])
     a = ap.parse_args()
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
@@ -60,11 +61,13 @@ def main():
         w = torch.randn(cout, cin, kh, kw, device=dev) * 0.05
         b = torch.randn(cout, device=dev)
         out = torch.empty(B, H, W, pad_to(cout, 8), device=dev, dtype=torch.bfloat16)
-        wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 64))
+        wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
         bp = pack_bias(b)
         flop = 2.0 * P * cout * cin * kh * kw
         line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"
         for t in a.tiles:
+            if (t == 5) != (cout <= 16) or (t in (6, 7) and cin % 64):
+                continue
             us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
             line += f" tile{t} {us:7.1f}us {flop / us / 1e6:6.1f}TF |"
             tot.setdefault(f"tile{t}", 0.0)

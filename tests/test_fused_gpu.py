@@ -23,23 +23,24 @@ def _bf(x):
 
 
 @pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5), (5, 1)])
-@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7])
 @pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
 def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     torch.manual_seed(0)
     B, H, W = 2, 11, 19
     kh, kw = k
     # input = cat[a (40 ch, stored in a 64-wide buffer at offset 8), b (32 ch)]
+    cb = 64 if tile in (6, 7) else 32   # 64-deep K tiles need 64-channel segments
     a_buf = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
-    b_buf = torch.randn(B, H, W, 32, device=cuda).to(torch.bfloat16)
+    b_buf = torch.randn(B, H, W, cb, device=cuda).to(torch.bfloat16)
     x = torch.cat([a_buf[..., 8:48], b_buf], -1).float().permute(0, 3, 1, 2)
     cout = 70
-    w = torch.randn(cout, 72, kh, kw, device=cuda) * 0.1
+    w = torch.randn(cout, 40 + cb, kh, kw, device=cuda) * 0.1
     b = torch.randn(cout, device=cuda)
     # segment 0 reads 64 channels from a_buf at offset 0: weights for [8,48) only
-    wp = pack_weight(w, [(64, [(0, 40, 8)]), (32, [(40, 32, 0)])], pad_to(cout, 64))
+    wp = pack_weight(w, [(64, [(0, 40, 8)]), (cb, [(40, cb, 0)])], pad_to(cout, 128))
     out = torch.full((B, H, W, 80), 7.0, device=cuda, dtype=torch.bfloat16)
-    conv_fused([(a_buf, 0, 64), (b_buf, 0, 32)], wp, pack_bias(b), kh, kw, cout, epi, out, 4,
+    conv_fused([(a_buf, 0, 64), (b_buf, 0, cb)], wp, pack_bias(b), kh, kw, cout, epi, out, 4,
                scale=0.25, tile=tile)
     ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2))
     if epi == EPI_RELU:
@@ -59,7 +60,7 @@ def test_gru_epilogues(cuda):
     wr = torch.randn(hd, 3 * hd, 1, 5, device=cuda) * 0.05
     wq = torch.randn(hd, 3 * hd, 1, 5, device=cuda) * 0.05
     bz, br, bq = (torch.randn(hd, device=cuda) * 0.1 for _ in range(3))
-    wzr = pack_weight(torch.cat([wz, wr]), [(3 * hd, [(0, 3 * hd, 0)])], 2 * hd)
+    wzr = pack_weight(torch.cat([wz, wr]), [(3 * hd, [(0, 3 * hd, 0)])], 128)
     z = torch.empty(B, H, W, hd, device=cuda, dtype=torch.bfloat16)
     rh = torch.empty_like(z)
     rs = torch.empty_like(z)
@@ -72,7 +73,7 @@ def test_gru_epilogues(cuda):
     torch.testing.assert_close(z.float().permute(0, 3, 1, 2), zr_, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(rs.float().permute(0, 3, 1, 2), r_, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(rh.float().permute(0, 3, 1, 2), r_ * h, atol=3e-2, rtol=3e-2)
-    wqp = pack_weight(wq, [(hd, [(0, hd, 0)]), (2 * hd, [(hd, 2 * hd, 0)])], hd)
+    wqp = pack_weight(wq, [(hd, [(0, hd, 0)]), (2 * hd, [(hd, 2 * hd, 0)])], 128)
     hx2 = hx.clone()
     conv_fused([(rh, 0, hd), (hx2, hd, 2 * hd)], wqp, pack_bias(bq), 1, 5, hd, EPI_GRU_Q, hx2, 0,
                aux1=hx2, a1off=0, aux2=z, a2off=0)
@@ -92,8 +93,12 @@ def test_flow_epilogue_and_flow_encode(cuda):
     b = torch.randn(2, device=cuda)
     coords = torch.randn(B, 2, H, W, device=cuda) * 3
     c0 = coords.clone()
-    conv_fused([(feat, 0, 64)], pack_weight(w, [(64, [(0, 64, 0)])], 64), pack_bias(b), 3, 3, 2, EPI_FLOW,
+    c1 = coords.clone()
+    conv_fused([(feat, 0, 64)], pack_weight(w, [(64, [(0, 64, 0)])], 128), pack_bias(b), 3, 3, 2, EPI_FLOW,
                coords)
+    conv_fused([(feat, 0, 64)], pack_weight(w, [(64, [(0, 64, 0)])], 128), pack_bias(b), 3, 3, 2, EPI_FLOW,
+               c1, tile=5)  # split-K small-N kernel
+    torch.testing.assert_close(c1, coords, atol=1e-3, rtol=1e-3)
     delta = F.conv2d(feat.float().permute(0, 3, 1, 2), _bf(w), b, padding=1)
     torch.testing.assert_close(coords, c0 + delta, atol=2e-2, rtol=2e-2)
     # flow encoder: relu(conv7x7(coords - grid)) and the flow itself into a slot
