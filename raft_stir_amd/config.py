@@ -26,6 +26,7 @@ class RAFTConfig:
     fnet_dim: int = 256
     # engine knobs (not in the reference): kernel choices for the GPU path
     fused_gru: bool = True             # fused HIP gate kernels in the ConvGRU
+    fused_train: bool = True           # whole-loop fused training engine (full RAFT, bf16)
     corr_dtype: str = "float32"        # storage dtype of the all-pairs pyramid
 
     @property
@@ -65,6 +66,7 @@ def resolve_config(args=None, **overrides) -> RAFTConfig:
         dropout=float(_get(args, "dropout", 0.0) or 0.0),
         corr_levels=4,
         fused_gru=bool(_get(args, "fused_gru", True)),
+        fused_train=bool(_get(args, "fused_train", True)),
         corr_dtype=str(_get(args, "corr_dtype", "float32")),
         **dims,
     )

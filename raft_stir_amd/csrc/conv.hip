@@ -38,6 +38,11 @@ enum Epi : int {
   EPI_GRU_ZR = 3,  // co < hd: z -> out ; co >= hd: r*h -> out2 (r -> out3 if set)
   EPI_GRU_Q = 4,   // h' = (1-z) h + z tanh(acc + b) -> out (q~ -> out2 if set)
   EPI_FLOW = 5,    // coords (fp32 NCHW) += acc + b   (co < 2)
+  // backward (dgrad) epilogues
+  EPI_RELU_BWD = 6,  // out(bf16) = v * (aux1 > 0)            (through the producer's ReLU)
+  EPI_ACC_F32 = 7,   // out(fp32) += v                        (gradient accumulation)
+  EPI_GRU_QBWD = 8,  // co < hd: drh = v -> out2(bf16)[co] = drh*h*r*(1-r) (dr_pre), out[co] += drh*r
+                     // co >= hd: out(fp32)[co] += v          (h = aux1, r = aux2)
 };
 
 struct Seg {
@@ -142,6 +147,40 @@ __device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM]
             const float q = tanhf_(v[j]);
             hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
             if (qs) qs[j] = f2bf(q);
+          }
+          break;
+        }
+        case EPI_RELU_BWD: {
+          const bf16_t* act = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
+          break;
+        }
+        case EPI_ACC_F32: {
+          float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (cb + j < a.Cout) o[j] += v[j];
+          break;
+        }
+        case EPI_GRU_QBWD: {
+          float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+          if (cb < a.hd) {
+            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+            const bf16_t* r = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+            bf16_t* drp = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float rv = bf2f(r[j]), hv = bf2f(h[j]);
+              drp[j] = f2bf(v[j] * hv * rv * (1.f - rv));
+              o[j] += v[j] * rv;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (cb + j < a.Cout) o[j] += v[j];
           }
           break;
         }
@@ -529,6 +568,47 @@ __global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ GRU gate backward
+// One ConvGRU pass h' = (1-z) h + z q~, q~ = tanh(q_pre), z = sigmoid(z_pre):
+//   dq_pre = dh' z (1 - q~^2)        -> dq (bf16, the q-conv dgrad/wgrad operand)
+//   dz_pre = dh' (q~ - h) z (1 - z)  -> dzr[:, 0:hd] (bf16)
+//   dh    <- dh' (1 - z)             (fp32, in place; the conv dgrads add to it)
+__global__ __launch_bounds__(256) void gru_gate_bwd_kernel(float* __restrict__ dh, int dhstr, const bf16_t* __restrict__ z,
+                                                           int zstr, const bf16_t* __restrict__ q, int qstr,
+                                                           const bf16_t* __restrict__ h, int hstr, int hoff,
+                                                           bf16_t* __restrict__ dq, int dqstr,
+                                                           bf16_t* __restrict__ dzr, int dzrstr, long P, int hd) {
+  const long total = P * hd;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / hd;
+    const int c = (int)(i - p * hd);
+    const float g = dh[p * dhstr + c];
+    const float zv = bf2f(z[p * zstr + c]), qv = bf2f(q[p * qstr + c]), hv = bf2f(h[p * hstr + hoff + c]);
+    dq[p * dqstr + c] = f2bf(g * zv * (1.f - qv * qv));
+    dzr[p * dzrstr + c] = f2bf(g * (qv - hv) * zv * (1.f - zv));
+    dh[p * dhstr + c] = g * (1.f - zv);
+  }
+}
+
+// Motion-encoder output gradient: d = G[:, off:off+n] * (act > 0) -> out (bf16, width
+// ostr, channels >= n zeroed), then G[:, off:off+nz] = 0 (consumed).
+__global__ __launch_bounds__(256) void relu_take_kernel(float* __restrict__ G, int gstr, int goff, int n, int nz,
+                                                        const bf16_t* __restrict__ act, int astr, int aoff,
+                                                        bf16_t* __restrict__ out, int ostr, long P) {
+  const long total = P * ostr;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / ostr;
+    const int c = (int)(i - p * ostr);
+    float v = 0.f;
+    if (c < n) {
+      const float g = G[p * gstr + goff + c];
+      v = bf2f(act[p * astr + aoff + c]) > 0.f ? g : 0.f;
+    }
+    out[i] = f2bf(v);
+    if (c < nz) G[p * gstr + goff + c] = 0.f;
+  }
+}
+
 }  // namespace conv
 
 // ------------------------------------------------------------------ launchers
@@ -599,6 +679,26 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
                        0, stream, a);
   }
+}
+
+static int egrid(long total) {
+  const long g = (total + 255) / 256;
+  return (int)(g < 16384 ? g : 16384);
+}
+
+void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
+                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd,
+                         hipStream_t stream) {
+  hipLaunchKernelGGL(conv::gru_gate_bwd_kernel, dim3(egrid(P * hd)), dim3(256), 0, stream, dh, dhstr,
+                     static_cast<const bf16_t*>(z), zstr, static_cast<const bf16_t*>(q), qstr,
+                     static_cast<const bf16_t*>(h), hstr, hoff, static_cast<bf16_t*>(dq), dqstr,
+                     static_cast<bf16_t*>(dzr), dzrstr, P, hd);
+}
+
+void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* act, int astr, int aoff, void* out,
+                      int ostr, long P, hipStream_t stream) {
+  hipLaunchKernelGGL(conv::relu_take_kernel, dim3(egrid(P * ostr)), dim3(256), 0, stream, G, gstr, goff, n, nz,
+                     static_cast<const bf16_t*>(act), astr, aoff, static_cast<bf16_t*>(out), ostr, P);
 }
 
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,

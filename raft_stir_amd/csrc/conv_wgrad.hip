@@ -44,12 +44,32 @@ struct Args {
   int kchunk;
 };
 
-__device__ __forceinline__ int tswz(int row, int chunk) { return row * 4 + (chunk ^ ((row >> 2) & 3)); }
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 64, BN = 64, BK = 32;
+// Transposed 4x16 read (gfx950 ds_read_b64_tr_b16): lane 4q+p of each 16-lane
+// group addresses row q, columns 4p..4p+3 of a 4-row x 16-column bf16 block;
+// lane i of the group receives column i of the 4 rows.
+__device__ __forceinline__ v4s_t tr16(const uint16_t* lds_base, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s_t*)((__attribute__((address_space(3))) char*)lds_base + byte_off));
+}
 
-__global__ __launch_bounds__(256) void wgrad_kernel(Args a) {
-  __shared__ uint4 lds[2][(BM + BN) * 4];  // rows of 32 pixels (4 x 16 B)
+constexpr int BN = 64, BK = 64;
+
+// Block: BM output channels x 64 input channels (one tap) x K split over
+// pixels; 4 waves (2 x 2), 64-pixel K steps staged in LDS in their natural
+// [pixel][channel] layout (16-byte rows copied as loaded) and read back as
+// MFMA fragments with the hardware transpose read.  Blocks of the first
+// N tile also accumulate the bias gradient (column sums of dY) from the
+// staging registers.
+template <int BM>
+__global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ db) {
+  constexpr int AROW = BM * 2 + 16, BROW = BN * 2 + 16;  // bytes per staged pixel row (+16 pad)
+  constexpr int CA = BM / 8, CB = BN / 8;                // 16-B chunks per row
+  constexpr int NA = BK * CA / 256, NB = BK * CB / 256;  // chunks per thread
+  constexpr int WM = BM / 2 / 16, WN = BN / 2 / 16;      // MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][BK * (AROW + BROW)];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int ntile = blockIdx.x;
@@ -60,8 +80,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a) {
   const int pend = min(a.P, pbeg + a.kchunk);
   const int H = a.H, W = a.W, HW = H * W;
   const int dy_ = tap / a.KW - a.PH, dx_ = tap % a.KW - a.PW;
+  const bool do_bias = db != nullptr && ntile == 0;
 
-  // segment holding channels [kb, kb + 64) of the concatenated input
   const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
   const int c01 = s0.C, c012 = s0.C + (a.nseg > 1 ? s1.C : 0);
   const int si = (kb >= c01) + (kb >= c012);
@@ -69,86 +89,131 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a) {
   const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);
   const int sper = si == 0 ? s0.period : (si == 1 ? s1.period : s2.period);
   const int cbase = kb - (si == 0 ? 0 : (si == 1 ? c01 : c012));
-
-  // staging assignment: thread -> (pixel row px = t / 8, channel group cg = t % 8).
-  // (macros, not lambdas: a lambda capturing the kernarg struct spills it to scratch)
-  const int spx = t >> 3, scg = t & 7;
-  const bf16_t* ybase = a.dy + a.yoff + m0 + scg * 8;
+  const bf16_t* ybase = a.dy + a.yoff + m0;
   const int ystr = a.ystr;
-  const uint4 zero = make_uint4(0, 0, 0, 0);
-  uint4 ry, rx;
-#define RS_WG_LOAD(P0)                                                                          \
-  do {                                                                                          \
-    const int p = (P0) + spx;                                                                   \
-    ry = zero;                                                                                  \
-    rx = zero;                                                                                  \
-    if (p < pend) {                                                                             \
-      ry = *reinterpret_cast<const uint4*>(ybase + (size_t)p * ystr);                           \
-      const int q = p % HW, y = q / W + dy_, x = q % W + dx_;                                   \
-      if (y >= 0 && y < H && x >= 0 && x < W) {                                                 \
-        const int src = (p - q) + y * W + x;                                                    \
-        rx = *reinterpret_cast<const uint4*>(sp + (size_t)(src % sper) * sst + cbase + scg * 8); \
-      }                                                                                         \
-    }                                                                                           \
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+  // chunk slot i of thread t: A (pixel (t + 256 i) / CA, channel group t % CA);
+  //                          B (pixel (t + 256 i) / CB, channel group t % CB)
+  const int acg = t % CA, bcg = t % CB;
+  u32x4_t ra[NA], rb[NB];
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+
+#define RS_WG_LOAD(P0)                                                                           \
+  do {                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                             \
+      const int p = (P0) + (t + 256 * i) / CA;                                                   \
+      const int pc = p < pend ? p : pbeg;                                                        \
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(ybase + (size_t)pc * ystr + acg * 8);      \
+      ra[i] = p < pend ? v : zero;                                                               \
+    }                                                                                            \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                             \
+      const int p = (P0) + (t + 256 * i) / CB;                                                   \
+      const int q = p % HW, y = q / W + dy_, x = q % W + dx_;                                    \
+      const bool ok = p < pend && y >= 0 && y < H && x >= 0 && x < W;                            \
+      const int src = ok ? (p - q) + y * W + x : 0;                                              \
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(sp + (size_t)(src % sper) * sst + cbase + bcg * 8); \
+      rb[i] = ok ? v : zero;                                                                     \
+    }                                                                                            \
   } while (0)
-  // transposed store: element j of the chunk -> row (cg*8 + j), pixel spx
-#define RS_WG_STORE(BUF)                                                                        \
-  do {                                                                                          \
-    uint16_t* A_ = reinterpret_cast<uint16_t*>(&lds[BUF][0]);                                   \
-    uint16_t* B_ = reinterpret_cast<uint16_t*>(&lds[BUF][BM * 4]);                              \
-    const uint32_t wy[4] = {ry.x, ry.y, ry.z, ry.w};                                            \
-    const uint32_t wx[4] = {rx.x, rx.y, rx.z, rx.w};                                            \
-    const int ch = spx >> 3, e = spx & 7;                                                       \
-    _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                             \
-      const int row = scg * 8 + j;                                                              \
-      A_[tswz(row, ch) * 8 + e] = (uint16_t)(j & 1 ? wy[j >> 1] >> 16 : wy[j >> 1] & 0xffff);   \
-      B_[tswz(row, ch) * 8 + e] = (uint16_t)(j & 1 ? wx[j >> 1] >> 16 : wx[j >> 1] & 0xffff);   \
-    }                                                                                           \
+#define RS_WG_STORE(BUF)                                                                         \
+  do {                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                             \
+      const int row = (t + 256 * i) / CA;                                                        \
+      *reinterpret_cast<u32x4_t*>(&lds[BUF][row * AROW + acg * 16]) = ra[i];                       \
+    }                                                                                            \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                             \
+      const int row = (t + 256 * i) / CB;                                                        \
+      *reinterpret_cast<u32x4_t*>(&lds[BUF][BK * AROW + row * BROW + bcg * 16]) = rb[i];           \
+    }                                                                                            \
+  } while (0)
+#define RS_WG_BIAS()                                                                             \
+  do {                                                                                           \
+    if (do_bias) {                                                                               \
+      _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                           \
+        bsum[0] += __uint_as_float(ra[i].x << 16);                                               \
+        bsum[1] += __uint_as_float(ra[i].x & 0xffff0000u);                                       \
+        bsum[2] += __uint_as_float(ra[i].y << 16);                                               \
+        bsum[3] += __uint_as_float(ra[i].y & 0xffff0000u);                                       \
+        bsum[4] += __uint_as_float(ra[i].z << 16);                                               \
+        bsum[5] += __uint_as_float(ra[i].z & 0xffff0000u);                                       \
+        bsum[6] += __uint_as_float(ra[i].w << 16);                                               \
+        bsum[7] += __uint_as_float(ra[i].w & 0xffff0000u);                                       \
+      }                                                                                          \
+    }                                                                                            \
   } while (0)
 
-  f32x4_t acc[2][2];
+  f32x4_t acc[WM][WN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int lr = lane & 15, lc = lane >> 4;
+  const int gi = lane & 15, g = lane >> 4;          // 16-lane group g, lane i in it
+  const int tq = gi >> 2, tp = gi & 3;              // tr16 address roles: row q, columns 4p..4p+3
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
   if (nsteps > 0) {
     RS_WG_LOAD(pbeg);
+    RS_WG_BIAS();
     RS_WG_STORE(0);
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
     if (s + 1 < nsteps) RS_WG_LOAD(pbeg + (s + 1) * BK);
-    uint4 fa[2], fb[2];
+    const uint16_t* base = reinterpret_cast<const uint16_t*>(&lds[buf][0]);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) fa[mt] = lds[buf][tswz(wm * 32 + mt * 16 + lr, lc)];
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      // rows (pixels) of this lane group's k-run: 32kk + 8g + {0..3} and + {4..7}
+      const int r0 = kk * 32 + 8 * g + tq;
+      bf16x8_t fa[WM], fb[WN];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) fb[nt] = lds[buf][BM * 4 + tswz(wn * 32 + nt * 16 + lr, lc)];
+      for (int mt = 0; mt < WM; ++mt) {
+        const int col = wm * (BM / 2) + mt * 16 + 4 * tp;
+        const v4s_t lo = tr16(base, r0 * AROW + col * 2);
+        const v4s_t hi = tr16(base, (r0 + 4) * AROW + col * 2);
+        fa[mt] = bf16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+      for (int nt = 0; nt < WN; ++nt) {
+        const int col = wn * (BN / 2) + nt * 16 + 4 * tp;
+        const v4s_t lo = tr16(base, BK * AROW + r0 * BROW + col * 2);
+        const v4s_t hi = tr16(base, BK * AROW + (r0 + 4) * BROW + col * 2);
+        fb[nt] = bf16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[mt]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[nt]),
-                                                              acc[mt][nt], 0, 0, 0);
-    if (s + 1 < nsteps) RS_WG_STORE(buf ^ 1);
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) {
+      RS_WG_BIAS();
+      RS_WG_STORE(buf ^ 1);
+    }
     __syncthreads();
   }
 #undef RS_WG_LOAD
 #undef RS_WG_STORE
+#undef RS_WG_BIAS
   if (nsteps == 0) return;
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int co = m0 + acg * 8 + j;
+      if (co < a.Cout) atomicAdd(db + co, bsum[j]);
+    }
+  }
   // C[co][k]: row = 4*(lane>>4) + j (co), col = lane & 15 (k)
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int co = m0 + wm * 32 + mt * 16 + (lane >> 4) * 4 + j;
-        const int k = kb + wn * 32 + nt * 16 + (lane & 15);
+        const int co = m0 + wm * (BM / 2) + mt * 16 + (lane >> 4) * 4 + j;
+        const int k = kb + wn * (BN / 2) + nt * 16 + (lane & 15);
         if (co < a.Cout) atomicAdd(a.dw + ((size_t)co * a.taps + tap) * a.Ktot + k, acc[mt][nt][j]);
       }
 }
@@ -167,7 +232,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 
 // convf1 weight gradient: dW[tap][ci][co] (the flow_encode layout [7][7][2][Cout])
 // += sum_p dF[p][co] * flow[p + off(tap)][ci], flow = coords - grid (fp32 NCHW),
-// and db[co] += sum_p dF[p][co].  Block = 64 pixels; thread (co, ci) keeps
+// and db[co] += sum_p dF[p][co].  Block = 512 pixels; thread (co, ci) keeps
 // 49 tap accumulators; per-block partials go out with atomics.
 __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict__ coords, int Bp, int H, int W,
                                                          const bf16_t* __restrict__ df,
@@ -175,7 +240,7 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
                                                          float* __restrict__ db) {
   const int HW = H * W;
   const int P = Bp * HW;
-  const int p0 = blockIdx.x * 64, p1 = min(P, p0 + 64);
+  const int p0 = blockIdx.x * 512, p1 = min(P, p0 + 512);
   for (int pair = threadIdx.x; pair < Cout * 2; pair += 256) {
     const int co = pair % Cout, ci = pair / Cout;
     float acc[49];
@@ -217,6 +282,7 @@ struct WgradLaunch {
   int nseg;
   int Bp, H, W, KH, KW, Ktot;
   float* dw;
+  float* db;  // optional: bias gradient (column sums of dY) fused in
 };
 
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
@@ -234,14 +300,18 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.KH = L.KH; a.KW = L.KW; a.PH = L.KH / 2; a.PW = L.KW / 2;
   a.Ktot = L.Ktot; a.taps = L.KH * L.KW;
   a.dw = L.dw;
+  const int bm = a.Cout > 64 ? 128 : 64;
   const int ntiles = a.taps * (a.Ktot / wgrad::BN);
-  const int mtiles = cdiv(a.Cout, wgrad::BM);
+  const int mtiles = cdiv(a.Cout, bm);
   int ksplit = cdiv(2048, ntiles * mtiles);
-  ksplit = max(1, min(ksplit, cdiv(a.P, 32 * 16)));
-  a.kchunk = round_up(cdiv(a.P, ksplit), 32);
+  ksplit = max(1, min(ksplit, cdiv(a.P, wgrad::BK * 8)));
+  a.kchunk = round_up(cdiv(a.P, ksplit), wgrad::BK);
   ksplit = cdiv(a.P, a.kchunk);
   dim3 grid(ntiles, mtiles, ksplit);
-  hipLaunchKernelGGL(wgrad::wgrad_kernel, grid, dim3(256), 0, stream, a);
+  if (bm == 128)
+    hipLaunchKernelGGL(wgrad::wgrad_kernel<128>, grid, dim3(256), 0, stream, a, L.db);
+  else
+    hipLaunchKernelGGL(wgrad::wgrad_kernel<64>, grid, dim3(256), 0, stream, a, L.db);
 }
 
 void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream) {
@@ -252,7 +322,7 @@ void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, 
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
                        float* db, hipStream_t stream) {
   const int P = Bp * H * W;
-  hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(cdiv(P, 64)), dim3(256), 0, stream, coords, Bp, H, W,
+  hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(cdiv(P, 512)), dim3(256), 0, stream, coords, Bp, H, W,
                      static_cast<const bf16_t*>(df), fstr, Cout, dw, db);
 }
 

@@ -89,8 +89,9 @@ template <typename GT>
 __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrMut gpyr, int levels,
                                                          const float* __restrict__ coords, int B,
                                                          int H1, int W1, int r,
-                                                         const GT* __restrict__ dout, long total) {
-  const int D = 2 * r + 1, K2 = D * D, CH = levels * K2;
+                                                         const GT* __restrict__ dout, long total,
+                                                         int dstride) {
+  const int D = 2 * r + 1, K2 = D * D;
   const int E = D + 1, E2 = E * E;  // integer cells per level
   const int N1 = H1 * W1;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrMut gpyr, int levels
     const int X = (int)bx - r + a, Y = (int)by - r + c;
     const int H = gpyr.H[l], W = gpyr.W[l];
     if (X < 0 || X >= W || Y < 0 || Y >= H) continue;
-    const GT* g = dout + pix * CH + l * K2;
+    const GT* g = dout + pix * dstride + l * K2;
     float acc = 0.f;
     // tap i = a uses this cell as its lower x-corner (weight 1-fx); tap a-1 as upper (fx)
 #pragma unroll
@@ -186,7 +187,8 @@ void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* W
 
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
-                            bool dout_bf16, hipStream_t stream) {
+                            bool dout_bf16, hipStream_t stream, int dstride) {
+  if (dstride <= 0) dstride = levels * (2 * r + 1) * (2 * r + 1);
   lookup::PyrMut p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? gpyr[l] : nullptr;
@@ -198,10 +200,10 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
   const int grid = lookup::grid_for(total);
   if (dout_bf16)
     hipLaunchKernelGGL(lookup::lookup_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<const bf16_t*>(dout), total);
+                       levels, coords, B, H1, W1, r, static_cast<const bf16_t*>(dout), total, dstride);
   else
     hipLaunchKernelGGL(lookup::lookup_bwd_kernel<float>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<const float*>(dout), total);
+                       levels, coords, B, H1, W1, r, static_cast<const float*>(dout), total, dstride);
 }
 
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,

@@ -25,7 +25,7 @@ void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* W
                             bool out_bf16, hipStream_t stream, int ostride);
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
-                            bool dout_bf16, hipStream_t stream);
+                            bool dout_bf16, hipStream_t stream, int dstride);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
                           float scale, hipStream_t stream);
 bool corr_otf_supported_channels(int C);
@@ -181,13 +181,13 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
   check_gpu(dout, "dout");
   check_dtype(dout, {at::kFloat, at::kBFloat16}, "dout");
   TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
-                  dout.size(3) == levels * D * D,
-              "dout must be (B,H1,W1,levels*(2r+1)^2)");
+                  dout.size(3) >= levels * D * D,
+              "dout must be (B,H1,W1,>=levels*(2r+1)^2) (rows may be K-padded)");
   const c10::DeviceGuard guard(coords.device());
   float* ptrs[4];
   for (int l = 0; l < levels; ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
-                             dout.data_ptr(), is_bf16(dout), cur_stream());
+                             dout.data_ptr(), is_bf16(dout), cur_stream(), dout.size(3));
 }
 
 void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {

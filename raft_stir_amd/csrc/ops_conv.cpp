@@ -30,19 +30,38 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
                      int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
                      hipStream_t stream);
+void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
+                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd,
+                         hipStream_t stream);
+void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* act, int astr, int aoff, void* out,
+                      int ostr, long P, hipStream_t stream);
+struct WgradLaunch {
+  const void* dy;
+  int ystr, yoff, Cout;
+  const void* seg_ptr[3];
+  int seg_C[3], seg_stride[3], seg_period[3];
+  int nseg;
+  int Bp, H, W, KH, KW, Ktot;
+  float* dw;
+  float* db;
+};
+void wgrad_launch(const WgradLaunch& L, hipStream_t stream);
+void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream);
+void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
+                       float* db, hipStream_t stream);
 }  // namespace rs
 
 namespace {
 using at::Tensor;
 
-constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5;
+constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8;
 
 hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
-void check_nhwc(const Tensor& t, int B, int H, int W, const char* n) {
+void check_nhwc(const Tensor& t, int B, int H, int W, const char* n, at::ScalarType dt = at::kBFloat16) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, n, ": contiguous NHWC GPU tensor required");
   TORCH_CHECK(t.size(0) == B && t.size(1) == H && t.size(2) == W, n, ": spatial shape mismatch");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, n, ": bf16 required");
+  TORCH_CHECK(t.scalar_type() == dt, n, ": ", dt, " required");
 }
 
 void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C,
@@ -104,7 +123,8 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
     TORCH_CHECK(Cout == 2, "conv_fused(flow): Cout must be 2");
     L.out = out.data_ptr(); L.ostr = 0; L.ooff = 0;
   } else {
-    check_nhwc(out, B, H, W, "out");
+    const bool f32out = epi == EPI_ACC_F32 || epi == EPI_GRU_QBWD;
+    check_nhwc(out, B, H, W, "out", f32out ? at::kFloat : at::kBFloat16);
     const int cw = epi == EPI_GRU_ZR ? hd : Cout;
     TORCH_CHECK(ooff >= 0 && ooff + cw <= out.size(3), "conv_fused: output window out of bounds");
     L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = ooff;
@@ -127,6 +147,15 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
     opt_nhwc(out2, o2off, Cout, "out2", &L.out2, &L.o2str, &L.o2off);
     opt_nhwc(aux1, a1off, Cout, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
     opt_nhwc(aux2, a2off, Cout, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
+  } else if (epi == EPI_RELU_BWD) {
+    TORCH_CHECK(aux1, "conv_fused(relu_bwd): needs aux1 (the ReLU output)");
+    opt_nhwc(aux1, a1off, Cout, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
+  } else if (epi == EPI_GRU_QBWD) {
+    TORCH_CHECK(hd % 4 == 0 && hd <= Cout && out2 && aux1 && aux2,
+                "conv_fused(gru_qbwd): needs out2 (dr_pre), aux1 (h), aux2 (r)");
+    opt_nhwc(out2, o2off, hd, "out2", &L.out2, &L.o2str, &L.o2off);
+    opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
+    opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
   rs::conv_launch(L, stream());
 }
@@ -159,9 +188,127 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
                       out.data_ptr(), out.size(3), ooff, fp, fstr, foff, stream());
 }
 
+// dW (fp32, [>=Cout][taps][Ktot], accumulated) += sum_p dY[p][yoff + co] X[p + tap][k]
+void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
+                at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH, int64_t KW,
+                const Tensor& dw, const c10::optional<Tensor>& db) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16,
+              "conv_wgrad: dy must be contiguous bf16 NHWC");
+  const int Bp = dy.size(0), H = dy.size(1), W = dy.size(2);
+  const int bm = Cout > 64 ? 128 : 64;
+  TORCH_CHECK(yoff >= 0 && yoff % 8 == 0 && yoff + (Cout + bm - 1) / bm * bm <= dy.size(3),
+              "conv_wgrad: dy channel window (rounded up to ", bm, ") out of bounds");
+  if (db) TORCH_CHECK(db->is_cuda() && db->scalar_type() == at::kFloat && db->numel() >= Cout, "conv_wgrad: db fp32");
+  TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size() &&
+                  seg_period.size() == segs.size(),
+              "conv_wgrad: segment spec");
+  rs::WgradLaunch L{};
+  int Ktot = 0;
+  for (size_t s = 0; s < 3; ++s) {
+    if (s < segs.size()) {
+      const Tensor& t = segs[s];
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 &&
+                      t.size(1) == H && t.size(2) == W,
+                  "conv_wgrad: segment must be contiguous bf16 NHWC with dy's spatial size");
+      const int per = seg_period[s];
+      TORCH_CHECK(per == t.size(0) * H * W && (Bp * H * W) % per == 0,
+                  "conv_wgrad: segment period must be its pixel count and divide dy's");
+      const int C = seg_C[s], off = seg_off[s];
+      TORCH_CHECK(C % 64 == 0 && off % 8 == 0 && off + C <= t.size(3), "conv_wgrad: segment window (C % 64)");
+      L.seg_ptr[s] = static_cast<const at::BFloat16*>(t.data_ptr()) + off;
+      L.seg_C[s] = C;
+      L.seg_stride[s] = t.size(3);
+      L.seg_period[s] = per;
+      Ktot += C;
+    } else {
+      L.seg_ptr[s] = L.seg_ptr[0];
+      L.seg_C[s] = 64;
+      L.seg_stride[s] = L.seg_stride[0];
+      L.seg_period[s] = L.seg_period[0];
+    }
+  }
+  TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.scalar_type() == at::kFloat && dw.dim() == 3 &&
+                  dw.size(0) >= Cout && dw.size(1) == KH * KW && dw.size(2) == Ktot,
+              "conv_wgrad: dw must be fp32 (>=Cout, taps, Ktot)");
+  const c10::DeviceGuard guard(dy.device());
+  L.dy = dy.data_ptr(); L.ystr = dy.size(3); L.yoff = yoff; L.Cout = Cout;
+  L.nseg = segs.size();
+  L.Bp = Bp; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.Ktot = Ktot;
+  L.dw = dw.data_ptr<float>();
+  L.db = db ? db->data_ptr<float>() : nullptr;
+  rs::wgrad_launch(L, stream());
+}
+
+void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.scalar_type() == at::kBFloat16, "colsum: bf16 dy");
+  TORCH_CHECK(yoff >= 0 && yoff + C <= dy.size(-1), "colsum: channel window");
+  TORCH_CHECK(db.is_cuda() && db.scalar_type() == at::kFloat && db.numel() >= C, "colsum: fp32 db");
+  const c10::DeviceGuard guard(dy.device());
+  const int P = dy.numel() / dy.size(-1);
+  rs::colsum_launch(dy.data_ptr(), dy.size(-1), yoff, C, P, db.data_ptr<float>(), stream());
+}
+
+void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const Tensor& db) {
+  TORCH_CHECK(coords.is_cuda() && coords.is_contiguous() && coords.scalar_type() == at::kFloat && coords.dim() == 4 &&
+                  coords.size(1) == 2,
+              "flow_wgrad: coords fp32 (B',2,H,W)");
+  const int Bp = coords.size(0), H = coords.size(2), W = coords.size(3);
+  TORCH_CHECK(df.is_cuda() && df.is_contiguous() && df.scalar_type() == at::kBFloat16 && df.dim() == 4 &&
+                  df.size(0) == Bp && df.size(1) == H && df.size(2) == W,
+              "flow_wgrad: df bf16 (B',H,W,C)");
+  const int Cout = db.numel();
+  TORCH_CHECK(Cout <= df.size(3) && Cout <= 128 && dw.numel() == 98 * Cout && dw.scalar_type() == at::kFloat &&
+                  db.scalar_type() == at::kFloat,
+              "flow_wgrad: dw fp32 [49][2][Cout], db fp32 [Cout]");
+  const c10::DeviceGuard guard(coords.device());
+  rs::flow_wgrad_launch(coords.data_ptr<float>(), Bp, H, W, df.data_ptr(), df.size(3), Cout, dw.data_ptr<float>(),
+                        db.data_ptr<float>(), stream());
+}
+
+// One ConvGRU pass backward through the gates (see csrc/conv.hip gru_gate_bwd_kernel).
+void gru_gate_bwd(const Tensor& dh, const Tensor& z, const Tensor& q, const Tensor& h, int64_t hoff, const Tensor& dq,
+                  const Tensor& dzr) {
+  const int hd = z.size(-1);
+  const int64_t P = z.numel() / hd;
+  auto chk = [&](const Tensor& t, at::ScalarType dt, int minc, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == dt && t.numel() / t.size(-1) == P &&
+                    t.size(-1) >= minc,
+                "gru_gate_bwd: ", n);
+  };
+  chk(dh, at::kFloat, hd, "dh (fp32)");
+  chk(q, at::kBFloat16, hd, "q");
+  chk(h, at::kBFloat16, hoff + hd, "h");
+  chk(dq, at::kBFloat16, hd, "dq");
+  chk(dzr, at::kBFloat16, hd, "dzr");
+  const c10::DeviceGuard guard(z.device());
+  rs::gru_gate_bwd_launch(dh.data_ptr<float>(), dh.size(-1), z.data_ptr(), hd, q.data_ptr(), q.size(-1), h.data_ptr(),
+                          h.size(-1), hoff, dq.data_ptr(), dq.size(-1), dzr.data_ptr(), dzr.size(-1), P, hd, stream());
+}
+
+// out = G[:, goff:goff+n] * (act[:, aoff:aoff+n] > 0) (zero-padded to out's width); G[:, goff:goff+nz] = 0
+void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tensor& act, int64_t aoff, const Tensor& out) {
+  const int64_t P = out.numel() / out.size(-1);
+  TORCH_CHECK(G.is_cuda() && G.is_contiguous() && G.scalar_type() == at::kFloat && G.numel() / G.size(-1) == P &&
+                  goff + std::max(n, nz) <= G.size(-1),
+              "relu_take: G");
+  TORCH_CHECK(act.is_contiguous() && act.scalar_type() == at::kBFloat16 && act.numel() / act.size(-1) == P &&
+                  aoff + n <= act.size(-1),
+              "relu_take: act");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kBFloat16 && n <= out.size(-1), "relu_take: out");
+  const c10::DeviceGuard guard(out.device());
+  rs::relu_take_launch(G.data_ptr<float>(), G.size(-1), goff, n, nz, act.data_ptr(), act.size(-1), aoff, out.data_ptr(),
+                       out.size(-1), P, stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
+        "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None) -> ()");
+  m.def("colsum(Tensor dy, int yoff, int C, Tensor(a!) db) -> ()");
+  m.def("flow_wgrad(Tensor coords, Tensor df, Tensor(a!) dw, Tensor(b!) db) -> ()");
+  m.def("gru_gate_bwd(Tensor(a!) dh, Tensor z, Tensor q, Tensor h, int hoff, Tensor(b!) dq, Tensor(c!) dzr) -> ()");
+  m.def("relu_take(Tensor(a!) G, int goff, int n, int nz, Tensor act, int aoff, Tensor(b!) out) -> ()");
   m.def("conv_fused(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, "
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile) -> ()");
@@ -172,4 +319,9 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("flow_encode", &flow_encode);
+  m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("colsum", &colsum);
+  m.impl("flow_wgrad", &flow_wgrad);
+  m.impl("gru_gate_bwd", &gru_gate_bwd);
+  m.impl("relu_take", &relu_take);
 }

@@ -1,0 +1,285 @@
+"""Fused TRAINING engine for the RAFT refinement loop (full RAFT, bf16).
+
+One ``torch.autograd.Function`` covers the whole 12-iteration refinement
+loop of reference core/raft.py:122-139 (update block of core/update.py).
+
+Forward: the same hand-written HIP launches as the inference engine
+(models/fused_update.py), but every activation a gradient needs is written
+into an [iters * B, H, W, C] slot instead of being overwritten:
+
+  S.corr, S.c1, S.f1, S.mot  motion-encoder inputs / ReLU outputs
+  S.hx[i] = [h_i | motion_i (126) | flow_i (2)]   (iters + 1 slots: h after pass 2)
+  S.h1                        h after the first SepConvGRU pass
+  S.z / S.r / S.q / S.rh      GRU gates, tanh(q), r*h per pass
+  S.head, S.mask              flow-head/mask hidden (ReLU), convex mask
+  S.cin / S.cout              coords before / after each update
+
+Backward, iteration by iteration in reverse (dgrads = the forward conv kernel
+with transposed + flipped packed weights and gradient epilogues):
+
+  convex_upsample_backward -> d mask, d flow
+  mask2 / flow dgrad (through the hidden ReLU)  -> d head
+  head dgrad             -> dh  (fp32, accumulated with dh of iteration i+1)
+  GRU pass 2, pass 1     -> gate backward kernel, q-conv dgrad with the
+                            r-gate epilogue, zr-conv dgrad (fp32 accumulation
+                            into G = [dh | d inp | d motion])
+  motion encoder dgrads  -> d corr -> pyramid window-lookup backward
+                            (into the CorrState pyramid gradient; the volume
+                            node folds it into d fmap1 / d fmap2 afterwards)
+
+Every conv's weight gradient is then ONE batched MFMA GEMM over all
+iterations' pixels (csrc/conv_wgrad.hip) instead of 12 per-iteration GEMMs
+and 12 accumulations, and every bias gradient one column sum.
+
+Numerics: bf16 operands, fp32 accumulation everywhere, fp32 gradient
+accumulators for the recurrent state -- the same contract as the reference's
+autocast training (which used fp16).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import _ext
+from ..ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR, EPI_RELU,
+                        EPI_RELU_BWD, EPI_SCALE, conv_fused, pack_bias, pack_weight, pad_to)
+
+R = torch.ops.raft_stir
+HD = 128          # hidden dim (full RAFT)
+CORR_C = 324
+CORR_PAD = 384
+
+
+class _PConv:
+    """A conv of the update block: forward packing, dgrad packing, grad unpacking."""
+
+    def __init__(self, convs, segs, scale=1.0):
+        self.convs = convs if isinstance(convs, (list, tuple)) else [convs]
+        self.segs = segs          # [(C, [(w0, n, s0), ...]), ...] as in pack_weight
+        self.scale = scale        # output scale folded into the epilogue (mask x 0.25)
+        w0 = self.convs[0].weight
+        self.kh, self.kw = w0.shape[2], w0.shape[3]
+        self.cout = sum(c.weight.shape[0] for c in self.convs)
+        self.cin = w0.shape[1]
+        self.ktot = sum(c for c, _ in segs)
+
+    @torch.no_grad()
+    def pack(self):
+        weight = torch.cat([c.weight for c in self.convs], 0)
+        bias = torch.cat([c.bias for c in self.convs], 0)
+        self.w = pack_weight(weight, self.segs, pad_to(self.cout, 128))
+        self.b = pack_bias(bias)
+        # dgrad: Wd[k][tap'][co] = scale * W[co][taps-1-tap'][k], co padded to 64
+        cy = pad_to(self.cout, 64)
+        wd = self.w[:cy].float().flip(1).permute(2, 1, 0) * self.scale
+        out = torch.zeros(pad_to(self.ktot, 128), wd.shape[1], cy, device=wd.device, dtype=torch.float32)
+        out[:self.ktot] = wd
+        self.wd = out.to(torch.bfloat16).contiguous()
+        self.cy = cy
+
+    def zero_grads(self, dev):
+        self.dw = torch.zeros(pad_to(self.cout, 128), self.kh * self.kw, self.ktot, device=dev)
+        self.db = torch.zeros(self.cout, device=dev)
+
+    def unpack_grads(self):
+        """packed [Cout][taps][Ktot] grads -> one (dW, db) per original conv."""
+        taps = self.kh * self.kw
+        gw = torch.zeros(self.cout, taps, self.cin, device=self.dw.device)
+        kb = 0
+        for c, pieces in self.segs:
+            for w0, n, s0 in pieces:
+                gw[:, :, w0:w0 + n] = self.dw[:self.cout, :, kb + s0:kb + s0 + n]
+            kb += c
+        gw = gw.reshape(self.cout, self.kh, self.kw, self.cin).permute(0, 3, 1, 2) * self.scale
+        db = self.db * self.scale
+        out, r0 = [], 0
+        for c in self.convs:
+            n = c.weight.shape[0]
+            out.append((gw[r0:r0 + n].contiguous(), db[r0:r0 + n].contiguous()))
+            r0 += n
+        return out
+
+
+class FusedTrainEngine:
+    def __init__(self, model):
+        self.model = model
+        ub = model.update_block
+        enc, g = ub.encoder, ub.gru
+        full = lambda c: [(c, [(0, c, 0)])]
+        gru_segs = [(HD, [(0, HD, 0)]), (128, [(HD, 128, 0)]), (128, [(HD + 128, 128, 0)])]
+        self.c1 = _PConv(enc.convc1, [(CORR_PAD, [(0, CORR_C, 0)])])
+        self.c2 = _PConv(enc.convc2, full(256))
+        self.f2 = _PConv(enc.convf2, full(128))
+        self.cv = _PConv(enc.conv, full(256))
+        self.zr = [_PConv([g.convz1, g.convr1], gru_segs), _PConv([g.convz2, g.convr2], gru_segs)]
+        self.q = [_PConv(g.convq1, gru_segs), _PConv(g.convq2, gru_segs)]
+        self.head = _PConv([ub.flow_head.conv1, ub.mask[0]], full(HD))
+        self.flow = _PConv(ub.flow_head.conv2, full(256))
+        self.mask2 = _PConv(ub.mask[2], full(256), scale=0.25)
+        self.convs = [self.c1, self.c2, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow, self.mask2]
+        self.f1 = enc.convf1
+        # parameter order handed to autograd (grads are returned in this order)
+        self.params = []
+        for pc in self.convs:
+            for c in pc.convs:
+                self.params += [c.weight, c.bias]
+        self.params += [self.f1.weight, self.f1.bias]
+        self._bufs = {}
+
+    @staticmethod
+    def eligible(model, image, corr_fn) -> bool:
+        return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
+                and model.cfg.mixed_precision and model.cfg.fused_gru and not model.cfg.small
+                and getattr(corr_fn, "hip", False) and _ext.use_hip(image)
+                and getattr(model.cfg, "fused_train", True))
+
+    def buffers(self, B, H, W, iters, dev):
+        key = (B, H, W, iters, dev)
+        S = self._bufs.get(key)
+        if S is None:
+            n = iters * B
+            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=torch.bfloat16)
+            S = dict(
+                corr=e(n, CORR_PAD), c1=e(n, 256), f1=e(n, 128), mot=e(n, 256), hx=e(n + B, 256), h1=e(n, HD),
+                z=[e(n, HD), e(n, HD)], r=[e(n, HD), e(n, HD)], q=[e(n, HD), e(n, HD)], rh=[e(n, HD), e(n, HD)],
+                head=e(n, 512), mask=e(n, 576), inp=e(B, 128),
+                cin=torch.empty(n, 2, H, W, device=dev), cout=torch.empty(n, 2, H, W, device=dev),
+                # gradient (dY) slots
+                d_mask=e(n, 640), d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
+                d_head=e(n, 512), d_zr=[e(n, 256), e(n, 256)], d_q=[e(n, HD), e(n, HD)], d_conv=e(n, 128),
+                d_c2f2=e(n, 256), d_c1=e(n, 256), d_f1=e(n, 128), d_corr=e(B, CORR_PAD),
+                G=torch.empty(B, H, W, 384, device=dev),
+            )
+            self._bufs = {key: S}  # one shape at a time (training crops are fixed)
+        return S
+
+
+class FusedTrainLoop(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, *params):
+        for pc in eng.convs:
+            pc.pack()
+        f1w = eng.f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()
+        f1b = eng.f1.bias.detach().float().contiguous()
+        B, _, H, W = coords1.shape
+        dev = coords1.device
+        S = eng.buffers(B, H, W, iters, dev)
+        sl = lambda t, i: t[i * B:(i + 1) * B]
+        S["hx"][:B, ..., :HD].copy_(net.permute(0, 2, 3, 1))
+        S["inp"].copy_(inp.permute(0, 2, 3, 1))
+        coords = coords1.detach().float().contiguous().clone()
+        c0 = coords0.detach().float().contiguous()
+        inpb = S["inp"]
+        preds = []
+        for i in range(iters):
+            hx, hx1 = sl(S["hx"], i), sl(S["hx"], i + 1)
+            sl(S["cin"], i).copy_(coords)
+            R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+            R.flow_encode(coords, f1w, f1b, sl(S["f1"], i), 0, hx, 254)
+            conv_fused([(sl(S["corr"], i), 0, CORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, 256, EPI_RELU, sl(S["c1"], i))
+            conv_fused([(sl(S["c1"], i), 0, 256)], eng.c2.w, eng.c2.b, 3, 3, 192, EPI_RELU, sl(S["mot"], i), 0)
+            conv_fused([(sl(S["f1"], i), 0, 128)], eng.f2.w, eng.f2.b, 3, 3, 64, EPI_RELU, sl(S["mot"], i), 192)
+            conv_fused([(sl(S["mot"], i), 0, 256)], eng.cv.w, eng.cv.b, 3, 3, 126, EPI_RELU, hx, HD)
+            h_in = [(hx, 0), (sl(S["h1"], i), 0)]
+            h_out = [(sl(S["h1"], i), 0), (hx1, 0)]
+            for p in range(2):
+                hb, ho = h_in[p]
+                z, r, q, rh = (sl(S[k][p], i) for k in ("z", "r", "q", "rh"))
+                conv_fused([(hb, ho, HD), (inpb, 0, 128), (hx, HD, 128)], eng.zr[p].w, eng.zr[p].b, eng.zr[p].kh,
+                           eng.zr[p].kw, 2 * HD, EPI_GRU_ZR, z, 0, hd=HD, out2=rh, out3=r, aux1=hb, a1off=ho)
+                ob, oo = h_out[p]
+                conv_fused([(rh, 0, HD), (inpb, 0, 128), (hx, HD, 128)], eng.q[p].w, eng.q[p].b, eng.q[p].kh,
+                           eng.q[p].kw, HD, EPI_GRU_Q, ob, oo, out2=q, aux1=hb, a1off=ho, aux2=z)
+            head = sl(S["head"], i)
+            conv_fused([(hx1, 0, HD)], eng.head.w, eng.head.b, 3, 3, 512, EPI_RELU, head, 0)
+            conv_fused([(head, 0, 256)], eng.flow.w, eng.flow.b, 3, 3, 2, EPI_FLOW, coords)
+            mask = sl(S["mask"], i)
+            conv_fused([(head, 256, 256)], eng.mask2.w, eng.mask2.b, 1, 1, 576, EPI_SCALE, mask, 0, scale=0.25)
+            sl(S["cout"], i).copy_(coords)
+            preds.append(R.convex_upsample(coords - c0, mask))
+        ctx.eng, ctx.state, ctx.S, ctx.iters = eng, corr_state, S, iters
+        ctx.c0 = c0
+        ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
+        return tuple(preds)
+
+    @staticmethod
+    def backward(ctx, *gpreds):
+        eng, st, S, iters = ctx.eng, ctx.state, ctx.S, ctx.iters
+        c0 = ctx.c0
+        B, H, W = S["inp"].shape[:3]
+        dev = c0.device
+        sl = lambda t, i: t[i * B:(i + 1) * B]
+        if st.gpyr is None:
+            st.gpyr = [torch.zeros_like(p) for p in st.pyr]
+        G = S["G"]
+        G.zero_()
+        inpb = S["inp"]
+        for i in reversed(range(iters)):
+            g = gpreds[i]
+            if g is None:
+                g = torch.zeros(B, 2, 8 * H, 8 * W, device=dev)
+            hx, hx1, head = sl(S["hx"], i), sl(S["hx"], i + 1), sl(S["head"], i)
+            dflow, dmask = R.convex_upsample_backward(sl(S["cout"], i) - c0, sl(S["mask"], i), g.contiguous())
+            dm, df, dh = sl(S["d_mask"], i), sl(S["d_flow"], i), sl(S["d_head"], i)
+            dm[..., :576].copy_(dmask)
+            df[..., :2].copy_(dflow.permute(0, 2, 3, 1))
+            conv_fused([(dm, 0, 576)], eng.mask2.wd, None, 1, 1, 256, EPI_RELU_BWD, dh, 256, aux1=head, a1off=256)
+            conv_fused([(df, 0, 64)], eng.flow.wd, None, 3, 3, 256, EPI_RELU_BWD, dh, 0, aux1=head, a1off=0)
+            conv_fused([(dh, 0, 512)], eng.head.wd, None, 3, 3, HD, EPI_ACC_F32, G, 0)
+            h_in = [(hx, 0), (sl(S["h1"], i), 0)]
+            for p in (1, 0):
+                hb, ho = h_in[p]
+                z, r, q = sl(S["z"][p], i), sl(S["r"][p], i), sl(S["q"][p], i)
+                dq, dzr = sl(S["d_q"][p], i), sl(S["d_zr"][p], i)
+                R.gru_gate_bwd(G, z, q, hb, ho, dq, dzr)
+                conv_fused([(dq, 0, HD)], eng.q[p].wd, None, eng.q[p].kh, eng.q[p].kw, 384, EPI_GRU_QBWD, G, 0,
+                           hd=HD, out2=dzr, o2off=HD, aux1=hb, a1off=ho, aux2=r)
+                conv_fused([(dzr, 0, 256)], eng.zr[p].wd, None, eng.zr[p].kh, eng.zr[p].kw, 384, EPI_ACC_F32, G, 0)
+            dcv = sl(S["d_conv"], i)
+            R.relu_take(G, 256, 126, 128, hx, HD, dcv)
+            dc2f2 = sl(S["d_c2f2"], i)
+            conv_fused([(dcv, 0, 128)], eng.cv.wd, None, 3, 3, 256, EPI_RELU_BWD, dc2f2, 0, aux1=sl(S["mot"], i))
+            dc1 = sl(S["d_c1"], i)
+            conv_fused([(dc2f2, 0, 192)], eng.c2.wd, None, 3, 3, 256, EPI_RELU_BWD, dc1, 0, aux1=sl(S["c1"], i))
+            conv_fused([(dc2f2, 192, 64)], eng.f2.wd, None, 3, 3, 128, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
+                       aux1=sl(S["f1"], i))
+            conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, S["d_corr"], 0)
+            R.corr_lookup_backward(st.gpyr, sl(S["cin"], i), st.radius, S["d_corr"])
+
+        # ---------------- weight / bias gradients, batched over all iterations
+        n = iters * B
+        P_all = n * H * W
+        P_inp = B * H * W
+        for pc in eng.convs:
+            pc.zero_grads(dev)
+        hxs = S["hx"][:n]
+
+        def wg(pc, dy, yoff, segs):
+            # weight gradient + fused bias gradient (column sums of dY)
+            R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
+                         [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db)
+
+        wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
+        wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
+        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)])
+        hins = [hxs, S["h1"]]
+        for p in range(2):
+            wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
+            wg(eng.q[p], S["d_q"][p], 0, [(S["rh"][p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
+        wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)])
+        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)])
+        wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
+        wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
+        dwf = torch.zeros(49, 2, 128, device=dev)
+        dbf = torch.zeros(128, device=dev)
+        R.flow_wgrad(S["cin"], S["d_f1"], dwf, dbf)
+
+        grads = []
+        for pc in eng.convs:
+            for gw, gb in pc.unpack_grads():
+                grads += [gw, gb]
+        grads += [dwf.reshape(7, 7, 2, 128).permute(3, 2, 0, 1).contiguous(), dbf]
+        grads = [gr.to(p.dtype) for gr, p in zip(grads, eng.params)]
+        d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
+        d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
+        token_grad = torch.zeros((), device=dev)
+        return (None, None, token_grad, d_net, d_inp, None, None, None, *grads)

@@ -18,6 +18,10 @@ Engine differences (outputs unchanged):
   * GPU inference (no autograd, bf16) runs the refinement loop through the
     fused engine of models/fused_update.py: ~12 hand-written HIP launches per
     iteration over persistent NHWC buffers instead of the module graph.
+  * GPU training (full RAFT, bf16) runs it as ONE autograd node
+    (models/fused_train.py): fused forward kernels saving activations, a
+    hand-written backward (dgrad convs with gradient epilogues, gate
+    backward kernels) and weight gradients batched over all iterations.
 """
 from __future__ import annotations
 
@@ -32,6 +36,7 @@ from ..ops.upsample import convex_upsample, upflow8
 from .corr import CorrBlock, AlternateCorrBlock
 from .extractor import BasicEncoder, SmallEncoder
 from .fused_update import FusedUpdate
+from .fused_train import FusedTrainEngine, FusedTrainLoop
 from .update import BasicUpdateBlock, SmallUpdateBlock
 
 
@@ -58,6 +63,13 @@ class RAFT(nn.Module):
         for m in self.modules():
             if hasattr(m, "fused") and m is not self:
                 m.fused = enabled
+
+    def _train_engine(self):
+        eng = self.__dict__.get("_fused_train")
+        if eng is None or eng.model is not self:
+            eng = FusedTrainEngine(self)
+            self.__dict__["_fused_train"] = eng
+        return eng
 
     def _fused_engine(self):
         eng = self.__dict__.get("_fused")
@@ -122,6 +134,12 @@ class RAFT(nn.Module):
             coords0, coords1 = self.initialize_flow(image1)
             if flow_init is not None:
                 coords1 = coords1 + flow_init
+
+            if not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn):
+                eng = self._train_engine()
+                preds = FusedTrainLoop.apply(eng, corr_fn.state, corr_fn.token, net, inp, coords0, coords1,
+                                             iters, *eng.params)
+                return list(preds)
 
             if FusedUpdate.eligible(self, image1, corr_fn):
                 eng = self._fused_engine()

@@ -14,7 +14,8 @@ from typing import List, Sequence, Tuple
 
 import torch
 
-EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_GRU_ZR, EPI_GRU_Q, EPI_FLOW = range(6)
+(EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_GRU_ZR, EPI_GRU_Q, EPI_FLOW,
+ EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD) = range(9)
 
 Piece = Tuple[int, int, int]          # (weight in-channel start, length, segment channel offset)
 SegSpec = Tuple[int, Sequence[Piece]]  # (segment channels read (multiple of 32), pieces)

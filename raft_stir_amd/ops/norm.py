@@ -84,13 +84,14 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None)
         residual = residual.contiguous(memory_format=_CL)
     xn = _nhwc(x)
     if isinstance(norm, nn.InstanceNorm2d):
-        mean, rstd = torch.ops.raft_stir.norm_stats(xn, True, norm.eps)
+        with torch.no_grad():  # the stats' gradient is part of _NormAct.backward
+            mean, rstd = torch.ops.raft_stir.norm_stats(xn, True, norm.eps)
         return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True)
     # BatchNorm2d
     batch_stats = norm.training
     if batch_stats:
-        mean, rstd = torch.ops.raft_stir.norm_stats(xn, False, norm.eps)
         with torch.no_grad():
+            mean, rstd = torch.ops.raft_stir.norm_stats(xn, False, norm.eps)
             n = x.numel() // x.shape[1]
             var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
             unbiased = var * (n / max(n - 1, 1))

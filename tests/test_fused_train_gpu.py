@@ -1,0 +1,99 @@
+"""Fused training engine (models/fused_train.py, csrc/conv_wgrad.hip) vs the
+module-graph autograd path and plain fp32 PyTorch."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from raft_stir_amd.config import make_args
+from raft_stir_amd.models import RAFT
+from raft_stir_amd.ops.conv import pad_to
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5)])
+def test_wgrad_batched_with_broadcast_segment(cuda, k):
+    """dW over (iters*B) pixels; segment 1 is broadcast over the iteration dim."""
+    torch.manual_seed(0)
+    iters, B, H, W = 3, 2, 9, 14
+    kh, kw = k
+    cout = 70
+    xa = torch.randn(iters * B, H, W, 128, device=cuda).to(torch.bfloat16)   # per-iteration
+    xb = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)            # broadcast
+    dy = torch.randn(iters * B, H, W, 128, device=cuda).to(torch.bfloat16)   # 70 real channels at offset 0
+    dw = torch.zeros(128, kh * kw, 64 + 64, device=cuda)
+    # segment 0: xa channels [64, 128); segment 1: xb channels [0, 64)
+    db2 = torch.zeros(cout, device=cuda)
+    torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [xa, xb], [64, 0], [64, 64], [iters * B * H * W, B * H * W],
+                                   kh, kw, dw, db2)
+    x = torch.cat([xa[..., 64:], xb.repeat(iters, 1, 1, 1)], -1).float().permute(0, 3, 1, 2).requires_grad_(False)
+    w = torch.zeros(cout, 128, kh, kw, device=cuda, requires_grad=True)
+    y = F.conv2d(x, w, padding=(kh // 2, kw // 2))
+    y.backward(dy[..., :cout].float().permute(0, 3, 1, 2))
+    want = w.grad.permute(0, 2, 3, 1).reshape(cout, kh * kw, 128)
+    torch.testing.assert_close(dw[:cout], want, atol=5e-2, rtol=1e-2)
+    assert dw[cout:].abs().max() == 0
+    db = torch.zeros(cout, device=cuda)
+    torch.ops.raft_stir.colsum(dy, 0, cout, db)
+    torch.testing.assert_close(db, dy[..., :cout].float().sum((0, 1, 2)), atol=5e-2, rtol=1e-3)
+    torch.testing.assert_close(db2, db, atol=5e-2, rtol=1e-3)   # bias fused into the wgrad kernel
+
+
+def test_flow_wgrad(cuda):
+    torch.manual_seed(1)
+    n, H, W = 4, 10, 13
+    from raft_stir_amd.ops.reference import coords_grid
+    coords = coords_grid(n, H, W, device=cuda) + torch.randn(n, 2, H, W, device=cuda) * 3
+    df = torch.randn(n, H, W, 128, device=cuda).to(torch.bfloat16)
+    dw = torch.zeros(49, 2, 128, device=cuda)
+    db = torch.zeros(128, device=cuda)
+    torch.ops.raft_stir.flow_wgrad(coords, df, dw, db)
+    flow = coords - coords_grid(n, H, W, device=cuda)
+    w = torch.zeros(128, 2, 7, 7, device=cuda, requires_grad=True)
+    b = torch.zeros(128, device=cuda, requires_grad=True)
+    F.conv2d(flow, w, b, padding=3).backward(df.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dw.reshape(7, 7, 2, 128).permute(3, 2, 0, 1), w.grad, atol=1e-2, rtol=1e-3)
+    torch.testing.assert_close(db, b.grad, atol=1e-2, rtol=1e-3)
+
+
+def _grads(model):
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+def test_fused_training_matches_module_graph(cuda):
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.train.loss import sequence_loss
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).train()
+    ref = copy.deepcopy(m)
+    ref.cfg = ref.cfg.__class__(**{**ref.cfg.to_dict(), "fused_train": False})
+    i1, i2, flow, valid = make_batch(2, 192, 256, seed=2, device=cuda)
+    res = {}
+    for name, net in (("fused", m), ("ref", ref)):
+        preds = net(i1, i2, iters=6)
+        assert len(preds) == 6
+        loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+        loss.backward()
+        res[name] = (loss.item(), [p.detach() for p in preds], _grads(net))
+    lf, pf, gf = res["fused"]
+    lr, pr, gr = res["ref"]
+    assert abs(lf - lr) < 2e-2 * abs(lr) + 1e-2, (lf, lr)
+    for a, b in zip(pf, pr):
+        assert (a - b).norm(dim=1).mean() < 0.1
+    assert gf.keys() == gr.keys()
+    bad = []
+    for k in gr:
+        a, b = gf[k].flatten(), gr[k].flatten()
+        # biases of encoder convs followed by Instance/BatchNorm (train mode)
+        # have an exactly-zero true gradient (the norm removes them): both
+        # paths only carry round-off there
+        normed = k.split(".")[0] in ("fnet", "cnet") and k.endswith(".bias") and k not in (
+            "fnet.conv2.bias", "cnet.conv2.bias")
+        if b.norm() < 1e-8 or normed:
+            continue
+        cos = F.cosine_similarity(a, b, dim=0).item()
+        if cos < 0.98:
+            bad.append((k, round(cos, 4), (a.norm() / b.norm()).item()))
+    assert not bad, bad
