@@ -232,37 +232,54 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 
 // convf1 weight gradient: dW[tap][ci][co] (the flow_encode layout [7][7][2][Cout])
 // += sum_p dF[p][co] * flow[p + off(tap)][ci], flow = coords - grid (fp32 NCHW),
-// and db[co] += sum_p dF[p][co].  Block = 512 pixels; thread (co, ci) keeps
-// 49 tap accumulators; per-block partials go out with atomics.
+// and db[co] += sum_p dF[p][co].  K = 98 per output: a VALU kernel.
+// Block = ROWS image rows of one image; the flow rows they touch (ROWS + 6,
+// zero-padded by 3 columns) are staged in LDS; thread (co, ci) walks each
+// row with a 7-wide sliding window in registers (1 LDS read + 1 dF read per
+// 7 FMAs) and keeps 49 tap accumulators; one atomic per output per block.
+constexpr int FROWS = 8;
 __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict__ coords, int Bp, int H, int W,
-                                                         const bf16_t* __restrict__ df,
-                                                         int fstr, int Cout, float* __restrict__ dw,
-                                                         float* __restrict__ db) {
-  const int HW = H * W;
-  const int P = Bp * HW;
-  const int p0 = blockIdx.x * 512, p1 = min(P, p0 + 512);
-  for (int pair = threadIdx.x; pair < Cout * 2; pair += 256) {
+                                                         const bf16_t* __restrict__ df, int fstr, int Cout,
+                                                         float* __restrict__ dw, float* __restrict__ db) {
+  extern __shared__ float fl[];  // [2][FROWS + 6][W + 6]
+  const int HW = H * W, WP = W + 6, RP = FROWS + 6;
+  const int rblocks = cdiv(H, FROWS);
+  const int b = blockIdx.x / rblocks, y0 = (blockIdx.x % rblocks) * FROWS;
+  for (int i = threadIdx.x; i < 2 * RP * WP; i += blockDim.x) {
+    const int ci = i / (RP * WP), rem = i % (RP * WP), ry = rem / WP, rx = rem % WP;
+    const int y = y0 + ry - 3, x = rx - 3;
+    float v = 0.f;
+    if (y >= 0 && y < H && x >= 0 && x < W)
+      v = coords[((size_t)b * 2 + ci) * HW + y * W + x] - (ci == 0 ? (float)x : (float)y);
+    fl[i] = v;
+  }
+  __syncthreads();
+  for (int pair = threadIdx.x; pair < Cout * 2; pair += blockDim.x) {
     const int co = pair % Cout, ci = pair / Cout;
+    const float* F = fl + ci * RP * WP;
     float acc[49];
 #pragma unroll
     for (int i = 0; i < 49; ++i) acc[i] = 0.f;
     float bsum = 0.f;
-    for (int p = p0; p < p1; ++p) {
-      const float g = bf2f(df[(size_t)p * fstr + co]);
-      if (ci == 0) bsum += g;
-      if (g == 0.f) continue;
-      const int q = p % HW, y = q / W, x = q % W;
-      const float* cp = coords + ((size_t)(p / HW) * 2 + ci) * HW;
+    for (int r = 0; r < FROWS && y0 + r < H; ++r) {
+      const bf16_t* grow = df + ((size_t)b * HW + (size_t)(y0 + r) * W) * fstr + co;
+      if (ci == 0)
+        for (int x = 0; x < W; ++x) bsum += bf2f(grow[(size_t)x * fstr]);
 #pragma unroll
       for (int ky = 0; ky < 7; ++ky) {
-        const int yy = y + ky - 3;
-        if (yy < 0 || yy >= H) continue;
-#pragma unroll
-        for (int kx = 0; kx < 7; ++kx) {
-          const int xx = x + kx - 3;
-          if (xx < 0 || xx >= W) continue;
-          const float f = cp[yy * W + xx] - (ci == 0 ? (float)xx : (float)yy);
-          acc[ky * 7 + kx] += g * f;
+        const float* frow = F + (r + ky) * WP;  // padded row: column x + kx of the image at index x + kx
+        float w0 = frow[0], w1 = frow[1], w2 = frow[2], w3 = frow[3], w4 = frow[4], w5 = frow[5];
+        for (int x = 0; x < W; ++x) {
+          const float w6 = frow[x + 6];
+          const float g = bf2f(grow[(size_t)x * fstr]);
+          acc[ky * 7 + 0] += g * w0;
+          acc[ky * 7 + 1] += g * w1;
+          acc[ky * 7 + 2] += g * w2;
+          acc[ky * 7 + 3] += g * w3;
+          acc[ky * 7 + 4] += g * w4;
+          acc[ky * 7 + 5] += g * w5;
+          acc[ky * 7 + 6] += g * w6;
+          w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
         }
       }
     }
@@ -321,8 +338,9 @@ void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, 
 
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
                        float* db, hipStream_t stream) {
-  const int P = Bp * H * W;
-  hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(cdiv(P, 512)), dim3(256), 0, stream, coords, Bp, H, W,
+  const int blocks = Bp * cdiv(H, wgrad::FROWS);
+  const size_t lds = sizeof(float) * 2 * (wgrad::FROWS + 6) * (W + 6);
+  hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(blocks), dim3(256), lds, stream, coords, Bp, H, W,
                      static_cast<const bf16_t*>(df), fstr, Cout, dw, db);
 }
 

@@ -260,6 +260,7 @@ void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const 
   TORCH_CHECK(Cout <= df.size(3) && Cout <= 128 && dw.numel() == 98 * Cout && dw.scalar_type() == at::kFloat &&
                   db.scalar_type() == at::kFloat,
               "flow_wgrad: dw fp32 [49][2][Cout], db fp32 [Cout]");
+  TORCH_CHECK(W <= 1024, "flow_wgrad: row width <= 1024 (LDS staging)");
   const c10::DeviceGuard guard(coords.device());
   rs::flow_wgrad_launch(coords.data_ptr<float>(), Bp, H, W, df.data_ptr(), df.size(3), Cout, dw.data_ptr<float>(),
                         db.data_ptr<float>(), stream());
