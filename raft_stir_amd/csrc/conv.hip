@@ -457,6 +457,193 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
 }
 
+// ------------------------------------------------------------------ direct-to-LDS variant
+// Same tile as conv_lds_kernel (BM output channels x BN pixels, 64-deep K
+// steps, st-XOR-swizzled 128-B LDS rows) but the tiles are copied global ->
+// LDS by global_load_lds_dwordx4 (no VGPR round trip, no ds_write), through a
+// 3-stage ring: loads of step k+2 are issued while step k is computed, and a
+// counted `s_waitcnt vmcnt` retires only step k's copies before the barrier.
+// The LDS destination of one wave-instruction is lane-linear, so the swizzle
+// is applied to the per-lane SOURCE chunk instead.  Out-of-image pixels read a
+// zero page.  Blocks are remapped so that each XCD (private L2) walks a
+// contiguous run of pixel tiles with all their output-channel tiles: the
+// halo rows of neighbouring tiles and the activation panel shared by the
+// Cout tiles of one pixel tile are L2 hits instead of cross-XCD refetches.
+__device__ uint4 g_zero_page[8];
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(const void* src, uint4* lds_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)src, (__attribute__((address_space(3))) void*)lds_base, 16,
+      0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  constexpr int BK = 64, CPR = 8, STAGES = 3;
+  constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
+  constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
+  static_assert(NA >= 1 && NB >= 1, "BM, BN must be multiples of 32");
+  __shared__ uint4 lds[STAGES][(BM + BN) * CPR];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int nct = cdiv(a.Cout, BM);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm0 = (lid % nct) * BM, bn0 = (lid / nct) * BN;
+  const int m0 = bm0 + wm * WM * 16, n0 = bn0 + wn * WN * 16;
+  const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
+  const int taps = a.KH * KW;
+  const int HW = H * W;
+
+  // staging: thread t, instruction i fills LDS chunk id = t + 256 i, i.e.
+  // row id / 8 at physical slot id % 8, which holds logical chunk
+  // slot ^ ((row >> 1) & 7) (see swz<8>)
+  const bf16_t* arow[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = t + 256 * i, r = id / CPR;
+    arow[i] = a.w + (size_t)(bm0 + r) * taps * Ktot + (((id % CPR) ^ ((r >> 1) & 7)) * 8);
+  }
+  int sb[NB], sy[NB], sx[NB], sc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int id = t + 256 * i, r = id / CPR;
+    const int p = bn0 + r;
+    sc[i] = ((id % CPR) ^ ((r >> 1) & 7)) * 8;
+    if (p < a.P) {
+      sb[i] = p / HW;
+      const int q = p - sb[i] * HW;
+      sy[i] = q / W;
+      sx[i] = q - sy[i] * W;
+    } else {
+      sb[i] = -1;
+      sy[i] = sx[i] = 0;
+    }
+  }
+  const int wbase = wave * 64;
+
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const int e1 = taps * (s0.C >> 6);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 6) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 6) : 0);
+
+#define RS_ISSUE(STEP, BUF)                                                                     \
+  do {                                                                                          \
+    const int step_ = (STEP);                                                                   \
+    const int si = (step_ >= e1) + (step_ >= e2);                                               \
+    const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);                          \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                    \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
+    const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);                              \
+    const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                             \
+    const int chunks = sC >> 6;                                                                 \
+    const int tap = local / chunks;                                                             \
+    const int c0 = (local - tap * chunks) * BK;                                                 \
+    const int dy = tap / KW - PH, dx = tap % KW - PW;                                           \
+    uint4* dst_ = lds[BUF];                                                                     \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                              \
+      glds16(arow[i] + (size_t)tap * Ktot + kseg + c0, dst_ + wbase + 256 * i);                 \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int yy = sy[i] + dy, xx = sx[i] + dx;                                               \
+      const bool ok = sb[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;                    \
+      const void* src_ = ok ? (const void*)(sp + ((size_t)(sb[i] * H + yy) * W + xx) * sst + c0 + sc[i]) \
+                            : (const void*)g_zero_page;                                         \
+      glds16(src_, dst_ + BM * CPR + wbase + 256 * i);                                          \
+    }                                                                                           \
+  } while (0)
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lc = lane >> 4;
+  // Fragment reads are inline-asm ds_read_b128: the compiler cannot prove
+  // they miss the in-flight LDS DMA and would otherwise drain vmcnt to 0 in
+  // front of them, collapsing the 3-stage ring to one step of lookahead.
+  // LDS byte addresses: row r, logical chunk c at r*128 + ((c ^ ((r>>1)&7))*16);
+  // for this lane (r>>1)&7 == (lr>>1)&7, so two bases (kk = 0, 1) per operand.
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+  constexpr uint32_t kStage = (BM + BN) * CPR * 16;
+  const int xr = (lr >> 1) & 7;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    abase[kk] = lds0 + (uint32_t)((wm * WM * 16 + lr) * 128 + (((kk * 4 + lc) ^ xr) * 16));
+    bbase[kk] = lds0 + (uint32_t)(BM * CPR * 16 + (wn * WN * 16 + lr) * 128 + (((kk * 4 + lc) ^ xr) * 16));
+  }
+  RS_ISSUE(0, 0);
+  if (nsteps > 1) RS_ISSUE(1, 1);
+  int buf = 0;
+  for (int step = 0; step < nsteps; ++step) {
+    if (step + 1 < nsteps) wait_vmcnt<NA + NB>();  // step's copies retired, step+1's may fly
+    else wait_vmcnt<0>();
+    asm volatile("s_barrier" ::: "memory");  // all waves' copies of `step` landed; buffer step-1 is free
+    const uint32_t so = buf * kStage;
+    u32x4_t fa[2][WM], fb[2][WN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[kk][mt]) : "v"(abase[kk] + so), "i"(mt * 2048)
+                     : "memory");
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[kk][nt]) : "v"(bbase[kk] + so), "i"(nt * 2048)
+                     : "memory");
+    }
+    if (step + 2 < nsteps) RS_ISSUE(step + 2, buf == 0 ? 2 : buf - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) asm volatile("" : "+v"(fa[kk][mt]));
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) asm volatile("" : "+v"(fb[kk][nt]));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[kk][mt]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[kk][nt]),
+                                                                acc[mt][nt], 0, 0, 0);
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+#undef RS_ISSUE
+
+  int pb[WN], py[WN], px[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int p = n0 + nt * 16 + lr;
+    if (p < a.P) {
+      pb[nt] = p / HW;
+      const int q = p - pb[nt] * HW;
+      py[nt] = q / W;
+      px[nt] = q - py[nt] * W;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = 0;
+    }
+  }
+  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
 // ------------------------------------------------------------------ small-N variant
 // Cout <= 16 (the flow head's 256 -> 2 conv): one 16x16 output tile per block
 // (16 pixels), the K steps split over the 4 waves (step = wave mod 4), partial
@@ -664,9 +851,21 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     } else if (L.tile == 6) {  // tile 3 with 64-deep K steps
       dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 64));
       hipLaunchKernelGGL((conv::conv_lds_kernel<64, 64, 2, 2, 64>), grid, dim3(256), 0, stream, a);
-    } else {  // 7: tile 4 with 64-deep K steps
+    } else if (L.tile == 7) {  // tile 4 with 64-deep K steps
       dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 128));
       hipLaunchKernelGGL((conv::conv_lds_kernel<128, 64, 2, 2, 64>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 8) {  // 128 co x 128 px, waves 2 x 2 (wave 64 x 64), 64-deep K steps
+      dim3 grid(cdiv(a.P, 128), cdiv(L.Cout, 128));
+      hipLaunchKernelGGL((conv::conv_lds_kernel<128, 128, 2, 2, 64>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 9) {  // direct-to-LDS, 64 co x 64 px
+      dim3 grid(cdiv(a.P, 64) * cdiv(L.Cout, 64));
+      hipLaunchKernelGGL((conv::conv_glds_kernel<64, 64, 2, 2>), grid, dim3(256), 0, stream, a);
+    } else if (L.tile == 10) {  // direct-to-LDS, 128 co x 64 px
+      dim3 grid(cdiv(a.P, 64) * cdiv(L.Cout, 128));
+      hipLaunchKernelGGL((conv::conv_glds_kernel<128, 64, 2, 2>), grid, dim3(256), 0, stream, a);
+    } else {  // 11: direct-to-LDS, 128 co x 128 px
+      dim3 grid(cdiv(a.P, 128) * cdiv(L.Cout, 128));
+      hipLaunchKernelGGL((conv::conv_glds_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, a);
     }
   } else if (L.tile == 1) {
     constexpr int WM = 4, WN = 2, WAVES_M = 1, WAVES_N = 4;

@@ -55,7 +55,7 @@ __device__ __forceinline__ v4s_t tr16(const uint16_t* lds_base, int byte_off) {
       (__attribute__((address_space(3))) v4s_t*)((__attribute__((address_space(3))) char*)lds_base + byte_off));
 }
 
-constexpr int BN = 64, BK = 64;
+constexpr int BK = 64;
 
 // Block: BM output channels x 64 input channels (one tap) x K split over
 // pixels; 4 waves (2 x 2), 64-pixel K steps staged in LDS in their natural
@@ -63,7 +63,7 @@ constexpr int BN = 64, BK = 64;
 // MFMA fragments with the hardware transpose read.  Blocks of the first
 // N tile also accumulate the bias gradient (column sums of dY) from the
 // staging registers.
-template <int BM>
+template <int BM, int BN>
 __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ db) {
   constexpr int AROW = BM * 2 + 16, BROW = BN * 2 + 16;  // bytes per staged pixel row (+16 pad)
   constexpr int CA = BM / 8, CB = BN / 8;                // 16-B chunks per row
@@ -300,6 +300,7 @@ struct WgradLaunch {
   int Bp, H, W, KH, KW, Ktot;
   float* dw;
   float* db;  // optional: bias gradient (column sums of dY) fused in
+  int bn128;  // allow 128-wide N tiles
 };
 
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
@@ -318,17 +319,22 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.Ktot = L.Ktot; a.taps = L.KH * L.KW;
   a.dw = L.dw;
   const int bm = a.Cout > 64 ? 128 : 64;
-  const int ntiles = a.taps * (a.Ktot / wgrad::BN);
+  bool seg128 = true;  // a 128-wide N tile must stay inside one segment
+  for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
+  const int bn = (bm == 128 && seg128 && L.bn128) ? 128 : 64;
+  const int ntiles = a.taps * (a.Ktot / bn);
   const int mtiles = cdiv(a.Cout, bm);
   int ksplit = cdiv(2048, ntiles * mtiles);
   ksplit = max(1, min(ksplit, cdiv(a.P, wgrad::BK * 8)));
   a.kchunk = round_up(cdiv(a.P, ksplit), wgrad::BK);
   ksplit = cdiv(a.P, a.kchunk);
   dim3 grid(ntiles, mtiles, ksplit);
-  if (bm == 128)
-    hipLaunchKernelGGL(wgrad::wgrad_kernel<128>, grid, dim3(256), 0, stream, a, L.db);
+  if (bn == 128)
+    hipLaunchKernelGGL((wgrad::wgrad_kernel<128, 128>), grid, dim3(256), 0, stream, a, L.db);
+  else if (bm == 128)
+    hipLaunchKernelGGL((wgrad::wgrad_kernel<128, 64>), grid, dim3(256), 0, stream, a, L.db);
   else
-    hipLaunchKernelGGL(wgrad::wgrad_kernel<64>, grid, dim3(256), 0, stream, a, L.db);
+    hipLaunchKernelGGL((wgrad::wgrad_kernel<64, 64>), grid, dim3(256), 0, stream, a, L.db);
 }
 
 void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream) {

@@ -44,6 +44,7 @@ struct WgradLaunch {
   int Bp, H, W, KH, KW, Ktot;
   float* dw;
   float* db;
+  int bn128;
 };
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream);
 void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream);
@@ -95,12 +96,13 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 7, "conv_fused: tile must be in [0,7]");
+  TORCH_CHECK(tile >= 0 && tile <= 11, "conv_fused: tile must be in [0,11]");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
-  const int tileM = tile == 0 ? 32 : ((tile == 4 || tile == 7) ? 128 : (tile == 5 ? 16 : 64));
-  if (tile == 6 || tile == 7)
+  const bool bm128 = tile == 4 || tile == 7 || tile == 8 || tile == 10 || tile == 11;
+  const int tileM = tile == 0 ? 32 : (bm128 ? 128 : (tile == 5 ? 16 : 64));
+  if (tile >= 6 && tile != 5)
     for (size_t s = 0; s < segs.size(); ++s)
-      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 6/7 (64-deep K) need segment channels % 64 == 0");
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 6-11 (64-deep K) need segment channels % 64 == 0");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
               "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
   TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == Ktot, "conv_fused: packed weight K mismatch");
@@ -191,7 +193,7 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
 // dW (fp32, [>=Cout][taps][Ktot], accumulated) += sum_p dY[p][yoff + co] X[p + tap][k]
 void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
                 at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH, int64_t KW,
-                const Tensor& dw, const c10::optional<Tensor>& db) {
+                const Tensor& dw, const c10::optional<Tensor>& db, int64_t bn128) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16,
               "conv_wgrad: dy must be contiguous bf16 NHWC");
   const int Bp = dy.size(0), H = dy.size(1), W = dy.size(2);
@@ -236,6 +238,7 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   L.Bp = Bp; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.Ktot = Ktot;
   L.dw = dw.data_ptr<float>();
   L.db = db ? db->data_ptr<float>() : nullptr;
+  L.bn128 = bn128;
   rs::wgrad_launch(L, stream());
 }
 
@@ -305,7 +308,7 @@ void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tenso
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
-        "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None) -> ()");
+        "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
   m.def("colsum(Tensor dy, int yoff, int C, Tensor(a!) db) -> ()");
   m.def("flow_wgrad(Tensor coords, Tensor df, Tensor(a!) dw, Tensor(b!) db) -> ()");
   m.def("gru_gate_bwd(Tensor(a!) dh, Tensor z, Tensor q, Tensor h, int hoff, Tensor(b!) dq, Tensor(c!) dzr) -> ()");

@@ -129,7 +129,8 @@ class FusedTrainEngine:
     def eligible(model, image, corr_fn) -> bool:
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
                 and model.cfg.mixed_precision and model.cfg.fused_gru and not model.cfg.small
-                and getattr(corr_fn, "hip", False) and _ext.use_hip(image)
+                and getattr(corr_fn, "hip", False) and getattr(corr_fn, "state", None) is not None
+                and _ext.use_hip(image)
                 and getattr(model.cfg, "fused_train", True))
 
     def buffers(self, B, H, W, iters, dev):
@@ -253,20 +254,21 @@ class FusedTrainLoop(torch.autograd.Function):
             pc.zero_grads(dev)
         hxs = S["hx"][:n]
 
-        def wg(pc, dy, yoff, segs):
-            # weight gradient + fused bias gradient (column sums of dY)
+        def wg(pc, dy, yoff, segs, bn128=0):
+            # weight gradient + fused bias gradient (column sums of dY); 128-wide
+            # N tiles where they measured faster (scripts/bench_conv.py --wgrad)
             R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
-                         [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db)
+                         [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db, bn128)
 
         wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
         wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
-        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)])
+        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)], bn128=1)
         hins = [hxs, S["h1"]]
         for p in range(2):
             wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
             wg(eng.q[p], S["d_q"][p], 0, [(S["rh"][p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
         wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)])
-        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)])
+        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], bn128=1)
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         dwf = torch.zeros(49, 2, 128, device=dev)

@@ -71,7 +71,7 @@ class FusedUpdate:
             return False
         if not _ext.use_hip(image):
             return False
-        return getattr(corr_fn, "hip", False)
+        return getattr(corr_fn, "hip", False)  # all-pairs pyramid or on-the-fly (HIP) correlation
 
     # ------------------------------------------------------------ weights
     def _version_key(self):
@@ -154,7 +154,7 @@ class FusedUpdate:
         if bufs is None:
             e = lambda c: torch.empty(B, H, W, c, device=dev, dtype=torch.bfloat16)
             z = lambda c: torch.zeros(B, H, W, c, device=dev, dtype=torch.bfloat16)
-            bufs = dict(corr=e(self.corr_pad), f1=e(self.f1_c), mot=e(self.mot_c), hx=z(self.hx_c),
+            bufs = dict(corr=z(self.corr_pad), f1=e(self.f1_c), mot=e(self.mot_c), hx=z(self.hx_c),
                         z=e(self.hd), rh=z(pad_to(self.hd, 32)), head=e(self.head_c))
             if not self.model.cfg.small:
                 bufs["c1"] = e(256)
@@ -179,12 +179,17 @@ class FusedUpdate:
         hx[..., :hd].copy_(net.permute(0, 2, 3, 1))
         hx[..., self.off_inp:self.off_inp + self.cd].copy_(inp.permute(0, 2, 3, 1))
         coords1 = coords1.float().contiguous().clone()
-        st = corr_fn.state
+        st = getattr(corr_fn, "state", None)  # None: on-the-fly correlation
         small = self.model.cfg.small
         preds, flow_up = [], None
         for itr in range(iters):
             want_up = (not test_mode) or itr == iters - 1
-            torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
+            if st is not None:
+                torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
+            else:  # memory-efficient path: correlate the pooled fmap2 pyramid on the fly
+                c = torch.ops.raft_stir.corr_otf(corr_fn.f1, corr_fn.f2s, coords1, corr_fn.radius, corr_fn.scale,
+                                                 True)
+                bufs["corr"][..., :c.shape[-1]].copy_(c)
             torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
             cp = self.corr_pad
             if small:

@@ -47,7 +47,8 @@ def main():
     ap.add_argument("--hw", type=int, nargs=2, default=[55, 136])
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--tiles", type=int, nargs="+", default=[3, 4, 5, 6, 7])
+    ap.add_argument("--wgrad", type=int, default=0, help="also bench wgrad with this many iterations batched")
+    ap.add_argument("--tiles", type=int, nargs="+", default=[5, 6, 7, 8])
     a = ap.parse_args()
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
@@ -65,11 +66,15 @@ def main():
         bp = pack_bias(b)
         flop = 2.0 * P * cout * cin * kh * kw
         line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"
+        ref_out = None
         for t in a.tiles:
-            if (t == 5) != (cout <= 16) or (t in (6, 7) and cin % 64):
+            if (t == 5) != (cout <= 16) or (t >= 6 and t != 5 and cin % 64):
                 continue
             us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
-            line += f" tile{t} {us:7.1f}us {flop / us / 1e6:6.1f}TF |"
+            if ref_out is None:
+                ref_out = out[..., :cout].float().clone()
+            err = (out[..., :cout].float() - ref_out).abs().max().item()
+            line += f" tile{t} {us:7.1f}us {flop / us / 1e6:6.1f}TF err={err:.2g} |"
             tot.setdefault(f"tile{t}", 0.0)
             tot[f"tile{t}"] += us
         xc = x.permute(0, 3, 1, 2)
@@ -79,6 +84,23 @@ def main():
         tot["miopen"] = tot.get("miopen", 0.0) + us
         print(line, flush=True)
     print("sum per iteration-set:", {k: round(v, 1) for k, v in tot.items()})
+    if a.wgrad:
+        # batched weight-gradient GEMMs over iters*B*H*W pixels
+        n = a.wgrad * B
+        for name, cin, cout, kh, kw in SHAPES:
+            if cin % 64 or cout <= 2:
+                continue
+            x = torch.randn(n, H, W, cin, device=dev).to(torch.bfloat16)
+            dy = torch.randn(n, H, W, pad_to(cout, 128), device=dev).to(torch.bfloat16)
+            dw = torch.zeros(pad_to(cout, 128), kh * kw, cin, device=dev)
+            db = torch.zeros(cout, device=dev)
+            flop = 2.0 * n * H * W * cout * cin * kh * kw
+            line = f"wgrad {name:8s} K(px)={n * H * W:7d} M={cout:4d} N={cin * kh * kw:5d} |"
+            for bn128 in (0, 1):
+                us = timeit(lambda: torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [n * H * W], kh, kw,
+                                                                     dw, db, bn128), max(5, a.reps // 5))
+                line += f" bn128={bn128} {us:8.1f}us {flop / us / 1e6:6.1f}TF |"
+            print(line, flush=True)
 
 
 if __name__ == "__main__":

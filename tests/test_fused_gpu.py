@@ -115,12 +115,13 @@ def test_flow_epilogue_and_flow_encode(cuda):
     torch.testing.assert_close(slot[..., 6:8].float().permute(0, 3, 1, 2), crd - grid, atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("small", [False, True])
-def test_fused_inference_matches_unfused(cuda, small):
+@pytest.mark.parametrize("small,alt", [(False, False), (True, False), (False, True)])
+def test_fused_inference_matches_unfused(cuda, small, alt):
     """Fused engine vs the module graph (same bf16 autocast), and vs fp32."""
     from raft_stir_amd.data.synthetic import make_batch
     torch.manual_seed(0)
-    m = RAFT(make_args(small=small, mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).eval()
+    m = RAFT(make_args(small=small, mixed_precision=True, alternate_corr=alt)).to(cuda)
+    m = m.to(memory_format=torch.channels_last).eval()
     unf = copy.deepcopy(m)
     unf.set_fused_gru(False)
     unf.cfg = unf.cfg.__class__(**{**unf.cfg.to_dict(), "fused_gru": False})

@@ -39,6 +39,11 @@ def test_wgrad_batched_with_broadcast_segment(cuda, k):
     torch.ops.raft_stir.colsum(dy, 0, cout, db)
     torch.testing.assert_close(db, dy[..., :cout].float().sum((0, 1, 2)), atol=5e-2, rtol=1e-3)
     torch.testing.assert_close(db2, db, atol=5e-2, rtol=1e-3)   # bias fused into the wgrad kernel
+    # 128-wide N tiles (one 128-channel segment)
+    x1 = torch.cat([xa[..., 64:], xb.repeat(iters, 1, 1, 1)], -1).contiguous()
+    dw3 = torch.zeros_like(dw)
+    torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x1], [0], [128], [iters * B * H * W], kh, kw, dw3, None, 1)
+    torch.testing.assert_close(dw3[:cout], want, atol=5e-2, rtol=1e-2)
 
 
 def test_flow_wgrad(cuda):
