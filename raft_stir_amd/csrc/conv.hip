@@ -28,6 +28,8 @@
 // with zeros for padding channels, so the K loop needs no bounds checks.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace rs {
 namespace conv {
 
@@ -74,6 +76,7 @@ struct Args {
   int a1str, a1off;
   const bf16_t* aux2;  // z
   int a2str, a2off;
+  int xcd_remap;  // conv_glds_kernel: remap block ids so each XCD walks contiguous tiles
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
@@ -488,19 +491,24 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, int STAGES>
 __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
-  constexpr int BK = 64, CPR = 8, STAGES = 3;
+  static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(STAGES >= 2 && STAGES <= 4, "STAGES");
+  constexpr int CPR = BK / 8;     // 16-B chunks per LDS row
+  constexpr int RB = CPR * 16;    // LDS row bytes
+  constexpr int SH = BK == 32 ? 5 : 6;
   constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
   constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
-  static_assert(NA >= 1 && NB >= 1, "BM, BN must be multiples of 32");
+  constexpr int NLD = NA + NB;    // DMA instructions per thread per K step
+  static_assert(NA >= 1 && NB >= 1, "tile too small for 256 threads");
   __shared__ uint4 lds[STAGES][(BM + BN) * CPR];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
   const int nct = cdiv(a.Cout, BM);
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lid = a.xcd_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int bm0 = (lid % nct) * BM, bn0 = (lid / nct) * BN;
   const int m0 = bm0 + wm * WM * 16, n0 = bn0 + wn * WN * 16;
   const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
@@ -508,20 +516,21 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
   const int HW = H * W;
 
   // staging: thread t, instruction i fills LDS chunk id = t + 256 i, i.e.
-  // row id / 8 at physical slot id % 8, which holds logical chunk
-  // slot ^ ((row >> 1) & 7) (see swz<8>)
+  // row id / CPR at physical slot id % CPR, which holds the logical chunk
+  // slot ^ xor(row) of swz<CPR>
+  auto xrow = [](int r) { return CPR == 4 ? (r >> 2) & 3 : (r >> 1) & 7; };
   const bf16_t* arow[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int id = t + 256 * i, r = id / CPR;
-    arow[i] = a.w + (size_t)(bm0 + r) * taps * Ktot + (((id % CPR) ^ ((r >> 1) & 7)) * 8);
+    arow[i] = a.w + (size_t)(bm0 + r) * taps * Ktot + (((id % CPR) ^ xrow(r)) * 8);
   }
   int sb[NB], sy[NB], sx[NB], sc[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int id = t + 256 * i, r = id / CPR;
     const int p = bn0 + r;
-    sc[i] = ((id % CPR) ^ ((r >> 1) & 7)) * 8;
+    sc[i] = ((id % CPR) ^ xrow(r)) * 8;
     if (p < a.P) {
       sb[i] = p / HW;
       const int q = p - sb[i] * HW;
@@ -535,9 +544,9 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
   const int wbase = wave * 64;
 
   const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
-  const int e1 = taps * (s0.C >> 6);
-  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 6) : 0);
-  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 6) : 0);
+  const int e1 = taps * (s0.C >> SH);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> SH) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> SH) : 0);
 
 #define RS_ISSUE(STEP, BUF)                                                                     \
   do {                                                                                          \
@@ -548,7 +557,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
     const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
     const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);                              \
     const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                             \
-    const int chunks = sC >> 6;                                                                 \
+    const int chunks = sC >> SH;                                                                \
     const int tap = local / chunks;                                                             \
     const int c0 = (local - tap * chunks) * BK;                                                 \
     const int dy = tap / KW - PH, dx = tap % KW - PW;                                           \
@@ -573,49 +582,52 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
   const int lr = lane & 15, lc = lane >> 4;
   // Fragment reads are inline-asm ds_read_b128: the compiler cannot prove
   // they miss the in-flight LDS DMA and would otherwise drain vmcnt to 0 in
-  // front of them, collapsing the 3-stage ring to one step of lookahead.
-  // LDS byte addresses: row r, logical chunk c at r*128 + ((c ^ ((r>>1)&7))*16);
-  // for this lane (r>>1)&7 == (lr>>1)&7, so two bases (kk = 0, 1) per operand.
+  // front of them, collapsing the ring to one step of lookahead.  For this
+  // lane the row XOR term is xrow(lr) (tile rows start at multiples of 16).
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
-  constexpr uint32_t kStage = (BM + BN) * CPR * 16;
-  const int xr = (lr >> 1) & 7;
-  uint32_t abase[2], bbase[2];
+  constexpr uint32_t kStage = (BM + BN) * RB;
+  constexpr int KK = BK / 32;
+  uint32_t abase[KK], bbase[KK];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    abase[kk] = lds0 + (uint32_t)((wm * WM * 16 + lr) * 128 + (((kk * 4 + lc) ^ xr) * 16));
-    bbase[kk] = lds0 + (uint32_t)(BM * CPR * 16 + (wn * WN * 16 + lr) * 128 + (((kk * 4 + lc) ^ xr) * 16));
+  for (int kk = 0; kk < KK; ++kk) {
+    abase[kk] = lds0 + (uint32_t)((wm * WM * 16 + lr) * RB + (((kk * 4 + lc) ^ xrow(lr)) * 16));
+    bbase[kk] = lds0 + (uint32_t)(BM * RB + (wn * WN * 16 + lr) * RB + (((kk * 4 + lc) ^ xrow(lr)) * 16));
   }
-  RS_ISSUE(0, 0);
-  if (nsteps > 1) RS_ISSUE(1, 1);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nsteps) RS_ISSUE(s, s);
   int buf = 0;
   for (int step = 0; step < nsteps; ++step) {
-    if (step + 1 < nsteps) wait_vmcnt<NA + NB>();  // step's copies retired, step+1's may fly
+    // retire this step's copies; keep up to STAGES-2 later steps in flight
+    const int ahead = min(STAGES - 2, nsteps - 1 - step);
+    if (STAGES >= 4 && ahead >= 2) wait_vmcnt<2 * NLD>();
+    else if (STAGES >= 3 && ahead >= 1) wait_vmcnt<NLD>();
     else wait_vmcnt<0>();
-    asm volatile("s_barrier" ::: "memory");  // all waves' copies of `step` landed; buffer step-1 is free
+    asm volatile("s_barrier" ::: "memory");  // all waves' copies landed; buffer step-1 is free
     const uint32_t so = buf * kStage;
-    u32x4_t fa[2][WM], fb[2][WN];
+    u32x4_t fa[KK][WM], fb[KK][WN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[kk][mt]) : "v"(abase[kk] + so), "i"(mt * 2048)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[kk][mt]) : "v"(abase[kk] + so), "i"(mt * 16 * RB)
                      : "memory");
 #pragma unroll
       for (int nt = 0; nt < WN; ++nt)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[kk][nt]) : "v"(bbase[kk] + so), "i"(nt * 2048)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[kk][nt]) : "v"(bbase[kk] + so), "i"(nt * 16 * RB)
                      : "memory");
     }
-    if (step + 2 < nsteps) RS_ISSUE(step + 2, buf == 0 ? 2 : buf - 1);
+    if (step + STAGES - 1 < nsteps) RS_ISSUE(step + STAGES - 1, buf == 0 ? STAGES - 1 : buf - 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt) asm volatile("" : "+v"(fa[kk][mt]));
 #pragma unroll
       for (int nt = 0; nt < WN; ++nt) asm volatile("" : "+v"(fb[kk][nt]));
     }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
@@ -623,7 +635,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[kk][mt]),
                                                                 __builtin_bit_cast(bf16x8_t, fb[kk][nt]),
                                                                 acc[mt][nt], 0, 0, 0);
-    buf = buf == 2 ? 0 : buf + 1;
+    buf = buf == STAGES - 1 ? 0 : buf + 1;
   }
 #undef RS_ISSUE
 
@@ -836,6 +848,11 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.out3 = L.out3; a.o3str = L.o3str; a.o3off = L.o3off;
   a.aux1 = static_cast<const bf16_t*>(L.aux1); a.a1str = L.a1str; a.a1off = L.a1off;
   a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
+  static const int xcd_env = [] {
+    const char* e = getenv("RS_CONV_XCD_REMAP");
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd_remap = xcd_env;
   if (L.tile == 5) {
     hipLaunchKernelGGL(conv::conv_smalln_kernel, dim3(cdiv(a.P, 16)), dim3(256), 0, stream, a);
   } else if (L.tile >= 2) {
@@ -857,15 +874,20 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     } else if (L.tile == 8) {  // 128 co x 128 px, waves 2 x 2 (wave 64 x 64), 64-deep K steps
       dim3 grid(cdiv(a.P, 128), cdiv(L.Cout, 128));
       hipLaunchKernelGGL((conv::conv_lds_kernel<128, 128, 2, 2, 64>), grid, dim3(256), 0, stream, a);
-    } else if (L.tile == 9) {  // direct-to-LDS, 64 co x 64 px
-      dim3 grid(cdiv(a.P, 64) * cdiv(L.Cout, 64));
-      hipLaunchKernelGGL((conv::conv_glds_kernel<64, 64, 2, 2>), grid, dim3(256), 0, stream, a);
-    } else if (L.tile == 10) {  // direct-to-LDS, 128 co x 64 px
-      dim3 grid(cdiv(a.P, 64) * cdiv(L.Cout, 128));
-      hipLaunchKernelGGL((conv::conv_glds_kernel<128, 64, 2, 2>), grid, dim3(256), 0, stream, a);
-    } else {  // 11: direct-to-LDS, 128 co x 128 px
-      dim3 grid(cdiv(a.P, 128) * cdiv(L.Cout, 128));
-      hipLaunchKernelGGL((conv::conv_glds_kernel<128, 128, 2, 2>), grid, dim3(256), 0, stream, a);
+    } else {  // direct-to-LDS ring (conv_glds_kernel), grid 1-D over (pixel tile, Cout tile)
+#define RS_GLDS(BM_, BN_, BK_, ST_)                                                                  \
+  hipLaunchKernelGGL((conv::conv_glds_kernel<BM_, BN_, 2, 2, BK_, ST_>),                             \
+                     dim3(cdiv(a.P, BN_) * cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
+      switch (L.tile) {
+        case 9: RS_GLDS(64, 64, 64, 3); break;
+        case 10: RS_GLDS(128, 64, 64, 3); break;
+        case 11: RS_GLDS(128, 64, 64, 2); break;
+        case 12: RS_GLDS(128, 64, 32, 4); break;
+        case 13: RS_GLDS(128, 64, 32, 3); break;
+        case 14: RS_GLDS(64, 64, 32, 4); break;
+        default: RS_GLDS(64, 64, 64, 2); break;  // 15
+      }
+#undef RS_GLDS
     }
   } else if (L.tile == 1) {
     constexpr int WM = 4, WN = 2, WAVES_M = 1, WAVES_N = 4;

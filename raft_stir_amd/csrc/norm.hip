@@ -25,6 +25,11 @@ constexpr int THREADS = 256;
 template <typename T> struct Vec;
 template <> struct Vec<float> {
   static constexpr int N = 4;
+  typedef float4 raw;
+  __device__ static raw ldraw(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ static void cvt(const raw& q, float* v) {
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
   __device__ static void load(const float* p, float* v) {
     float4 q = *reinterpret_cast<const float4*>(p);
     v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
@@ -35,6 +40,16 @@ template <> struct Vec<float> {
 };
 template <> struct Vec<bf16_t> {
   static constexpr int N = 8;
+  typedef uint4 raw;
+  __device__ static raw ldraw(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+  __device__ static void cvt(const raw& q, float* v) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
   __device__ static void load(const bf16_t* p, float* v) {
     uint4 q = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -104,30 +119,46 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
     const T* x = static_cast<const T*>(a.x) + (size_t)b * a.P * a.C;
     const T* dy = static_cast<const T*>(a.dy) + (size_t)b * a.P * a.C;
     const T* res = a.res ? static_cast<const T*>(a.res) + (size_t)b * a.P * a.C : nullptr;
-    for (int p = p0 + row; p < p1; p += rows) {
-      const size_t off = (size_t)p * a.C + col * VN;
-      float xv[VN];
-      V::load(x + off, xv);
-      if (MODE == 0) {
+    for (int p = p0 + row; p < p1; p += rows * 4) {
+      typename V::raw xq[4], dq[4], rq[4];
 #pragma unroll
-        for (int i = 0; i < VN; ++i) {
-          acc0[i] += xv[i];
-          acc1[i] += xv[i] * xv[i];
+      for (int u = 0; u < 4; ++u) {
+        const int pp = p + u * rows;
+        if (pp < p1) {
+          const size_t off = (size_t)pp * a.C + col * VN;
+          xq[u] = V::ldraw(x + off);
+          if (MODE == 1) {
+            dq[u] = V::ldraw(dy + off);
+            if (res) rq[u] = V::ldraw(res + off);
+          }
         }
-      } else {
-        float dv[VN], rv[VN];
-        V::load(dy + off, dv);
-        if (res) V::load(res + off, rv);
+      }
 #pragma unroll
-        for (int i = 0; i < VN; ++i) {
-          const float xh = (xv[i] - mu[i]) * rs_[i];
-          const float pre = ga[i] * xh + be[i];
-          const float y1 = a.relu ? fmaxf(pre, 0.f) : pre;
-          float gg = dv[i];
-          if (res && rv[i] + y1 <= 0.f) gg = 0.f;
-          if (a.relu && pre <= 0.f) gg = 0.f;
-          acc0[i] += gg;
-          acc1[i] += gg * xh;
+      for (int u = 0; u < 4; ++u) {
+        if (p + u * rows >= p1) break;
+        float xv[VN];
+        V::cvt(xq[u], xv);
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < VN; ++i) {
+            acc0[i] += xv[i];
+            acc1[i] += xv[i] * xv[i];
+          }
+        } else {
+          float dv[VN], rv[VN];
+          V::cvt(dq[u], dv);
+          if (res) V::cvt(rq[u], rv);
+#pragma unroll
+          for (int i = 0; i < VN; ++i) {
+            const float xh = (xv[i] - mu[i]) * rs_[i];
+            const float pre = ga[i] * xh + be[i];
+            const float y1 = a.relu ? fmaxf(pre, 0.f) : pre;
+            float gg = dv[i];
+            if (res && rv[i] + y1 <= 0.f) gg = 0.f;
+            if (a.relu && pre <= 0.f) gg = 0.f;
+            acc0[i] += gg;
+            acc1[i] += gg * xh;
+          }
         }
       }
     }
@@ -197,30 +228,63 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, i
 }
 
 // --------------------------------------------------------------- elementwise
+// Grid (S, B): block (s, b) streams pixels [p0, p1) of sample b.  Thread t
+// owns channel vector t % CV for its whole life, so its per-channel constants
+// are folded once into registers (scale = gamma*rstd, shift = beta -
+// mean*scale, ...) instead of being re-gathered per element; the pixel loop
+// is unrolled UNR deep so that many 16-B loads are in flight per thread.
+constexpr int UNR = 4;
+
 template <typename T>
 __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
   using V = Vec<T>;
   constexpr int VN = V::N;
-  const size_t nvec = (size_t)a.B * a.P * a.C / VN;
   const int CV = a.C / VN;
-  for (size_t v = blockIdx.x * (size_t)THREADS + threadIdx.x; v < nvec;
-       v += (size_t)gridDim.x * THREADS) {
-    const int c0 = (int)(v % CV) * VN;
-    const int b = (int)(v / ((size_t)a.P * CV));
-    const int g = a.G == 1 ? 0 : b;
-    float xv[VN], rv[VN], out[VN];
-    V::load(static_cast<const T*>(a.x) + v * VN, xv);
-    if (a.res) V::load(static_cast<const T*>(a.res) + v * VN, rv);
+  const int rows = THREADS / CV;
+  const int row = threadIdx.x / CV, col = threadIdx.x % CV;
+  if (row >= rows) return;
+  const int b = blockIdx.y, g = a.G == 1 ? 0 : b;
+  const int chunk = cdiv(a.P, a.S);
+  const int p0 = blockIdx.x * chunk, p1 = min(a.P, p0 + chunk);
+  float sc[VN], sh[VN];
 #pragma unroll
-    for (int i = 0; i < VN; ++i) {
-      const int c = c0 + i;
-      const float xh = (xv[i] - a.mean[g * a.C + c]) * a.rstd[g * a.C + c];
-      float y = (a.gamma ? a.gamma[c] : 1.f) * xh + (a.beta ? a.beta[c] : 0.f);
-      if (a.relu) y = fmaxf(y, 0.f);
-      if (a.res) y = fmaxf(y + rv[i], 0.f);
-      out[i] = y;
+  for (int i = 0; i < VN; ++i) {
+    const int c = col * VN + i;
+    const float r = a.rstd[g * a.C + c];
+    sc[i] = (a.gamma ? a.gamma[c] : 1.f) * r;
+    sh[i] = (a.beta ? a.beta[c] : 0.f) - a.mean[g * a.C + c] * sc[i];
+  }
+  const size_t base = (size_t)b * a.P * a.C + col * VN;
+  const T* x = static_cast<const T*>(a.x) + base;
+  const T* res = a.res ? static_cast<const T*>(a.res) + base : nullptr;
+  T* y = static_cast<T*>(a.y) + base;
+  const bool relu = a.relu;
+  for (int p = p0 + row; p < p1; p += rows * UNR) {
+    typename V::raw xq[UNR], rq[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pp = p + u * rows;
+      if (pp < p1) {
+        xq[u] = V::ldraw(x + (size_t)pp * a.C);
+        if (res) rq[u] = V::ldraw(res + (size_t)pp * a.C);
+      }
     }
-    V::store(static_cast<T*>(a.y) + v * VN, out);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pp = p + u * rows;
+      if (pp >= p1) break;
+      float out[VN], xv[1][VN], rv[1][VN];
+      V::cvt(xq[u], xv[0]);
+      if (res) V::cvt(rq[u], rv[0]);
+#pragma unroll
+      for (int i = 0; i < VN; ++i) {
+        float v = xv[0][i] * sc[i] + sh[i];
+        if (relu) v = fmaxf(v, 0.f);
+        if (res) v = fmaxf(v + rv[0][i], 0.f);
+        out[i] = v;
+      }
+      V::store(y + (size_t)pp * a.C, out);
+    }
   }
 }
 
@@ -228,35 +292,75 @@ template <typename T>
 __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   using V = Vec<T>;
   constexpr int VN = V::N;
-  const size_t nvec = (size_t)a.B * a.P * a.C / VN;
   const int CV = a.C / VN;
-  for (size_t v = blockIdx.x * (size_t)THREADS + threadIdx.x; v < nvec;
-       v += (size_t)gridDim.x * THREADS) {
-    const int c0 = (int)(v % CV) * VN;
-    const int b = (int)(v / ((size_t)a.P * CV));
-    const int g = a.G == 1 ? 0 : b;
-    float xv[VN], dv[VN], rv[VN], dxo[VN], dro[VN];
-    V::load(static_cast<const T*>(a.x) + v * VN, xv);
-    V::load(static_cast<const T*>(a.dy) + v * VN, dv);
-    if (a.res) V::load(static_cast<const T*>(a.res) + v * VN, rv);
+  const int rows = THREADS / CV;
+  const int row = threadIdx.x / CV, col = threadIdx.x % CV;
+  if (row >= rows) return;
+  const int b = blockIdx.y, g = a.G == 1 ? 0 : b;
+  const int chunk = cdiv(a.P, a.S);
+  const int p0 = blockIdx.x * chunk, p1 = min(a.P, p0 + chunk);
+  // pre = x*sc + sh ; dx = k1*gg - k1*m1 - (x - mean)*k2  with
+  // k1 = gamma*rstd, m1 = s1/N, k2 = gamma*rstd^2*s2/N
+  float sc[VN], sh[VN], k0[VN], k2[VN], mu[VN];
 #pragma unroll
-    for (int i = 0; i < VN; ++i) {
-      const int c = c0 + i;
-      const float m = a.mean[g * a.C + c], r = a.rstd[g * a.C + c];
-      const float ga = a.gamma ? a.gamma[c] : 1.f;
-      const float xh = (xv[i] - m) * r;
-      const float pre = ga * xh + (a.beta ? a.beta[c] : 0.f);
-      const float y1 = a.relu ? fmaxf(pre, 0.f) : pre;
-      float gout = dv[i];
-      if (a.res && rv[i] + y1 <= 0.f) gout = 0.f;
-      dro[i] = gout;
-      float gg = gout;
-      if (a.relu && pre <= 0.f) gg = 0.f;
-      dxo[i] = ga * r * (gg - a.s1[g * a.C + c] * a.inv_n - xh * a.s2[g * a.C + c] * a.inv_n);
-    }
-    V::store(static_cast<T*>(a.dx) + v * VN, dxo);
-    if (a.dres) V::store(static_cast<T*>(a.dres) + v * VN, dro);
+  for (int i = 0; i < VN; ++i) {
+    const int c = col * VN + i;
+    const float r = a.rstd[g * a.C + c];
+    const float ga = a.gamma ? a.gamma[c] : 1.f;
+    mu[i] = a.mean[g * a.C + c];
+    sc[i] = ga * r;
+    sh[i] = (a.beta ? a.beta[c] : 0.f) - mu[i] * sc[i];
+    k0[i] = sc[i] * a.s1[g * a.C + c] * a.inv_n;
+    k2[i] = sc[i] * r * a.s2[g * a.C + c] * a.inv_n;
   }
+  const size_t base = (size_t)b * a.P * a.C + col * VN;
+  const T* x = static_cast<const T*>(a.x) + base;
+  const T* dy = static_cast<const T*>(a.dy) + base;
+  const T* res = a.res ? static_cast<const T*>(a.res) + base : nullptr;
+  T* dx = static_cast<T*>(a.dx) + base;
+  T* dres = a.dres ? static_cast<T*>(a.dres) + base : nullptr;
+  const bool relu = a.relu;
+  for (int p = p0 + row; p < p1; p += rows * UNR) {
+    typename V::raw xq[UNR], dq[UNR], rq[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pp = p + u * rows;
+      if (pp < p1) {
+        xq[u] = V::ldraw(x + (size_t)pp * a.C);
+        dq[u] = V::ldraw(dy + (size_t)pp * a.C);
+        if (res) rq[u] = V::ldraw(res + (size_t)pp * a.C);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int pp = p + u * rows;
+      if (pp >= p1) break;
+      float dxo[VN], dro[VN], xv[VN], dv[VN], rv[VN];
+      V::cvt(xq[u], xv);
+      V::cvt(dq[u], dv);
+      if (res) V::cvt(rq[u], rv);
+#pragma unroll
+      for (int i = 0; i < VN; ++i) {
+        const float pre = xv[i] * sc[i] + sh[i];
+        const float y1 = relu ? fmaxf(pre, 0.f) : pre;
+        float gout = dv[i];
+        if (res && rv[i] + y1 <= 0.f) gout = 0.f;
+        dro[i] = gout;
+        const float gg = (relu && pre <= 0.f) ? 0.f : gout;
+        dxo[i] = sc[i] * gg - k0[i] - (xv[i] - mu[i]) * k2[i];
+      }
+      V::store(dx + (size_t)pp * a.C, dxo);
+      if (dres) V::store(dres + (size_t)pp * a.C, dro);
+    }
+  }
+}
+
+// blocks per sample for the elementwise passes: ~2048 blocks in total, at
+// least UNR*2 pixel rows per thread
+int pick_apply_splits(int B, int P, int C, int vn) {
+  const int rows = THREADS / (C / vn);
+  int S = cdiv(2048, B);
+  return max(1, min(S, cdiv(P, rows * UNR * 2)));
 }
 
 int pick_splits(int B, int P, int C, int vn) {
@@ -302,13 +406,11 @@ void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mea
   norm::Args a{};
   a.x = x; a.res = res; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.y = y;
   a.B = B; a.P = P; a.C = C; a.G = G; a.relu = relu;
-  const size_t nvec = (size_t)B * P * C / (bf16 ? 8 : 4);
+  a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
   if (bf16)
-    hipLaunchKernelGGL(norm::apply_fwd_kernel<bf16_t>, dim3(norm::grid_elem(nvec)),
-                       dim3(norm::THREADS), 0, s, a);
+    hipLaunchKernelGGL(norm::apply_fwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
   else
-    hipLaunchKernelGGL(norm::apply_fwd_kernel<float>, dim3(norm::grid_elem(nvec)),
-                       dim3(norm::THREADS), 0, s, a);
+    hipLaunchKernelGGL(norm::apply_fwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
 }
 
 void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, const float* mean,
@@ -328,13 +430,11 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
                      C, G, 0.f, 0.f, s1, s2);
   a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres;
   a.inv_n = batch_stats ? 1.f / (float)((G == 1 ? (double)B : 1.0) * P) : 0.f;
-  const size_t nvec = (size_t)B * P * C / (bf16 ? 8 : 4);
+  a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
   if (bf16)
-    hipLaunchKernelGGL(norm::apply_bwd_kernel<bf16_t>, dim3(norm::grid_elem(nvec)),
-                       dim3(norm::THREADS), 0, s, a);
+    hipLaunchKernelGGL(norm::apply_bwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
   else
-    hipLaunchKernelGGL(norm::apply_bwd_kernel<float>, dim3(norm::grid_elem(nvec)),
-                       dim3(norm::THREADS), 0, s, a);
+    hipLaunchKernelGGL(norm::apply_bwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
 }
 
 }  // namespace rs

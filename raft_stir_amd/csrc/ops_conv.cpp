@@ -96,13 +96,13 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 11, "conv_fused: tile must be in [0,11]");
+  TORCH_CHECK(tile >= 0 && tile <= 15, "conv_fused: tile must be in [0,15]");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
-  const bool bm128 = tile == 4 || tile == 7 || tile == 8 || tile == 10 || tile == 11;
+  const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13);
   const int tileM = tile == 0 ? 32 : (bm128 ? 128 : (tile == 5 ? 16 : 64));
-  if (tile >= 6 && tile != 5)
+  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14)  // 64-deep K steps
     for (size_t s = 0; s < segs.size(); ++s)
-      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 6-11 (64-deep K) need segment channels % 64 == 0");
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: 64-deep-K tiles need segment channels % 64 == 0");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
               "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
   TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == Ktot, "conv_fused: packed weight K mismatch");

@@ -26,7 +26,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.norm import norm_act
+from ..ops.norm import conv_norm_act
 
 
 def make_norm(kind: str, channels: int, groups: int) -> nn.Module:
@@ -59,10 +59,10 @@ class ResidualBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm3)
 
     def forward(self, x):
-        y = norm_act(self.norm1, self.conv1(x))
-        skip = x if self.downsample is None else norm_act(self.norm3, self.downsample[0](x), relu=False)
+        y = conv_norm_act(self.conv1, self.norm1, x)
+        skip = x if self.downsample is None else conv_norm_act(self.downsample[0], self.norm3, x, relu=False)
         # relu(skip + relu(norm2(conv2(y)))) as one fused pass on GPU
-        return norm_act(self.norm2, self.conv2(y), relu=True, residual=skip)
+        return conv_norm_act(self.conv2, self.norm2, y, relu=True, residual=skip)
 
 
 class BottleneckBlock(nn.Module):
@@ -86,10 +86,10 @@ class BottleneckBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm4)
 
     def forward(self, x):
-        y = norm_act(self.norm1, self.conv1(x))
-        y = norm_act(self.norm2, self.conv2(y))
-        skip = x if self.downsample is None else norm_act(self.norm4, self.downsample[0](x), relu=False)
-        return norm_act(self.norm3, self.conv3(y), relu=True, residual=skip)
+        y = conv_norm_act(self.conv1, self.norm1, x)
+        y = conv_norm_act(self.conv2, self.norm2, y)
+        skip = x if self.downsample is None else conv_norm_act(self.downsample[0], self.norm4, x, relu=False)
+        return conv_norm_act(self.conv3, self.norm3, y, relu=True, residual=skip)
 
 
 class _Encoder(nn.Module):
@@ -137,7 +137,7 @@ class _Encoder(nn.Module):
         if pair:
             n = x[0].shape[0]
             x = torch.cat(list(x), dim=0)
-        x = norm_act(self.norm1, self.conv1(x))
+        x = conv_norm_act(self.conv1, self.norm1, x)
         x = self.layer3(self.layer2(self.layer1(x)))
         x = self.conv2(x)
         if self.training and self.dropout is not None:

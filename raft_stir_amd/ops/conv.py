@@ -51,15 +51,17 @@ def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
 
 
 def choose_tile(P: int, cout: int, seg_chans) -> int:
-    """Kernel variant for a conv (measured on MI355X, scripts/bench_conv.py):
-    5 = split-K small-N (Cout <= 16); 6/7 = LDS-staged 64x64 / 128x64 tiles
-    with 64-deep K steps (all segments % 64 == 0); 3/4 = the same with 32-deep
-    K steps."""
+    """Kernel variant for a conv (measured on MI355X, scripts/bench_conv.py;
+    profiles/conv_tiles_r1.md):
+    5 = split-K small-N (Cout <= 16); 6 = LDS-staged 64x64 tile with 64-deep K
+    steps; 11 = 128x64 tile fed by global->LDS DMA (2-stage ring, XCD-aware
+    block order) -- both need every segment % 64 == 0; 3/4 = 64x64 / 128x64
+    register-staged tiles with 32-deep K steps otherwise."""
     if cout <= 16:
         return 5
     big = cout >= 192 or (cout >= 126 and P >= 16384)
     if all(c % 64 == 0 for c in seg_chans):
-        return 7 if big else 6
+        return 11 if big else 6
     return 4 if big else 3
 
 

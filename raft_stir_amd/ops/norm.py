@@ -31,12 +31,13 @@ def _nhwc(x):
 
 class _NormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, mean, rstd, relu, batch_stats):
+    def forward(ctx, x, gamma, beta, res, mean, rstd, relu, batch_stats, bias=None):
         xn = _nhwc(x)
         rn = _nhwc(res) if res is not None else None
         y = torch.ops.raft_stir.norm_act(xn, mean, rstd, gamma, beta, rn, relu)
         ctx.save_for_backward(x, gamma, beta, res, mean, rstd)
         ctx.relu, ctx.batch_stats = relu, batch_stats
+        ctx.bias_meta = (bias.shape, bias.dtype) if bias is not None else None
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -49,7 +50,17 @@ class _NormAct(torch.autograd.Function):
         dgamma = s2.sum(0) if gamma is not None and ctx.needs_input_grad[1] else None
         dbeta = s1.sum(0) if beta is not None and ctx.needs_input_grad[2] else None
         dres_out = dres.permute(0, 3, 1, 2) if res is not None else None
-        return dx.permute(0, 3, 1, 2), dgamma, dbeta, dres_out, None, None, None, None
+        dbias = None
+        if ctx.bias_meta is not None and ctx.needs_input_grad[8]:
+            shape, dtype = ctx.bias_meta
+            if ctx.batch_stats:
+                # a per-channel constant is removed by the batch/instance
+                # mean: its gradient is exactly zero
+                dbias = torch.zeros(shape, dtype=dtype, device=dy.device)
+            else:  # running statistics: d pre / d bias = gamma * rstd
+                g = gamma.float() if gamma is not None else 1.0
+                dbias = (s1.sum(0) * g * rstd.reshape(-1)).to(dtype)
+        return dx.permute(0, 3, 1, 2), dgamma, dbeta, dres_out, None, None, None, None, dbias
 
 
 def _hip_ok(norm, x, residual):
@@ -72,8 +83,12 @@ def _hip_ok(norm, x, residual):
     return False
 
 
-def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None):
+def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None):
+    """``bias``: the producing convolution's bias, folded into the statistics
+    (see :func:`conv_norm_act`); None if already applied."""
     if not _hip_ok(norm, x, residual):
+        if bias is not None:
+            x = x + bias.to(x.dtype).view(1, -1, 1, 1)
         y = norm(x)
         if relu:
             y = F.relu(y)
@@ -86,7 +101,7 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None)
     if isinstance(norm, nn.InstanceNorm2d):
         with torch.no_grad():  # the stats' gradient is part of _NormAct.backward
             mean, rstd = torch.ops.raft_stir.norm_stats(xn, True, norm.eps)
-        return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True)
+        return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True, bias)
     # BatchNorm2d
     batch_stats = norm.training
     if batch_stats:
@@ -96,11 +111,34 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None)
             var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
             unbiased = var * (n / max(n - 1, 1))
             m = norm.momentum
-            norm.running_mean.mul_(1 - m).add_(mean.reshape(-1), alpha=m)
+            bmean = mean.reshape(-1) if bias is None else mean.reshape(-1) + bias.detach().float()
+            norm.running_mean.mul_(1 - m).add_(bmean, alpha=m)
             norm.running_var.mul_(1 - m).add_(unbiased, alpha=m)
             norm.num_batches_tracked.add_(1)
     else:
         mean = norm.running_mean.float().reshape(1, -1)
+        if bias is not None:  # gamma * (x + b - mean) * rstd + beta
+            mean = mean - bias.detach().float().reshape(1, -1)
         rstd = torch.rsqrt(norm.running_var.float() + norm.eps).reshape(1, -1)
     return _NormAct.apply(x, norm.weight, norm.bias, residual, mean.contiguous(), rstd.contiguous(),
-                          relu, batch_stats)
+                          relu, batch_stats, bias)
+
+
+def _norm_kind_ok(norm):
+    if isinstance(norm, nn.InstanceNorm2d):
+        return not norm.affine and not norm.track_running_stats
+    if isinstance(norm, nn.BatchNorm2d):
+        return norm.affine and norm.track_running_stats and norm.momentum is not None
+    return False
+
+
+def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None):
+    """``norm_act(norm, conv(x), relu, residual)``.  On the GPU path the conv
+    runs without its bias and the bias is folded into the normalisation
+    (instance / train-mode batch norm remove it exactly; eval-mode batch norm
+    shifts its running mean by it): no bias-add pass over the conv output
+    forward and no bias-gradient reduction over it backward."""
+    if conv.bias is None or not _ext.use_hip(x) or not _norm_kind_ok(norm):
+        return norm_act(norm, conv(x), relu, residual)
+    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    return norm_act(norm, y, relu, residual, bias=conv.bias)

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--wgrad", type=int, default=0, help="also bench wgrad with this many iterations batched")
     ap.add_argument("--tiles", type=int, nargs="+", default=[5, 6, 7, 8])
+    ap.add_argument("--only", nargs="+", default=None, help="shape names to run")
+    ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
+    ap.add_argument("--no-miopen", action="store_true")
     a = ap.parse_args()
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
@@ -58,6 +61,8 @@ def main():
     P = B * H * W
     tot = {}
     for name, cin, cout, kh, kw in SHAPES:
+        if a.only and name not in a.only:
+            continue
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
         w = torch.randn(cout, cin, kh, kw, device=dev) * 0.05
         b = torch.randn(cout, device=dev)
@@ -68,7 +73,7 @@ def main():
         line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"
         ref_out = None
         for t in a.tiles:
-            if (t == 5) != (cout <= 16) or (t >= 6 and t != 5 and cin % 64):
+            if (t == 5) != (cout <= 16) or (t >= 6 and t not in (12, 13, 14) and cin % 64):
                 continue
             us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
             if ref_out is None:
@@ -77,18 +82,25 @@ def main():
             line += f" tile{t} {us:7.1f}us {flop / us / 1e6:6.1f}TF err={err:.2g} |"
             tot.setdefault(f"tile{t}", 0.0)
             tot[f"tile{t}"] += us
-        xc = x.permute(0, 3, 1, 2)
-        wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        us = timeit(lambda: F.relu(F.conv2d(xc, wb, b.to(torch.bfloat16), padding=(kh // 2, kw // 2))), a.reps)
-        line += f" miopen {us:7.1f}us {flop / us / 1e6:6.1f}TF"
-        tot["miopen"] = tot.get("miopen", 0.0) + us
+        if a.gemm:
+            ga = torch.randn(P, cin * kh * kw, device=dev).to(torch.bfloat16)
+            gb = torch.randn(cin * kh * kw, cout, device=dev).to(torch.bfloat16)
+            us = timeit(lambda: torch.mm(ga, gb), a.reps)
+            line += f" gemm {us:7.1f}us {flop / us / 1e6:6.1f}TF |"
+            del ga, gb
+        if not a.no_miopen:
+            xc = x.permute(0, 3, 1, 2)
+            wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            us = timeit(lambda: F.relu(F.conv2d(xc, wb, b.to(torch.bfloat16), padding=(kh // 2, kw // 2))), a.reps)
+            line += f" miopen {us:7.1f}us {flop / us / 1e6:6.1f}TF"
+            tot["miopen"] = tot.get("miopen", 0.0) + us
         print(line, flush=True)
     print("sum per iteration-set:", {k: round(v, 1) for k, v in tot.items()})
     if a.wgrad:
         # batched weight-gradient GEMMs over iters*B*H*W pixels
         n = a.wgrad * B
         for name, cin, cout, kh, kw in SHAPES:
-            if cin % 64 or cout <= 2:
+            if cin % 64 or cout <= 2 or (a.only and name not in a.only):
                 continue
             x = torch.randn(n, H, W, cin, device=dev).to(torch.bfloat16)
             dy = torch.randn(n, H, W, pad_to(cout, 128), device=dev).to(torch.bfloat16)

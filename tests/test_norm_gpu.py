@@ -74,3 +74,39 @@ def test_norm_act_large_spatial(cuda):
     y = norm_act(norm, x)
     yr = F.relu(norm(x.float()))
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("kind", ["instance", "batch_train", "batch_eval"])
+def test_conv_norm_act_folds_bias(cuda, kind):
+    """conv_norm_act (bias folded into the norm) vs relu(norm(conv(x) + b)) in fp32."""
+    from raft_stir_amd.ops.norm import conv_norm_act
+    torch.manual_seed(2)
+    C = 64
+    conv = nn.Conv2d(32, C, 3, padding=1)
+    with torch.no_grad():
+        conv.bias.uniform_(-1, 1)
+    if kind == "instance":
+        norm = nn.InstanceNorm2d(C)
+    else:
+        norm = nn.BatchNorm2d(C)
+        with torch.no_grad():
+            norm.weight.uniform_(0.5, 1.5)
+            norm.running_mean.uniform_(-0.2, 0.2)
+            norm.running_var.uniform_(0.5, 2.0)
+        norm.train(kind == "batch_train")
+    conv, norm = conv.to(cuda), norm.to(cuda)
+    rconv, rnorm = copy.deepcopy(conv), copy.deepcopy(norm)
+    x = torch.randn(2, 32, 24, 40, device=cuda).contiguous(memory_format=torch.channels_last)
+    y = conv_norm_act(conv, norm, x)
+    yr = F.relu(rnorm(rconv(x)))
+    torch.testing.assert_close(y, yr, atol=1e-4, rtol=1e-4)
+    g = torch.randn_like(yr)
+    y.backward(g.contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    torch.testing.assert_close(conv.weight.grad, rconv.weight.grad, atol=1e-3, rtol=1e-3)
+    if kind == "batch_eval":
+        torch.testing.assert_close(conv.bias.grad, rconv.bias.grad, atol=1e-3, rtol=1e-3)
+    else:  # exactly zero (the reference carries round-off only)
+        assert conv.bias.grad.abs().max() == 0 and rconv.bias.grad.abs().max() < 1e-3
+        if kind == "batch_train":
+            torch.testing.assert_close(norm.running_mean, rnorm.running_mean, atol=1e-5, rtol=1e-5)
