@@ -39,7 +39,7 @@ enum Epi : int {
   EPI_SCALE = 2,   // (acc + b) * scale
   EPI_GRU_ZR = 3,  // co < hd: z -> out ; co >= hd: r*h -> out2 (r -> out3 if set)
   EPI_GRU_Q = 4,   // h' = (1-z) h + z tanh(acc + b) -> out (q~ -> out2 if set)
-  EPI_FLOW = 5,    // coords (fp32 NCHW) += acc + b   (co < 2)
+  EPI_FLOW = 5,    // coords (fp32 NCHW) = (out2 ? out2 : coords) + acc + b   (co < 2)
   // backward (dgrad) epilogues
   EPI_RELU_BWD = 6,  // out(bf16) = v * (aux1 > 0)            (through the producer's ReLU)
   EPI_ACC_F32 = 7,   // out(fp32) += v                        (gradient accumulation)
@@ -103,14 +103,15 @@ __device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM]
       for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
       const bool full = cb + 3 < a.Cout;
       switch (a.epi) {
-        case EPI_FLOW: {
+        case EPI_FLOW: {  // coords (+)= delta; out2 (if set) is the source coords
           float* crd = static_cast<float*>(a.out);
+          const float* src = a.out2 ? static_cast<const float*>(a.out2) : crd;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int co = cb + j;
             if (co < a.Cout && co < 2) {
-              float* d = crd + ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
-              *d += v[j];
+              const size_t o = ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
+              crd[o] = src[o] + v[j];
             }
           }
           break;

@@ -124,6 +124,12 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
                 "conv_fused(flow): out must be fp32 coords (B,2,H,W)");
     TORCH_CHECK(Cout == 2, "conv_fused(flow): Cout must be 2");
     L.out = out.data_ptr(); L.ostr = 0; L.ooff = 0;
+    if (out2) {  // out-of-place: out = out2 + delta
+      TORCH_CHECK(out2->is_cuda() && out2->is_contiguous() && out2->scalar_type() == at::kFloat &&
+                      out2->sizes() == out.sizes(),
+                  "conv_fused(flow): out2 (source coords) must match out");
+      L.out2 = out2->data_ptr();
+    }
   } else {
     const bool f32out = epi == EPI_ACC_F32 || epi == EPI_GRU_QBWD;
     check_nhwc(out, B, H, W, "out", f32out ? at::kFloat : at::kBFloat16);

@@ -12,12 +12,20 @@ into an [iters * B, H, W, C] slot instead of being overwritten:
   S.h1                        h after the first SepConvGRU pass
   S.z / S.r / S.q / S.rh      GRU gates, tanh(q), r*h per pass
   S.head, S.mask              flow-head/mask hidden (ReLU), convex mask
-  S.cin / S.cout              coords before / after each update
+  S.C[i]                      coords before update i (iters + 1 slots)
 
-Backward, iteration by iteration in reverse (dgrads = the forward conv kernel
-with transposed + flipped packed weights and gradient epilogues):
+The convex upsampling of all iterations is one launch after the loop (the
+predictions do not feed back), so the Function returns one
+[iters * B, 2, 8H, 8W] tensor that the model splits into views; the fused
+sequence loss (train/loss.py) consumes it whole.
 
-  convex_upsample_backward -> d mask, d flow
+Weights are packed for the kernels by one static gather per step (and the
+gradients unpacked by one), see FusedTrainEngine._build_maps.
+
+Backward: one batched convex_upsample_backward, then iteration by iteration
+in reverse (dgrads = the forward conv kernel with transposed + flipped
+packed weights and gradient epilogues):
+
   mask2 / flow dgrad (through the hidden ReLU)  -> d head
   head dgrad             -> dh  (fp32, accumulated with dh of iteration i+1)
   GRU pass 2, pass 1     -> gate backward kernel, q-conv dgrad with the
@@ -62,39 +70,43 @@ class _PConv:
         self.cin = w0.shape[1]
         self.ktot = sum(c for c, _ in segs)
 
-    @torch.no_grad()
-    def pack(self):
-        weight = torch.cat([c.weight for c in self.convs], 0)
-        bias = torch.cat([c.bias for c in self.convs], 0)
-        self.w = pack_weight(weight, self.segs, pad_to(self.cout, 128))
-        self.b = pack_bias(bias)
-        # dgrad: Wd[k][tap'][co] = scale * W[co][taps-1-tap'][k], co padded to 64
-        cy = pad_to(self.cout, 64)
-        wd = self.w[:cy].float().flip(1).permute(2, 1, 0) * self.scale
-        out = torch.zeros(pad_to(self.ktot, 128), wd.shape[1], cy, device=wd.device, dtype=torch.float32)
-        out[:self.ktot] = wd
-        self.wd = out.to(torch.bfloat16).contiguous()
-        self.cy = cy
-
-    def zero_grads(self, dev):
-        self.dw = torch.zeros(pad_to(self.cout, 128), self.kh * self.kw, self.ktot, device=dev)
-        self.db = torch.zeros(self.cout, device=dev)
-
-    def unpack_grads(self):
-        """packed [Cout][taps][Ktot] grads -> one (dW, db) per original conv."""
-        taps = self.kh * self.kw
-        gw = torch.zeros(self.cout, taps, self.cin, device=self.dw.device)
+    def index_maps(self, pidx, fill):
+        """Index maps (into the flat parameter vector) of the packed forward
+        weight [Cout_pad128][taps][Ktot], the bias, and the dgrad weight
+        Wd[k][tap'][co] = W[co][taps-1-tap'][k] ([pad128(Ktot)][taps][pad64(Cout)])."""
+        weight = torch.cat([pidx[id(c.weight)] for c in self.convs], 0)
+        bias = torch.cat([pidx[id(c.bias)] for c in self.convs], 0)
+        cout, cin, kh, kw = weight.shape
+        taps = kh * kw
+        wt = weight.permute(0, 2, 3, 1).reshape(cout, taps, cin)
+        w = torch.full((pad_to(cout, 128), taps, self.ktot), fill, dtype=torch.long)
         kb = 0
         for c, pieces in self.segs:
             for w0, n, s0 in pieces:
-                gw[:, :, w0:w0 + n] = self.dw[:self.cout, :, kb + s0:kb + s0 + n]
+                w[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
             kb += c
-        gw = gw.reshape(self.cout, self.kh, self.kw, self.cin).permute(0, 3, 1, 2) * self.scale
-        db = self.db * self.scale
+        cy = pad_to(cout, 64)
+        wd = torch.full((pad_to(self.ktot, 128), taps, cy), fill, dtype=torch.long)
+        wd[:self.ktot] = w[:cy].flip(1).permute(2, 1, 0)
+        self.cy = cy
+        return w, bias, wd
+
+    def grad_maps(self, gidx):
+        """Per original conv (weight, bias) index maps into the packed gradient
+        buffers gidx = (dW [Cout_pad128][taps][Ktot], db [Cout]) index views."""
+        dwi, dbi = gidx
+        taps = self.kh * self.kw
+        gw = torch.empty(self.cout, taps, self.cin, dtype=torch.long)
+        kb = 0
+        for c, pieces in self.segs:
+            for w0, n, s0 in pieces:
+                gw[:, :, w0:w0 + n] = dwi[:self.cout, :, kb + s0:kb + s0 + n]
+            kb += c
+        gw = gw.reshape(self.cout, self.kh, self.kw, self.cin).permute(0, 3, 1, 2)
         out, r0 = [], 0
         for c in self.convs:
             n = c.weight.shape[0]
-            out.append((gw[r0:r0 + n].contiguous(), db[r0:r0 + n].contiguous()))
+            out.append((gw[r0:r0 + n].contiguous(), dbi[r0:r0 + n].contiguous()))
             r0 += n
         return out
 
@@ -124,6 +136,112 @@ class FusedTrainEngine:
                 self.params += [c.weight, c.bias]
         self.params += [self.f1.weight, self.f1.bias]
         self._bufs = {}
+        self._maps = None
+
+    def _build_maps(self, dev):
+        """Static gather maps: packing every update-block weight for the fused
+        kernels (forward + dgrad layouts) is ONE index_select over the
+        concatenated parameters per step, and unpacking every weight / bias
+        gradient from the kernels' packed accumulators ONE index_select over
+        the flat gradient buffer -- instead of ~200 small copy kernels."""
+        sizes = [p.numel() for p in self.params]
+        nsrc = sum(sizes)
+        fill = nsrc  # index of the appended zero
+        ids = torch.arange(nsrc)
+        pidx, off = {}, 0
+        for p in self.params:
+            pidx[id(p)] = ids[off:off + p.numel()].view(p.shape)
+            off += p.numel()
+        bf_maps, f32_maps, layout = [], [], []
+        nbf = 0
+        for pc in self.convs:
+            w, b, wd = pc.index_maps(pidx, fill)
+            layout.append((pc, w.shape, wd.shape, b.shape))
+            bf_maps += [w.reshape(-1), wd.reshape(-1)]
+            f32_maps.append(b.reshape(-1))
+        f1w = pidx[id(self.f1.weight)].permute(2, 3, 1, 0).contiguous()  # [7][7][2][128]
+        f32_maps += [f1w.reshape(-1), pidx[id(self.f1.bias)].reshape(-1)]
+        nbf = sum(m.numel() for m in bf_maps)
+        gather = torch.cat(bf_maps + f32_maps)
+        # scale (mask x 0.25) folded into the dgrad weights: element range in the bf16 region
+        o, scaled = 0, []
+        for pc, ws, wds, bs in layout:
+            o += ws.numel()
+            if pc.scale != 1.0:
+                scaled.append((o, o + wds.numel(), pc.scale))
+            o += wds.numel()
+        # gradient buffer: per conv dW [Cout_pad128][taps][Ktot] + db [Cout], then flow-conv dW, db
+        glayout, go = [], 0
+        for pc in self.convs:
+            dws = (pad_to(pc.cout, 128), pc.kh * pc.kw, pc.ktot)
+            n = dws[0] * dws[1] * dws[2]
+            glayout.append((go, dws, go + n, pc.cout))
+            go += n + pc.cout
+        gf1 = (go, go + 49 * 2 * 128)
+        gtotal = gf1[1] + 128
+        gids = torch.arange(gtotal)
+        gmaps, gscaled, o = [], [], 0
+        for pc, (dwo, dws, dbo, nb) in zip(self.convs, glayout):
+            dwi = gids[dwo:dwo + dws[0] * dws[1] * dws[2]].view(dws)
+            dbi = gids[dbo:dbo + nb]
+            for gw, gb in pc.grad_maps((dwi, dbi)):
+                gmaps += [gw.reshape(-1), gb.reshape(-1)]
+                if pc.scale != 1.0:
+                    scaled_range = (o, o + gw.numel() + gb.numel(), pc.scale)
+                    gscaled.append(scaled_range)
+                o += gw.numel() + gb.numel()
+        f1g = gids[gf1[0]:gf1[1]].view(7, 7, 2, 128).permute(3, 2, 0, 1).contiguous()
+        gmaps += [f1g.reshape(-1), gids[gf1[1]:gf1[1] + 128]]
+        self._maps = dict(dev=dev, gather=gather.to(dev), nbf=nbf, layout=layout, scaled=scaled,
+                          glayout=glayout, gf1=gf1, gtotal=gtotal, ggather=torch.cat(gmaps).to(dev),
+                          gscaled=gscaled, zero=torch.zeros(1, device=dev))
+
+    @torch.no_grad()
+    def pack(self, dev):
+        """Per-step weight packing (see _build_maps): cat + gather + bf16 cast."""
+        if self._maps is None or self._maps["dev"] != dev:
+            self._build_maps(dev)
+        M = self._maps
+        src = torch.cat([p.detach().reshape(-1).float() for p in self.params] + [M["zero"]])
+        vals = src.index_select(0, M["gather"])
+        for a, b, s in M["scaled"]:
+            vals[a:b].mul_(s)
+        nbf = M["nbf"]
+        bf = vals[:nbf].to(torch.bfloat16)
+        ob, of = 0, nbf
+        for pc, ws, wds, bs in M["layout"]:
+            n = ws.numel()
+            pc.w = bf[ob:ob + n].view(ws)
+            ob += n
+            n = wds.numel()
+            pc.wd = bf[ob:ob + n].view(wds)
+            ob += n
+            pc.b = vals[of:of + bs.numel()]
+            of += bs.numel()
+        self.f1w = vals[of:of + 49 * 2 * 128].view(7, 7, 2, 128)
+        of += 49 * 2 * 128
+        self.f1b = vals[of:of + 128]
+
+    def grad_buffers(self, dev):
+        """One zero-filled fp32 buffer holding every packed gradient accumulator."""
+        M = self._maps
+        g = torch.zeros(M["gtotal"], device=dev)
+        for pc, (dwo, dws, dbo, nb) in zip(self.convs, M["glayout"]):
+            pc.dw = g[dwo:dwo + dws[0] * dws[1] * dws[2]].view(dws)
+            pc.db = g[dbo:dbo + nb]
+        a, b = M["gf1"]
+        return g, g[a:b].view(49, 2, 128), g[b:b + 128]
+
+    def unpack_grads(self, g):
+        M = self._maps
+        flat = g.index_select(0, M["ggather"])
+        for a, b, s in M["gscaled"]:
+            flat[a:b].mul_(s)
+        out, o = [], 0
+        for p in self.params:
+            out.append(flat[o:o + p.numel()].view(p.shape))
+            o += p.numel()
+        return out
 
     @staticmethod
     def eligible(model, image, corr_fn) -> bool:
@@ -143,9 +261,10 @@ class FusedTrainEngine:
                 corr=e(n, CORR_PAD), c1=e(n, 256), f1=e(n, 128), mot=e(n, 256), hx=e(n + B, 256), h1=e(n, HD),
                 z=[e(n, HD), e(n, HD)], r=[e(n, HD), e(n, HD)], q=[e(n, HD), e(n, HD)], rh=[e(n, HD), e(n, HD)],
                 head=e(n, 512), mask=e(n, 576), inp=e(B, 128),
-                cin=torch.empty(n, 2, H, W, device=dev), cout=torch.empty(n, 2, H, W, device=dev),
-                # gradient (dY) slots
-                d_mask=e(n, 640), d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
+                C=torch.empty(n + B, 2, H, W, device=dev),  # coords before iteration i = slot i
+                # gradient (dY) slots (zero-initialised: only the leading channels are written)
+                d_mask=torch.zeros(n, H, W, 640, device=dev, dtype=torch.bfloat16),
+                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
                 d_head=e(n, 512), d_zr=[e(n, 256), e(n, 256)], d_q=[e(n, HD), e(n, HD)], d_conv=e(n, 128),
                 d_c2f2=e(n, 256), d_c1=e(n, 256), d_f1=e(n, 128), d_corr=e(B, CORR_PAD),
                 G=torch.empty(B, H, W, 384, device=dev),
@@ -157,23 +276,21 @@ class FusedTrainEngine:
 class FusedTrainLoop(torch.autograd.Function):
     @staticmethod
     def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, *params):
-        for pc in eng.convs:
-            pc.pack()
-        f1w = eng.f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()
-        f1b = eng.f1.bias.detach().float().contiguous()
         B, _, H, W = coords1.shape
         dev = coords1.device
+        eng.pack(dev)
+        f1w, f1b = eng.f1w, eng.f1b
         S = eng.buffers(B, H, W, iters, dev)
         sl = lambda t, i: t[i * B:(i + 1) * B]
         S["hx"][:B, ..., :HD].copy_(net.permute(0, 2, 3, 1))
         S["inp"].copy_(inp.permute(0, 2, 3, 1))
-        coords = coords1.detach().float().contiguous().clone()
+        C = S["C"]
+        sl(C, 0).copy_(coords1.detach())
         c0 = coords0.detach().float().contiguous()
         inpb = S["inp"]
-        preds = []
         for i in range(iters):
             hx, hx1 = sl(S["hx"], i), sl(S["hx"], i + 1)
-            sl(S["cin"], i).copy_(coords)
+            coords = sl(C, i)
             R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
             R.flow_encode(coords, f1w, f1b, sl(S["f1"], i), 0, hx, 254)
             conv_fused([(sl(S["corr"], i), 0, CORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, 256, EPI_RELU, sl(S["c1"], i))
@@ -192,37 +309,42 @@ class FusedTrainLoop(torch.autograd.Function):
                            eng.q[p].kw, HD, EPI_GRU_Q, ob, oo, out2=q, aux1=hb, a1off=ho, aux2=z)
             head = sl(S["head"], i)
             conv_fused([(hx1, 0, HD)], eng.head.w, eng.head.b, 3, 3, 512, EPI_RELU, head, 0)
-            conv_fused([(head, 0, 256)], eng.flow.w, eng.flow.b, 3, 3, 2, EPI_FLOW, coords)
-            mask = sl(S["mask"], i)
-            conv_fused([(head, 256, 256)], eng.mask2.w, eng.mask2.b, 1, 1, 576, EPI_SCALE, mask, 0, scale=0.25)
-            sl(S["cout"], i).copy_(coords)
-            preds.append(R.convex_upsample(coords - c0, mask))
+            # coords_{i+1} = coords_i + delta (out of place: the history is kept for backward)
+            conv_fused([(head, 0, 256)], eng.flow.w, eng.flow.b, 3, 3, 2, EPI_FLOW, sl(C, i + 1), out2=coords)
+            conv_fused([(head, 256, 256)], eng.mask2.w, eng.mask2.b, 1, 1, 576, EPI_SCALE, sl(S["mask"], i), 0,
+                       scale=0.25)
+        # every iteration's convex upsampling in one launch (they do not feed back)
+        n = iters * B
+        flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
+        up = R.convex_upsample(flows, S["mask"])
         ctx.eng, ctx.state, ctx.S, ctx.iters = eng, corr_state, S, iters
         ctx.c0 = c0
         ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
-        return tuple(preds)
+        return up
 
     @staticmethod
-    def backward(ctx, *gpreds):
+    def backward(ctx, g_up):
         eng, st, S, iters = ctx.eng, ctx.state, ctx.S, ctx.iters
         c0 = ctx.c0
         B, H, W = S["inp"].shape[:3]
         dev = c0.device
+        n = iters * B
         sl = lambda t, i: t[i * B:(i + 1) * B]
         if st.gpyr is None:
             st.gpyr = [torch.zeros_like(p) for p in st.pyr]
         G = S["G"]
         G.zero_()
         inpb = S["inp"]
+        C = S["C"]
+        if g_up is None:
+            g_up = torch.zeros(n, 2, 8 * H, 8 * W, device=dev)
+        flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
+        dflow, dmask = R.convex_upsample_backward(flows, S["mask"], g_up.contiguous())
+        S["d_mask"][..., :576].copy_(dmask)
+        S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
         for i in reversed(range(iters)):
-            g = gpreds[i]
-            if g is None:
-                g = torch.zeros(B, 2, 8 * H, 8 * W, device=dev)
             hx, hx1, head = sl(S["hx"], i), sl(S["hx"], i + 1), sl(S["head"], i)
-            dflow, dmask = R.convex_upsample_backward(sl(S["cout"], i) - c0, sl(S["mask"], i), g.contiguous())
             dm, df, dh = sl(S["d_mask"], i), sl(S["d_flow"], i), sl(S["d_head"], i)
-            dm[..., :576].copy_(dmask)
-            df[..., :2].copy_(dflow.permute(0, 2, 3, 1))
             conv_fused([(dm, 0, 576)], eng.mask2.wd, None, 1, 1, 256, EPI_RELU_BWD, dh, 256, aux1=head, a1off=256)
             conv_fused([(df, 0, 64)], eng.flow.wd, None, 3, 3, 256, EPI_RELU_BWD, dh, 0, aux1=head, a1off=0)
             conv_fused([(dh, 0, 512)], eng.head.wd, None, 3, 3, HD, EPI_ACC_F32, G, 0)
@@ -244,14 +366,10 @@ class FusedTrainLoop(torch.autograd.Function):
             conv_fused([(dc2f2, 192, 64)], eng.f2.wd, None, 3, 3, 128, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
                        aux1=sl(S["f1"], i))
             conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, S["d_corr"], 0)
-            R.corr_lookup_backward(st.gpyr, sl(S["cin"], i), st.radius, S["d_corr"])
+            R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, S["d_corr"])
 
         # ---------------- weight / bias gradients, batched over all iterations
-        n = iters * B
-        P_all = n * H * W
-        P_inp = B * H * W
-        for pc in eng.convs:
-            pc.zero_grads(dev)
+        gbuf, dwf, dbf = eng.grad_buffers(dev)
         hxs = S["hx"][:n]
 
         def wg(pc, dy, yoff, segs, bn128=0):
@@ -271,16 +389,9 @@ class FusedTrainLoop(torch.autograd.Function):
         wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], bn128=1)
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
-        dwf = torch.zeros(49, 2, 128, device=dev)
-        dbf = torch.zeros(128, device=dev)
-        R.flow_wgrad(S["cin"], S["d_f1"], dwf, dbf)
-
-        grads = []
-        for pc in eng.convs:
-            for gw, gb in pc.unpack_grads():
-                grads += [gw, gb]
-        grads += [dwf.reshape(7, 7, 2, 128).permute(3, 2, 0, 1).contiguous(), dbf]
-        grads = [gr.to(p.dtype) for gr, p in zip(grads, eng.params)]
+        R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
+        grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype)
+                 for gr, p in zip(eng.unpack_grads(gbuf), eng.params)]
         d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
         d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
         token_grad = torch.zeros((), device=dev)

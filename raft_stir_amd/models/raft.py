@@ -137,9 +137,10 @@ class RAFT(nn.Module):
 
             if not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn):
                 eng = self._train_engine()
-                preds = FusedTrainLoop.apply(eng, corr_fn.state, corr_fn.token, net, inp, coords0, coords1,
-                                             iters, *eng.params)
-                return list(preds)
+                up = FusedTrainLoop.apply(eng, corr_fn.state, corr_fn.token, net, inp, coords0, coords1,
+                                          iters, *eng.params)
+                # consecutive views of one tensor: the fused loss reads it whole
+                return list(up.view(iters, *coords1.shape[:1], *up.shape[1:]).unbind(0))
 
             if FusedUpdate.eligible(self, image1, corr_fn):
                 eng = self._fused_engine()

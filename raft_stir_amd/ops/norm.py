@@ -16,6 +16,8 @@ Everything else (CPU, export, GroupNorm, identity) takes the composite path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -23,6 +25,7 @@ import torch.nn.functional as F
 from . import _ext
 
 _CL = torch.channels_last
+_FOLD_BIAS = os.environ.get("RS_FOLD_BIAS", "1") != "0"
 
 
 def _nhwc(x):
@@ -138,7 +141,7 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
     (instance / train-mode batch norm remove it exactly; eval-mode batch norm
     shifts its running mean by it): no bias-add pass over the conv output
     forward and no bias-gradient reduction over it backward."""
-    if conv.bias is None or not _ext.use_hip(x) or not _norm_kind_ok(norm):
+    if conv.bias is None or not _FOLD_BIAS or not _ext.use_hip(x) or not _norm_kind_ok(norm):
         return norm_act(norm, conv(x), relu, residual)
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return norm_act(norm, y, relu, residual, bias=conv.bias)
