@@ -8,12 +8,15 @@ __version__ = "0.1.0"
 
 import os as _os
 
-# MIOpen (the encoder convolutions) would otherwise run a ~20 s on-line
-# solution search on the first call of every conv shape missing from its
-# shipped find-db (measured: scripts/first_step_probe.py; the steady-state
-# step time is the same or better in FAST mode).  Must be set before MIOpen
-# initialises; a user setting wins.
-_os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# MIOpen (the encoder convolutions) runs an on-line solution search (~20 s)
+# on the first call of every conv shape missing from its shipped find-db.
+# The results of that search on MI355X for this model's shapes are kept in
+# the package (miopen_db/, a text find-db written by MIOpen itself), so a
+# fresh process starts with them.  MIOPEN_FIND_MODE=FAST is NOT an option:
+# its fallback picks CK weight-gradient kernels ~50x slower (535 ms/step vs
+# 39 ms measured).  A user setting wins; must be set before MIOpen starts.
+_os.environ.setdefault("MIOPEN_USER_DB_PATH",
+                       _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "miopen_db"))
 
 from .config import RAFTConfig, resolve_config, make_args  # noqa: F401
 
