@@ -77,6 +77,8 @@ struct Args {
   const bf16_t* aux2;  // z
   int a2str, a2off;
   int xcd_remap;  // conv_glds_kernel: remap block ids so each XCD walks contiguous tiles
+  unsigned seg_bytes[3];
+  unsigned w_bytes;
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
@@ -657,6 +659,191 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
   epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
 }
 
+// ------------------------------------------------------------------ buffer-DMA variant
+// conv_glds_kernel spends most of its issue slots on per-lane address
+// arithmetic (segment / tap / chunk decode with integer divisions, 64-bit
+// pointer math and bounds tests for every staged row at every K step): with
+// one or two waves per SIMD that VALU work, not the MFMAs, set the step time.
+// Here the per-step work is almost all scalar:
+//  * the (segment, tap, chunk) walk is a scalar counter, no divisions;
+//  * tiles are copied with buffer_load_dwordx4 ... lds through per-segment
+//    buffer descriptors: the weight tile's step offset is the scalar SOFFSET
+//    (zero VALU per A row), a pixel row's offset is its precomputed base + the
+//    scalar tap shift (one add);
+//  * zero padding: each staged pixel row keeps a bitmask of the taps that
+//    land inside the image (built once per block); a row outside gets an
+//    offset past the buffer's end, which the buffer unit returns as zeros.
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, soff,
+                                           0, 0);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
+__global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(STAGES >= 2 && STAGES <= 3, "STAGES");
+  constexpr int BK = 64, CPR = 8, RB = 128;
+  constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
+  constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
+  constexpr int NLD = NA + NB;
+  constexpr int kFar = 0x7ffffff0;  // past every buffer: reads as zero
+  __shared__ uint4 lds[STAGES][(BM + BN) * CPR];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int nct = cdiv(a.Cout, BM);
+  const int lid = a.xcd_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int bm0 = (lid % nct) * BM, bn0 = (lid / nct) * BN;
+  const int m0 = bm0 + wm * WM * 16, n0 = bn0 + wn * WN * 16;
+  const int H = a.H, W = a.W, KW = a.KW, Ktot = a.Ktot;
+  const int taps = a.KH * KW;
+  const int HW = H * W;
+
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const __amdgpu_buffer_rsrc_t rs0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s0.ptr, (short)0, a.seg_bytes[0], 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s1.ptr, (short)0, a.seg_bytes[1], 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s2.ptr, (short)0, a.seg_bytes[2], 0x00020000);
+
+  // staging slot (thread t, instruction i) = LDS chunk t + 256 i: row r, physical
+  // slot id % 8 holding logical chunk slot ^ ((r >> 1) & 7)  (swz<8>)
+  int aoff[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = t + 256 * i, r = id / CPR;
+    aoff[i] = ((bm0 + r) * taps * Ktot + (((id % CPR) ^ ((r >> 1) & 7)) * 8)) * 2;
+  }
+  // pixel rows: offset (elements, stride-free) of pixel (y - PH, x - PW) and the valid-tap mask
+  int bpix[NB], bch[NB];
+  unsigned bmask[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int id = t + 256 * i, r = id / CPR;
+    const int p = bn0 + r;
+    bch[i] = ((id % CPR) ^ ((r >> 1) & 7)) * 8;
+    bmask[i] = 0u;
+    bpix[i] = 0;
+    if (p < a.P) {
+      const int b = p / HW, q = p - b * HW, y = q / W, x = q - y * W;
+      bpix[i] = (b * H + y - a.PH) * W + (x - a.PW);
+      for (int tp = 0, ty = 0, tx = 0; tp < taps; ++tp) {
+        const int yy = y + ty - a.PH, xx = x + tx - a.PW;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) bmask[i] |= 1u << tp;
+        if (++tx == KW) { tx = 0; ++ty; }
+      }
+    }
+  }
+  const int wbase = wave * 64;
+  const int e1 = taps * (s0.C >> 6);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 6) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 6) : 0);
+
+  // scalar walk of the K steps: segment si, tap (ty, tx), channel chunk c0
+  int si = 0, tap = 0, ty = 0, tx = 0, c0 = 0, kseg = 0;
+  // (a macro, not a lambda: capturing the staging arrays by reference would
+  // take their address and move them to scratch)
+#define RS_BISSUE(BUF)                                                                          \
+  do {                                                                                          \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                    \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
+    const __amdgpu_buffer_rsrc_t rb = si == 0 ? rs0 : (si == 1 ? rs1 : rs2);                    \
+    uint4* dst = lds[BUF];                                                                      \
+    const int asoff = (tap * Ktot + kseg + c0) * 2;                                             \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) bdma16(rw, dst + wbase + 256 * i, aoff[i], asoff); \
+    const int tsh = ty * W + tx;                                                                \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int v = ((bmask[i] >> tap) & 1u) ? ((bpix[i] + tsh) * sst + c0 + bch[i]) * 2 : kFar; \
+      bdma16(rb, dst + BM * CPR + wbase + 256 * i, v, 0);                                       \
+    }                                                                                           \
+    c0 += BK; /* advance to the next K step */                                                  \
+    if (c0 == sC) {                                                                             \
+      c0 = 0;                                                                                   \
+      ++tap;                                                                                    \
+      if (++tx == KW) { tx = 0; ++ty; }                                                         \
+      if (tap == taps) { tap = 0; ty = 0; kseg += sC; ++si; }                                   \
+    }                                                                                           \
+  } while (0)
+
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lc = lane >> 4;
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+  constexpr uint32_t kStage = (BM + BN) * RB;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    abase[kk] = lds0 + (uint32_t)((wm * WM * 16 + lr) * RB + (((kk * 4 + lc) ^ ((lr >> 1) & 7)) * 16));
+    bbase[kk] = lds0 + (uint32_t)(BM * RB + (wn * WN * 16 + lr) * RB + (((kk * 4 + lc) ^ ((lr >> 1) & 7)) * 16));
+  }
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nsteps) RS_BISSUE(s);
+  int buf = 0;
+  for (int step = 0; step < nsteps; ++step) {
+    if (STAGES == 3 && step + 1 < nsteps) wait_vmcnt<NLD>();
+    else wait_vmcnt<0>();
+    asm volatile("s_barrier" ::: "memory");
+    const uint32_t so = buf * kStage;
+    u32x4_t fa[2][WM], fb[2][WN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[kk][mt]) : "v"(abase[kk] + so), "i"(mt * 16 * RB)
+                     : "memory");
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[kk][nt]) : "v"(bbase[kk] + so), "i"(nt * 16 * RB)
+                     : "memory");
+    }
+    if (step + STAGES - 1 < nsteps) RS_BISSUE(buf == 0 ? STAGES - 1 : buf - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) asm volatile("" : "+v"(fa[kk][mt]));
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) asm volatile("" : "+v"(fb[kk][nt]));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[kk][mt]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[kk][nt]),
+                                                                acc[mt][nt], 0, 0, 0);
+    buf = buf == STAGES - 1 ? 0 : buf + 1;
+  }
+
+#undef RS_BISSUE
+
+  int pb[WN], py[WN], px[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int p = n0 + nt * 16 + lr;
+    if (p < a.P) {
+      pb[nt] = p / HW;
+      const int q = p - pb[nt] * HW;
+      py[nt] = q / W;
+      px[nt] = q - py[nt] * W;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = 0;
+    }
+  }
+  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
 // ------------------------------------------------------------------ small-N variant
 // Cout <= 16 (the flow head's 256 -> 2 conv): one 16x16 output tile per block
 // (16 pixels), the K steps split over the 4 waves (step = wave mod 4), partial
@@ -827,7 +1014,9 @@ struct ConvLaunch {
   void* out3; int o3str, o3off;
   const void* aux1; int a1str, a1off;
   const void* aux2; int a2str, a2off;
-  int tile;  // 0: 32co x 32px per wave (2x2 waves); 1: 64co x 32px per wave
+  int tile;  // kernel variant (ops/conv.py choose_tile)
+  unsigned seg_bytes[3];  // bytes from seg_ptr to the end of its tensor (buffer range checks)
+  unsigned w_bytes;
 };
 
 void conv_launch(const ConvLaunch& L, hipStream_t stream) {
@@ -849,6 +1038,8 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.out3 = L.out3; a.o3str = L.o3str; a.o3off = L.o3off;
   a.aux1 = static_cast<const bf16_t*>(L.aux1); a.a1str = L.a1str; a.a1off = L.a1off;
   a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
+  for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
+  a.w_bytes = L.w_bytes;
   static const int xcd_env = [] {
     const char* e = getenv("RS_CONV_XCD_REMAP");
     return e ? atoi(e) : 1;
@@ -886,7 +1077,15 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
         case 12: RS_GLDS(128, 64, 32, 4); break;
         case 13: RS_GLDS(128, 64, 32, 3); break;
         case 14: RS_GLDS(64, 64, 32, 4); break;
-        default: RS_GLDS(64, 64, 64, 2); break;  // 15
+        case 15: RS_GLDS(64, 64, 64, 2); break;
+#define RS_BUF(BM_, BN_, ST_)                                                                        \
+  hipLaunchKernelGGL((conv::conv_buf_kernel<BM_, BN_, 2, 2, ST_>), dim3(cdiv(a.P, BN_) * cdiv(L.Cout, BM_)), \
+                     dim3(256), 0, stream, a)
+        case 16: RS_BUF(128, 64, 2); break;
+        case 17: RS_BUF(64, 64, 2); break;
+        case 18: RS_BUF(128, 64, 3); break;
+        default: RS_BUF(64, 64, 3); break;  // 19
+#undef RS_BUF
       }
 #undef RS_GLDS
     }

@@ -57,6 +57,11 @@ __device__ __forceinline__ v4s_t tr16(const uint16_t* lds_base, int byte_off) {
 
 constexpr int BK = 64;
 
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
 // Block: BM output channels x 64 input channels (one tap) x K split over
 // pixels; 4 waves (2 x 2), 64-pixel K steps staged in LDS in their natural
 // [pixel][channel] layout (16-byte rows copied as loaded) and read back as
@@ -72,11 +77,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][BK * (AROW + BROW)];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int ntile = blockIdx.x;
   const int nkb = a.Ktot / BN;
+  const int ntiles = a.taps * nkb, mtiles = cdiv(a.Cout, BM);
+  // XCD-aware order: the (tap, K-chunk, Cout) tiles of one pixel range are
+  // consecutive logical blocks, and each XCD walks a contiguous run of them,
+  // so a range's dY / X rows are fetched into one L2 and shared there
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = lid % ntiles;
+  const int m0 = (lid / ntiles % mtiles) * BM;
+  const int pbeg = lid / (ntiles * mtiles) * a.kchunk;
   const int tap = ntile / nkb, kb = (ntile % nkb) * BN;
-  const int m0 = blockIdx.y * BM;
-  const int pbeg = blockIdx.z * a.kchunk;
   const int pend = min(a.P, pbeg + a.kchunk);
   const int H = a.H, W = a.W, HW = H * W;
   const int dy_ = tap / a.KW - a.PH, dx_ = tap % a.KW - a.PW;
@@ -88,6 +98,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
   const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);
   const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);
   const int sper = si == 0 ? s0.period : (si == 1 ? s1.period : s2.period);
+  const int nbs = sper / HW;  // images in the segment (it repeats with that period)
   const int cbase = kb - (si == 0 ? 0 : (si == 1 ? c01 : c012));
   const bf16_t* ybase = a.dy + a.yoff + m0;
   const int ystr = a.ystr;
@@ -96,6 +107,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
   //                          B (pixel (t + 256 i) / CB, channel group t % CB)
   const int acg = t % CA, bcg = t % CB;
   u32x4_t ra[NA], rb[NB];
+  // (image within the segment period, y, x) of each B staging row's current pixel
+  int bb[NB], by[NB], bx[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int p = pbeg + (t + 256 * i) / CB;
+    const int b = p / HW, q = p - b * HW;
+    bb[i] = b % nbs;
+    by[i] = q / W;
+    bx[i] = q - by[i] * W;
+  }
   float bsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
@@ -110,11 +131,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
     }                                                                                            \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                             \
       const int p = (P0) + (t + 256 * i) / CB;                                                   \
-      const int q = p % HW, y = q / W + dy_, x = q % W + dx_;                                    \
+      const int y = by[i] + dy_, x = bx[i] + dx_;                                                \
       const bool ok = p < pend && y >= 0 && y < H && x >= 0 && x < W;                            \
-      const int src = ok ? (p - q) + y * W + x : 0;                                              \
-      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(sp + (size_t)(src % sper) * sst + cbase + bcg * 8); \
+      const int src = ok ? (bb[i] * H + y) * W + x : 0;                                          \
+      const u32x4_t v = *reinterpret_cast<const u32x4_t*>(sp + (size_t)src * sst + cbase + bcg * 8); \
       rb[i] = ok ? v : zero;                                                                     \
+      bx[i] += BK; /* advance this row's pixel by one K step */                                  \
+      while (bx[i] >= W) { bx[i] -= W; ++by[i]; }                                                \
+      while (by[i] >= H) { by[i] -= H; if (++bb[i] == nbs) bb[i] = 0; }                          \
     }                                                                                            \
   } while (0)
 #define RS_WG_STORE(BUF)                                                                         \
@@ -263,24 +287,27 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
     float bsum = 0.f;
     for (int r = 0; r < FROWS && y0 + r < H; ++r) {
       const bf16_t* grow = df + ((size_t)b * HW + (size_t)(y0 + r) * W) * fstr + co;
-      if (ci == 0)
-        for (int x = 0; x < W; ++x) bsum += bf2f(grow[(size_t)x * fstr]);
+      // x outer, taps inner: each dY value is loaded once and feeds 49 FMAs;
+      // the 7 padded flow rows slide through registers (win[ky][kx] = flow
+      // at (y0 + r + ky - 3, x + kx - 3))
+      float win[7][7];
 #pragma unroll
-      for (int ky = 0; ky < 7; ++ky) {
-        const float* frow = F + (r + ky) * WP;  // padded row: column x + kx of the image at index x + kx
-        float w0 = frow[0], w1 = frow[1], w2 = frow[2], w3 = frow[3], w4 = frow[4], w5 = frow[5];
-        for (int x = 0; x < W; ++x) {
-          const float w6 = frow[x + 6];
-          const float g = bf2f(grow[(size_t)x * fstr]);
-          acc[ky * 7 + 0] += g * w0;
-          acc[ky * 7 + 1] += g * w1;
-          acc[ky * 7 + 2] += g * w2;
-          acc[ky * 7 + 3] += g * w3;
-          acc[ky * 7 + 4] += g * w4;
-          acc[ky * 7 + 5] += g * w5;
-          acc[ky * 7 + 6] += g * w6;
-          w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-        }
+      for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 6; ++kx) win[ky][kx] = F[(r + ky) * WP + kx];
+      for (int x = 0; x < W; ++x) {
+        const float g = bf2f(grow[(size_t)x * fstr]);
+        bsum += g;
+#pragma unroll
+        for (int ky = 0; ky < 7; ++ky) win[ky][6] = F[(r + ky) * WP + x + 6];
+#pragma unroll
+        for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 7; ++kx) acc[ky * 7 + kx] += g * win[ky][kx];
+#pragma unroll
+        for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 6; ++kx) win[ky][kx] = win[ky][kx + 1];
       }
     }
 #pragma unroll
@@ -328,7 +355,7 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   ksplit = max(1, min(ksplit, cdiv(a.P, wgrad::BK * 8)));
   a.kchunk = round_up(cdiv(a.P, ksplit), wgrad::BK);
   ksplit = cdiv(a.P, a.kchunk);
-  dim3 grid(ntiles, mtiles, ksplit);
+  dim3 grid(ntiles * mtiles * ksplit);
   if (bn == 128)
     hipLaunchKernelGGL((wgrad::wgrad_kernel<128, 128>), grid, dim3(256), 0, stream, a, L.db);
   else if (bm == 128)

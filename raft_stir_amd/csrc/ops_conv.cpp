@@ -25,6 +25,8 @@ struct ConvLaunch {
   const void* aux1; int a1str, a1off;
   const void* aux2; int a2str, a2off;
   int tile;
+  unsigned seg_bytes[3];  // bytes from seg_ptr to the end of its tensor (buffer range checks)
+  unsigned w_bytes;
 };
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
@@ -87,18 +89,22 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
       L.seg_ptr[s] = static_cast<const at::BFloat16*>(segs[s].data_ptr()) + off;
       L.seg_C[s] = C;
       L.seg_stride[s] = Cb;
+      TORCH_CHECK(segs[s].numel() * 2 < (int64_t(1) << 31), "conv_fused: segment tensor must be < 2 GiB");
+      L.seg_bytes[s] = (unsigned)((segs[s].numel() - off) * 2);
       Ktot += C;
     } else {
       L.seg_ptr[s] = L.seg_ptr[0];
       L.seg_C[s] = 32;
       L.seg_stride[s] = L.seg_stride[0];
+      L.seg_bytes[s] = L.seg_bytes[0];
     }
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 15, "conv_fused: tile must be in [0,15]");
+  TORCH_CHECK(tile >= 0 && tile <= 19, "conv_fused: tile must be in [0,19]");
+  TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-19) support at most 32 taps");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
-  const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13);
+  const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13) || tile == 16 || tile == 18;
   const int tileM = tile == 0 ? 32 : (bm128 ? 128 : (tile == 5 ? 16 : 64));
   if (tile >= 6 && tile != 12 && tile != 13 && tile != 14)  // 64-deep K steps
     for (size_t s = 0; s < segs.size(); ++s)
@@ -114,6 +120,7 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
                 "conv_fused: bias must be fp32 (Cout,)");
   }
   L.w = w.data_ptr();
+  L.w_bytes = (unsigned)(w.numel() * 2);
   L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.B = B; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.PH = KH / 2; L.PW = KW / 2;
   L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;

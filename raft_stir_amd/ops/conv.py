@@ -50,18 +50,19 @@ def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
     return b.contiguous()
 
 
-def choose_tile(P: int, cout: int, seg_chans) -> int:
+def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
     """Kernel variant for a conv (measured on MI355X, scripts/bench_conv.py;
     profiles/conv_tiles_r1.md):
-    5 = split-K small-N (Cout <= 16); 6 = LDS-staged 64x64 tile with 64-deep K
-    steps; 11 = 128x64 tile fed by global->LDS DMA (2-stage ring, XCD-aware
-    block order) -- both need every segment % 64 == 0; 3/4 = 64x64 / 128x64
-    register-staged tiles with 32-deep K steps otherwise."""
+    5 = split-K small-N (Cout <= 16); 16 / 17 = 128x64 / 64x64 tiles fed by
+    buffer_load...lds DMA with a scalar K walk (every segment % 64 == 0, at
+    most 32 taps); 3/4 = 64x64 / 128x64 register-staged tiles with 32-deep K
+    steps otherwise."""
     if cout <= 16:
         return 5
+    if all(c % 64 == 0 for c in seg_chans) and taps <= 32:
+        k = taps * sum(seg_chans)
+        return 16 if (P >= 16384 and cout >= 192 and k >= 384) else 17
     big = cout >= 192 or (cout >= 126 and P >= 16384)
-    if all(c % 64 == 0 for c in seg_chans):
-        return 11 if big else 6
     return 4 if big else 3
 
 
@@ -74,6 +75,6 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
     chans = [int(s[2]) for s in segs]
     if tile is None:
         t0 = tensors[0]
-        tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans)
+        tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans, kh * kw)
     torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                    out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

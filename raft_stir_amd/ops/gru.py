@@ -79,9 +79,15 @@ def begin_forward():
 
 
 def _weights(convz, convr, convq, dt):
-    key = (id(convz), dt)
+    # keyed on the parameters' storage and version counters too: a module
+    # used outside RAFT.forward (no begin_forward) or a new module reusing a
+    # freed one's id must never see stale weights
+    ps = (convz.weight, convz.bias, convr.weight, convr.bias, convq.weight, convq.bias)
+    key = (id(convz), dt) + tuple((p.data_ptr(), p._version) for p in ps)
     w = _WCACHE.get(key)
     if w is None:
+        if len(_WCACHE) > 32:
+            _WCACHE.clear()
         wzr = torch.cat([convz.weight, convr.weight], dim=0).to(dt).contiguous(memory_format=_CL)
         bzr = torch.cat([convz.bias, convr.bias], dim=0).to(dt)
         wq = convq.weight.to(dt).contiguous(memory_format=_CL)

@@ -23,14 +23,14 @@ def _bf(x):
 
 
 @pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5), (5, 1)])
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7, 11, 15, 16, 17, 18, 19])
 @pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
 def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     torch.manual_seed(0)
     B, H, W = 2, 11, 19
     kh, kw = k
     # input = cat[a (40 ch, stored in a 64-wide buffer at offset 8), b (32 ch)]
-    cb = 64 if tile in (6, 7) else 32   # 64-deep K tiles need 64-channel segments
+    cb = 64 if tile >= 6 else 32   # 64-deep K tiles need 64-channel segments
     a_buf = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
     b_buf = torch.randn(B, H, W, cb, device=cuda).to(torch.bfloat16)
     x = torch.cat([a_buf[..., 8:48], b_buf], -1).float().permute(0, 3, 1, 2)
