@@ -42,6 +42,7 @@ struct Args {
   int Ktot, taps;
   float* dw;
   int kchunk;
+  unsigned dy_bytes, seg_bytes[3];
 };
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
@@ -242,6 +243,231 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
       }
 }
 
+// ------------------------------------------------------------------ DMA variant
+// Same block decomposition as wgrad_kernel, but both tiles are copied
+// global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging, no
+// ds_write) and the per-step address work is nearly all scalar:
+//  * dY rows: fixed per-lane offset + the step's scalar SOFFSET;
+//  * X rows: per-lane (image, y, x) advanced incrementally, one bounds test,
+//    out-of-image taps read past the buffer end (zeros);
+//  * LDS rows are unpadded (DMA writes lane-linear 1 KiB pieces), so the
+//    bank spread the +16 B pad gave the transpose reads comes from an XOR of
+//    the 32-B column block with (row & 3) instead, applied to the per-lane
+//    SOURCE chunk and to the tr16 read address.
+// The bias gradient of the first N tile is summed from the staged dY tile in
+// LDS.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restrict__ db) {
+  constexpr int RA = BM * 2, RB_ = BN * 2;               // bytes per staged pixel row
+  constexpr int CA = BM / 8, CB = BN / 8;                // 16-B chunks per row
+  constexpr int NA = BK * CA / 256, NB = BK * CB / 256;  // DMA instructions per thread
+  constexpr int WM = BM / 2 / 16, WN = BN / 2 / 16;
+  constexpr int kFar = 0x7ffffff0;
+  constexpr int STAGE = BK * (RA + RB_);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int nkb = a.Ktot / BN;
+  const int ntiles = a.taps * nkb, mtiles = cdiv(a.Cout, BM);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = lid % ntiles;
+  const int m0 = (lid / ntiles % mtiles) * BM;
+  const int pbeg = lid / (ntiles * mtiles) * a.kchunk;
+  const int tap = ntile / nkb, kb = (ntile % nkb) * BN;
+  const int pend = min(a.P, pbeg + a.kchunk);
+  const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
+  if (nsteps == 0) return;
+  const int H = a.H, W = a.W, HW = H * W;
+  const int dy_ = tap / a.KW - a.PH, dx_ = tap % a.KW - a.PW;
+  const bool do_bias = db != nullptr && ntile == 0;
+
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const int c01 = s0.C, c012 = s0.C + (a.nseg > 1 ? s1.C : 0);
+  const int si = (kb >= c01) + (kb >= c012);
+  const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);
+  const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);
+  const int sper = si == 0 ? s0.period : (si == 1 ? s1.period : s2.period);
+  const unsigned sbytes = si == 0 ? a.seg_bytes[0] : (si == 1 ? a.seg_bytes[1] : a.seg_bytes[2]);
+  const int nbs = sper / HW;
+  const int cbase = kb - (si == 0 ? 0 : (si == 1 ? c01 : c012));
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)sp, (short)0, sbytes, 0x00020000);
+
+  // staging: thread t, instruction i -> LDS chunk t + 256 i = (row, physical slot);
+  // the slot holds logical chunk slot ^ ((row & 3) << 1)
+  int arow[NA], aoff[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = t + 256 * i, r = id / CA, pos = id % CA;
+    arow[i] = r;
+    aoff[i] = ((pbeg + r) * a.ystr + a.yoff + m0 + ((pos ^ ((r & 3) << 1)) * 8)) * 2;
+  }
+  int bb[NB], by[NB], bx[NB], brow[NB], bch[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int id = t + 256 * i, r = id / CB, pos = id % CB;
+    brow[i] = r;
+    bch[i] = cbase + ((pos ^ ((r & 3) << 1)) * 8);
+    const int p = pbeg + r;
+    const int b = p / HW, q = p - b * HW;
+    bb[i] = b % nbs;
+    by[i] = q / W;
+    bx[i] = q - by[i] * W;
+  }
+  const int wbase = wave * 64;
+  const int ystep = BK * a.ystr * 2;  // dY bytes per K step
+
+#define RS_WD_ISSUE(S, BUF)                                                                     \
+  do {                                                                                          \
+    uint8_t* st_ = lds + (BUF) * STAGE;                                                         \
+    const int rem_ = pend - pbeg - (S) * BK;  /* valid rows in this step */                     \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                            \
+      const int v = arow[i] < rem_ ? aoff[i] : kFar;                                            \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                 \
+          ry, (__attribute__((address_space(3))) void*)(st_ + (wbase + 256 * i) * 16), 16, v,   \
+          (S) * ystep, 0, 0);                                                                   \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int y = by[i] + dy_, x = bx[i] + dx_;                                               \
+      const bool ok = brow[i] < rem_ && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W; \
+      const int v = ok ? (((bb[i] * H + y) * W + x) * sst + bch[i]) * 2 : kFar;                 \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                 \
+          rx, (__attribute__((address_space(3))) void*)(st_ + BK * RA + (wbase + 256 * i) * 16), \
+          16, v, 0, 0, 0);                                                                      \
+      bx[i] += BK;                                                                              \
+      while (bx[i] >= W) { bx[i] -= W; ++by[i]; }                                               \
+      while (by[i] >= H) { by[i] -= H; if (++bb[i] == nbs) bb[i] = 0; }                         \
+    }                                                                                           \
+  } while (0)
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
+  // bias: thread t sums logical chunk t % CA of rows t / CA + (256 / CA) j
+  const int bcol = t % CA;
+
+  const int gi = lane & 15, g = lane >> 4;
+  const int tq = gi >> 2, tp = gi & 3;
+  const int swq = tq << 1;  // (row & 3) << 1 for every row this lane's tr16 reads touch
+  // LDS reads are inline asm: the compiler cannot prove they miss the
+  // in-flight DMA of the next tile and would drain vmcnt in front of them
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  uint32_t aaddr[WM], baddr[WN];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt) {
+    const int ch = ((wm * (BM / 2) + mt * 16) / 8 + (tp >> 1)) ^ swq;  // 16-B chunk
+    aaddr[mt] = lds0 + (8 * g + tq) * RA + ch * 16 + (tp & 1) * 8;
+  }
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int ch = ((wn * (BN / 2) + nt * 16) / 8 + (tp >> 1)) ^ swq;
+    baddr[nt] = lds0 + BK * RA + (8 * g + tq) * RB_ + ch * 16 + (tp & 1) * 8;
+  }
+  RS_WD_ISSUE(0, 0);
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // tile s landed; buffer s-1 free
+    if (s + 1 < nsteps) RS_WD_ISSUE(s + 1, buf ^ 1);
+    const uint32_t so = buf * STAGE;
+    if (do_bias) {
+      u32x4_t bv[BK * CA / 256];
+#pragma unroll
+      for (int j = 0; j < BK * CA / 256; ++j) {
+        const int r = t / CA + (256 / CA) * j;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(bv[j])
+                     : "v"(lds0 + so + r * RA + ((bcol ^ ((r & 3) << 1)) * 16)) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < BK * CA / 256; ++j) {
+        asm volatile("" : "+v"(bv[j]));
+        bsum[0] += __uint_as_float(bv[j].x << 16);
+        bsum[1] += __uint_as_float(bv[j].x & 0xffff0000u);
+        bsum[2] += __uint_as_float(bv[j].y << 16);
+        bsum[3] += __uint_as_float(bv[j].y & 0xffff0000u);
+        bsum[4] += __uint_as_float(bv[j].z << 16);
+        bsum[5] += __uint_as_float(bv[j].z & 0xffff0000u);
+        bsum[6] += __uint_as_float(bv[j].w << 16);
+        bsum[7] += __uint_as_float(bv[j].w & 0xffff0000u);
+      }
+    }
+    // fragments of both 32-pixel halves: rows 32kk + 8g + tq (lo) and + 4 (hi)
+    v4s_t alo[2][WM], ahi[2][WM], blo[2][WN], bhi[2][WN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(alo[kk][mt]) : "v"(aaddr[mt] + so),
+                     "i"(kk * 32 * RA) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(ahi[kk][mt]) : "v"(aaddr[mt] + so),
+                     "i"((kk * 32 + 4) * RA) : "memory");
+      }
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(blo[kk][nt]) : "v"(baddr[nt] + so),
+                     "i"(kk * 32 * RB_) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(bhi[kk][nt]) : "v"(baddr[nt] + so),
+                     "i"((kk * 32 + 4) * RB_) : "memory");
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t fa[WM], fb[WN];
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) {
+        asm volatile("" : "+v"(alo[kk][mt]), "+v"(ahi[kk][mt]));
+        fa[mt] = bf16x8_t{alo[kk][mt].x, alo[kk][mt].y, alo[kk][mt].z, alo[kk][mt].w,
+                          ahi[kk][mt].x, ahi[kk][mt].y, ahi[kk][mt].z, ahi[kk][mt].w};
+      }
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) {
+        asm volatile("" : "+v"(blo[kk][nt]), "+v"(bhi[kk][nt]));
+        fb[nt] = bf16x8_t{blo[kk][nt].x, blo[kk][nt].y, blo[kk][nt].z, blo[kk][nt].w,
+                          bhi[kk][nt].x, bhi[kk][nt].y, bhi[kk][nt].z, bhi[kk][nt].w};
+      }
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    }
+  }
+#undef RS_WD_ISSUE
+  if (do_bias) {
+    // threads sharing a chunk column: reduce in LDS after the last use of the tiles
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t * 8 + j] = bsum[j];
+    __syncthreads();
+    if (t < CA) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float s = 0.f;
+        for (int u = t; u < 256; u += CA) s += red[u * 8 + j];
+        const int co = m0 + t * 8 + j;
+        if (co < a.Cout) atomicAdd(db + co, s);
+      }
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = m0 + wm * (BM / 2) + mt * 16 + (lane >> 4) * 4 + j;
+        const int k = kb + wn * (BN / 2) + nt * 16 + (lane & 15);
+        if (co < a.Cout) atomicAdd(a.dw + ((size_t)co * a.taps + tap) * a.Ktot + k, acc[mt][nt][j]);
+      }
+}
+
 // db[c] += sum_p dY[p][yoff + c]; block = 256 pixels, threads over channels.
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ dy, int ystr, int yoff,
                                                      int C, int P, float* __restrict__ db) {
@@ -328,6 +554,8 @@ struct WgradLaunch {
   float* dw;
   float* db;  // optional: bias gradient (column sums of dY) fused in
   int bn128;  // allow 128-wide N tiles
+  unsigned dy_bytes, seg_bytes[3];  // buffer range checks
+  int dma;  // 1: buffer-DMA kernel
 };
 
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
@@ -345,6 +573,8 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.KH = L.KH; a.KW = L.KW; a.PH = L.KH / 2; a.PW = L.KW / 2;
   a.Ktot = L.Ktot; a.taps = L.KH * L.KW;
   a.dw = L.dw;
+  a.dy_bytes = L.dy_bytes;
+  for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
   const int bm = a.Cout > 64 ? 128 : 64;
   bool seg128 = true;  // a 128-wide N tile must stay inside one segment
   for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
@@ -356,6 +586,15 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.kchunk = round_up(cdiv(a.P, ksplit), wgrad::BK);
   ksplit = cdiv(a.P, a.kchunk);
   dim3 grid(ntiles * mtiles * ksplit);
+  if (L.dma) {
+    if (bn == 128)
+      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128>), grid, dim3(256), 0, stream, a, L.db);
+    else if (bm == 128)
+      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 64>), grid, dim3(256), 0, stream, a, L.db);
+    else
+      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<64, 64>), grid, dim3(256), 0, stream, a, L.db);
+    return;
+  }
   if (bn == 128)
     hipLaunchKernelGGL((wgrad::wgrad_kernel<128, 128>), grid, dim3(256), 0, stream, a, L.db);
   else if (bm == 128)

@@ -7,6 +7,7 @@
 #include <torch/library.h>
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 namespace rs {
 struct ConvLaunch {
@@ -46,7 +47,8 @@ struct WgradLaunch {
   int Bp, H, W, KH, KW, Ktot;
   float* dw;
   float* db;
-  int bn128;
+  int bn128;  unsigned dy_bytes, seg_bytes[3];  // buffer range checks
+  int dma;  // 1: buffer-DMA kernel
 };
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream);
 void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream);
@@ -234,12 +236,15 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
       L.seg_C[s] = C;
       L.seg_stride[s] = t.size(3);
       L.seg_period[s] = per;
+      TORCH_CHECK(t.numel() * 2 < (int64_t(1) << 31), "conv_wgrad: segment tensor must be < 2 GiB");
+      L.seg_bytes[s] = (unsigned)((t.numel() - off) * 2);
       Ktot += C;
     } else {
       L.seg_ptr[s] = L.seg_ptr[0];
       L.seg_C[s] = 64;
       L.seg_stride[s] = L.seg_stride[0];
       L.seg_period[s] = L.seg_period[0];
+      L.seg_bytes[s] = L.seg_bytes[0];
     }
   }
   TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.scalar_type() == at::kFloat && dw.dim() == 3 &&
@@ -247,6 +252,13 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
               "conv_wgrad: dw must be fp32 (>=Cout, taps, Ktot)");
   const c10::DeviceGuard guard(dy.device());
   L.dy = dy.data_ptr(); L.ystr = dy.size(3); L.yoff = yoff; L.Cout = Cout;
+  TORCH_CHECK(dy.numel() * 2 < (int64_t(1) << 31), "conv_wgrad: dY tensor must be < 2 GiB");
+  L.dy_bytes = (unsigned)(dy.numel() * 2);
+  static const int dma_env = [] {
+    const char* e = getenv("RS_WGRAD_DMA");
+    return e ? atoi(e) : 1;
+  }();
+  L.dma = dma_env;
   L.nseg = segs.size();
   L.Bp = Bp; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.Ktot = Ktot;
   L.dw = dw.data_ptr<float>();

@@ -380,13 +380,13 @@ class FusedTrainLoop(torch.autograd.Function):
 
         wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
         wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
-        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)], bn128=1)
+        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)])
         hins = [hxs, S["h1"]]
         for p in range(2):
             wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
             wg(eng.q[p], S["d_q"][p], 0, [(S["rh"][p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
         wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)])
-        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], bn128=1)
+        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)])
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
