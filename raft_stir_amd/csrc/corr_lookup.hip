@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrMut gpyr, int levels
 
 // G0 = scale * (g0 + g1/4 + g2/16 + g3/64) expanded to level-0 cells, in place.
 __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, long rows,
-                                                       float scale) {
+                                                       float scale, bf16_t* __restrict__ out_bf16) {
   const int H0 = g.H[0], W0 = g.W[0];
   const long total = rows * H0 * W0;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -151,7 +151,10 @@ __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, lon
       if (yl < g.H[l] && xl < g.W[l])
         v += w * g.p[l][row * (size_t)g.H[l] * g.W[l] + (size_t)yl * g.W[l] + xl];
     }
-    g.p[0][idx] = v * scale;
+    if (out_bf16)
+      out_bf16[idx] = f2bf(v * scale);  // GEMM operand for the fmap gradients
+    else
+      g.p[0][idx] = v * scale;
   }
 }
 
@@ -207,7 +210,7 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
 }
 
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
-                          float scale, hipStream_t stream) {
+                          float scale, hipStream_t stream, void* out_bf16) {
   lookup::PyrMut p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? gpyr[l] : nullptr;
@@ -217,7 +220,7 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int 
   const long total = rows * Hs[0] * Ws[0];
   if (total == 0) return;
   hipLaunchKernelGGL(lookup::pyr_fold_kernel, dim3(lookup::grid_for(total)), dim3(256), 0, stream,
-                     p, levels, rows, scale);
+                     p, levels, rows, scale, static_cast<bf16_t*>(out_bf16));
 }
 
 }  // namespace rs

@@ -186,33 +186,39 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
 }
 
 // Combine partials: MODE 0 -> mean/rstd, MODE 1 -> s1/s2.
-// Block (g, 32-channel chunk): 8 row-groups of 32 lanes each sum a strided
-// share of the (b, s) partials in fp64, then an LDS reduction across groups.
+// Block (g, 8-channel chunk): 32 row-groups of 8 lanes each sum a strided
+// share of the (b, s) partials in fp64, then an LDS tree across the groups
+// (short serial chains: batch-norm groups have B * S partials per channel).
 template <int MODE>
 __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, int S, int C, int G,
                                                        float eps, float inv_n, float* o0, float* o1) {
   const int g = blockIdx.x;
-  const int c = blockIdx.y * 32 + (threadIdx.x & 31);
-  const int part = threadIdx.x >> 5;
+  const int c = blockIdx.y * 8 + (threadIdx.x & 7);
+  const int part = threadIdx.x >> 3;
   const int b0 = G == 1 ? 0 : g, nb = G == 1 ? B : 1;
   double t0 = 0.0, t1 = 0.0;
   if (c < C) {
-    for (int i = part; i < nb * S; i += 8) {
+    for (int i = part; i < nb * S; i += 32) {
       const int b = b0 + i / S, s = i % S;
       const float* w = ws + (((size_t)b * S + s) * C + c) * 2;
       t0 += w[0];
       t1 += w[1];
     }
   }
-  __shared__ double sm[2][8][32];
-  sm[0][part][threadIdx.x & 31] = t0;
-  sm[1][part][threadIdx.x & 31] = t1;
+  __shared__ double sm[2][256];
+  sm[0][threadIdx.x] = t0;
+  sm[1][threadIdx.x] = t1;
   __syncthreads();
-  if (part == 0 && c < C) {
-    for (int p = 1; p < 8; ++p) {
-      t0 += sm[0][p][threadIdx.x];
-      t1 += sm[1][p][threadIdx.x];
+  for (int st = 128; st >= 8; st >>= 1) {
+    if (threadIdx.x < st) {
+      sm[0][threadIdx.x] += sm[0][threadIdx.x + st];
+      sm[1][threadIdx.x] += sm[1][threadIdx.x + st];
     }
+    __syncthreads();
+  }
+  if (threadIdx.x < 8 && c < C) {
+    t0 = sm[0][threadIdx.x];
+    t1 = sm[1][threadIdx.x];
     const int idx = g * C + c;
     if (MODE == 0) {
       const double m = t0 * inv_n;
@@ -396,7 +402,7 @@ void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, flo
   else
     hipLaunchKernelGGL((norm::reduce_kernel<float, 0>), grid, dim3(norm::THREADS), 0, s, a);
   const float inv_n = 1.f / (float)((G == 1 ? (double)B : 1.0) * P);
-  hipLaunchKernelGGL(norm::finalize_kernel<0>, dim3(G, cdiv(C, 32)), dim3(256), 0, s, ws, B, a.S,
+  hipLaunchKernelGGL(norm::finalize_kernel<0>, dim3(G, cdiv(C, 8)), dim3(256), 0, s, ws, B, a.S,
                      C, G, eps, inv_n, mean, rstd);
 }
 
@@ -426,7 +432,7 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
     hipLaunchKernelGGL((norm::reduce_kernel<bf16_t, 1>), grid, dim3(norm::THREADS), 0, s, a);
   else
     hipLaunchKernelGGL((norm::reduce_kernel<float, 1>), grid, dim3(norm::THREADS), 0, s, a);
-  hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 32)), dim3(256), 0, s, ws, B, a.S,
+  hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 8)), dim3(256), 0, s, ws, B, a.S,
                      C, G, 0.f, 0.f, s1, s2);
   a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres;
   a.inv_n = batch_stats ? 1.f / (float)((G == 1 ? (double)B : 1.0) * P) : 0.f;

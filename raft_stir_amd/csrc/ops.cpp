@@ -27,7 +27,7 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
-                          float scale, hipStream_t stream);
+                          float scale, hipStream_t stream, void* out_bf16 = nullptr);
 bool corr_otf_supported_channels(int C);
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
@@ -199,6 +199,22 @@ void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
+}
+
+// Same fold, written as bf16 into `out` (B, N1, H0, W0) instead of in place:
+// the operand of the bf16 fmap-gradient GEMMs.
+void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Tensor& out) {
+  TORCH_CHECK(!gpyr.empty() && gpyr.size() <= 4, "pyramid must have 1..4 levels");
+  const int B = gpyr[0].size(0), N1 = gpyr[0].size(1);
+  int Hs[4], Ws[4];
+  check_pyr(gpyr, B, N1, Hs, Ws);
+  check_gpu(out, "out");
+  check_dtype(out, {at::kBFloat16}, "out");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == gpyr[0].numel(), "pyr_grad_fold_bf16: out shape");
+  const c10::DeviceGuard guard(gpyr[0].device());
+  float* ptrs[4];
+  for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), out.data_ptr());
 }
 
 // ---------------------------------------------------------------- on-the-fly corr
@@ -414,6 +430,7 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("corr_lookup_into(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_lookup_backward(Tensor(a!)[] gpyr, Tensor coords, int radius, Tensor dout) -> ()");
   m.def("pyr_grad_fold(Tensor(a!)[] gpyr, float scale) -> ()");
+  m.def("pyr_grad_fold_bf16(Tensor[] gpyr, float scale, Tensor(a!) out) -> ()");
   m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
   m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
@@ -431,6 +448,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("corr_lookup_into", &corr_lookup_into);
   m.impl("corr_lookup_backward", &corr_lookup_backward);
   m.impl("pyr_grad_fold", &pyr_grad_fold);
+  m.impl("pyr_grad_fold_bf16", &pyr_grad_fold_bf16);
   m.impl("corr_otf", &corr_otf);
   m.impl("corr_otf_backward", &corr_otf_backward);
   m.impl("convex_upsample", &convex_upsample);

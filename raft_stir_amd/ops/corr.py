@@ -72,10 +72,18 @@ class _CorrVolume(torch.autograd.Function):
             return None, None, None
         B, N1, C = f1.shape
         _, H2, W2, _ = f2.shape
-        torch.ops.raft_stir.pyr_grad_fold(state.gpyr, state.scale)
-        G = state.gpyr[0].view(B, N1, H2 * W2)
-        df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C).float())
-        df2 = torch.bmm(G.transpose(1, 2), f1.float())
+        if f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16:
+            # bf16 GEMMs (fp32 accumulation) on a bf16 copy of the folded
+            # gradient: ~5x faster than the fp32 GEMMs on MI355X
+            G = torch.empty(B, N1, H2 * W2, device=f1.device, dtype=torch.bfloat16)
+            torch.ops.raft_stir.pyr_grad_fold_bf16(state.gpyr, state.scale, G)
+            df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
+            df2 = torch.bmm(G.transpose(1, 2), f1)
+        else:
+            torch.ops.raft_stir.pyr_grad_fold(state.gpyr, state.scale)
+            G = state.gpyr[0].view(B, N1, H2 * W2)
+            df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C).float())
+            df2 = torch.bmm(G.transpose(1, 2), f1.float())
         state.gpyr = None
         state.pyr = None
         return df1.to(f1.dtype), df2.view(B, H2, W2, C).to(f2.dtype), None

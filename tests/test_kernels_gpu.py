@@ -179,3 +179,25 @@ def test_fused_gru_pass(cuda, sep):
     torch.testing.assert_close(xb.grad.cpu(), xa.grad, rtol=1e-3, atol=1e-3)
     for n, p in m2.named_parameters():
         torch.testing.assert_close(p.grad.cpu(), ref_grads[n], rtol=1e-3, atol=2e-3)
+
+
+def test_allpairs_corr_autograd_bf16(cuda):
+    """bf16 feature maps: the folded pyramid gradient goes through bf16 GEMMs."""
+    from raft_stir_amd.ops.corr import AllPairsCorr
+    B, C, H, W, r = 2, 256, 17, 21, 4
+    f1, f2 = _fmaps(B, C, H, W, "cpu", seed=5)
+    f1, f2 = f1.bfloat16().float(), f2.bfloat16().float()
+    coords = [_coords(B, H, W, "cpu", seed=s) for s in range(2)]
+    g = torch.Generator().manual_seed(9)
+    wts = [torch.randn(B, 4 * (2 * r + 1) ** 2, H, W, generator=g) for _ in coords]
+    a1, a2 = f1.clone().requires_grad_(), f2.clone().requires_grad_()
+    pyr = ref.corr_pyramid(a1, a2, 4)
+    sum((ref.corr_lookup(pyr, c, r) * w).sum() for c, w in zip(coords, wts)).backward()
+    b1 = f1.to(cuda).bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_()
+    b2 = f2.to(cuda).bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_()
+    blk = AllPairsCorr(b1, b2, 4, r)
+    sum((blk(c.to(cuda)).float() * w.to(cuda)).sum() for c, w in zip(coords, wts)).backward()
+    for got, want in ((b1.grad, a1.grad), (b2.grad, a2.grad)):
+        got = got.float().cpu()
+        rel = (got - want).norm() / want.norm()
+        assert rel < 2e-2, rel
