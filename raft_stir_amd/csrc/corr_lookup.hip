@@ -131,6 +131,121 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrMut gpyr, int levels
   }
 }
 
+// ---------------------------------------------------------------- wave-per-pixel variants
+// (radius 3 / 4, the RAFT-small / RAFT configurations).  One wave owns one
+// pixel; per level the (2r+2)^2 integer cells its window touches are staged
+// in LDS with x-fastest (row-coalesced) loads, then each lane produces output
+// channels from LDS with the level's shared bilinear weights (every tap has
+// the same fractional offset).  All index math is 32-bit with compile-time
+// divisors.  Backward mirrors it: the pixel's dout slice is staged in LDS and
+// each lane gathers the <= 4 taps of one cell, then updates its pyramid-
+// gradient row with x-fastest (coalesced) read-modify-writes.
+template <typename P>
+__device__ __forceinline__ auto lvl_ptr(const P& pyr, int l) {
+  return l == 0 ? pyr.p[0] : (l == 1 ? pyr.p[1] : (l == 2 ? pyr.p[2] : pyr.p[3]));
+}
+template <typename P>
+__device__ __forceinline__ int lvl_H(const P& pyr, int l) {
+  return l == 0 ? pyr.H[0] : (l == 1 ? pyr.H[1] : (l == 2 ? pyr.H[2] : pyr.H[3]));
+}
+template <typename P>
+__device__ __forceinline__ int lvl_W(const P& pyr, int l) {
+  return l == 0 ? pyr.W[0] : (l == 1 ? pyr.W[1] : (l == 2 ? pyr.W[2] : pyr.W[3]));
+}
+
+template <int R, typename OutT>
+__global__ __launch_bounds__(256) void lookup_fwd_wave_kernel(Pyr pyr, int levels, const float* __restrict__ coords,
+                                                              int N1, int P, OutT* __restrict__ out, int ostride) {
+  constexpr int D = 2 * R + 1, K2 = D * D, E = D + 1, E2 = E * E;
+  __shared__ float win[4][4][E2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pix = blockIdx.x * 4 + w;
+  if (pix >= P) return;
+  const int b = pix / N1, n = pix - b * N1;
+  const float cx0 = coords[(size_t)(b * 2) * N1 + n], cy0 = coords[(size_t)(b * 2 + 1) * N1 + n];
+  float fxs[4], fys[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    if (l >= levels) break;
+    const float inv = 1.f / (float)(1 << l);
+    const float cx = cx0 * inv, cy = cy0 * inv;
+    const float bx = floorf(cx), by = floorf(cy);
+    fxs[l] = cx - bx;
+    fys[l] = cy - by;
+    const int X0 = (int)bx - R, Y0 = (int)by - R;
+    const int H = lvl_H(pyr, l), W = lvl_W(pyr, l);
+    const float* row = lvl_ptr(pyr, l) + (size_t)pix * H * W;
+    for (int idx = lane; idx < E2; idx += 64) {
+      const int c = idx / E, a = idx - c * E;
+      const int X = X0 + a, Y = Y0 + c;
+      win[w][l][idx] = (X >= 0 && X < W && Y >= 0 && Y < H) ? row[(size_t)Y * W + X] : 0.f;
+    }
+  }
+  // each wave only touches its own LDS slice: a wave-level ordering point suffices
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int CH = levels * K2;
+  OutT* o = out + (size_t)pix * ostride;
+  for (int ch = lane; ch < ostride; ch += 64) {
+    float v = 0.f;
+    if (ch < CH) {
+      const int l = ch / K2, k = ch - l * K2;
+      const int i = k / D, j = k - i * D;  // i: x tap, j: y tap
+      const float fx = l == 0 ? fxs[0] : (l == 1 ? fxs[1] : (l == 2 ? fxs[2] : fxs[3]));
+      const float fy = l == 0 ? fys[0] : (l == 1 ? fys[1] : (l == 2 ? fys[2] : fys[3]));
+      const float* L = win[w][l] + j * E + i;
+      v = (1.f - fy) * ((1.f - fx) * L[0] + fx * L[1]) + fy * ((1.f - fx) * L[E] + fx * L[E + 1]);
+    }
+    io<OutT>::st(o + ch, v);
+  }
+}
+
+template <int R, typename GT>
+__global__ __launch_bounds__(256) void lookup_bwd_wave_kernel(PyrMut gpyr, int levels, const float* __restrict__ coords,
+                                                              int N1, int P, const GT* __restrict__ dout,
+                                                              int dstride) {
+  constexpr int D = 2 * R + 1, K2 = D * D, E = D + 1, E2 = E * E;
+  __shared__ float gs[4][4][K2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pix = blockIdx.x * 4 + w;
+  if (pix >= P) return;
+  const int b = pix / N1, n = pix - b * N1;
+  const float cx0 = coords[(size_t)(b * 2) * N1 + n], cy0 = coords[(size_t)(b * 2 + 1) * N1 + n];
+  const GT* g = dout + (size_t)pix * dstride;
+  for (int idx = lane; idx < levels * K2; idx += 64) gs[w][idx / K2][idx % K2] = io<GT>::ld(g + idx);
+  // each wave only touches its own LDS slice: a wave-level ordering point suffices
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    if (l >= levels) break;
+    const float inv = 1.f / (float)(1 << l);
+    const float cx = cx0 * inv, cy = cy0 * inv;
+    const float bx = floorf(cx), by = floorf(cy);
+    const float fx = cx - bx, fy = cy - by;
+    const int X0 = (int)bx - R, Y0 = (int)by - R;
+    const int H = lvl_H(gpyr, l), W = lvl_W(gpyr, l);
+    float* row = lvl_ptr(gpyr, l) + (size_t)pix * H * W;
+    const float* G = gs[w][l];  // G[i * D + j], i: x tap, j: y tap
+    for (int idx = lane; idx < E2; idx += 64) {
+      const int c = idx / E, a = idx - c * E;  // cell (x = a, y = c), x fastest
+      const int X = X0 + a, Y = Y0 + c;
+      if (X < 0 || X >= W || Y < 0 || Y >= H) continue;
+      float acc = 0.f;
+      // tap i = a uses this cell as its lower x-corner (1 - fx), tap a - 1 as its upper (fx)
+      if (a < D) {
+        if (c < D) acc += (1.f - fx) * (1.f - fy) * G[a * D + c];
+        if (c > 0) acc += (1.f - fx) * fy * G[a * D + c - 1];
+      }
+      if (a > 0) {
+        if (c < D) acc += fx * (1.f - fy) * G[(a - 1) * D + c];
+        if (c > 0) acc += fx * fy * G[(a - 1) * D + c - 1];
+      }
+      row[(size_t)Y * W + X] += acc;
+    }
+  }
+}
+
 // G0 = scale * (g0 + g1/4 + g2/16 + g3/64) expanded to level-0 cells, in place.
 __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, long rows,
                                                        float scale, bf16_t* __restrict__ out_bf16) {
@@ -179,6 +294,17 @@ void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* W
   if (ostride <= 0) ostride = CH;
   const long total = (long)B * H1 * W1 * ostride;
   if (total == 0) return;
+  const long P = (long)B * H1 * W1;
+  if ((r == 3 || r == 4) && P < (1L << 30)) {
+    const dim3 g((unsigned)((P + 3) / 4));
+#define RS_LF(R_, T_)                                                                                    \
+  hipLaunchKernelGGL((lookup::lookup_fwd_wave_kernel<R_, T_>), g, dim3(256), 0, stream, p, levels, coords, \
+                     H1 * W1, (int)P, static_cast<T_*>(out), ostride)
+    if (r == 3) { if (out_bf16) RS_LF(3, bf16_t); else RS_LF(3, float); }
+    else { if (out_bf16) RS_LF(4, bf16_t); else RS_LF(4, float); }
+#undef RS_LF
+    return;
+  }
   const int grid = lookup::grid_for(total);
   if (out_bf16)
     hipLaunchKernelGGL(lookup::lookup_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, p,
@@ -200,6 +326,17 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
   }
   const long total = (long)B * H1 * W1 * levels * (2 * r + 2) * (2 * r + 2);
   if (total == 0) return;
+  const long P = (long)B * H1 * W1;
+  if ((r == 3 || r == 4) && P < (1L << 30)) {
+    const dim3 g((unsigned)((P + 3) / 4));
+#define RS_LB(R_, T_)                                                                                    \
+  hipLaunchKernelGGL((lookup::lookup_bwd_wave_kernel<R_, T_>), g, dim3(256), 0, stream, p, levels, coords, \
+                     H1 * W1, (int)P, static_cast<const T_*>(dout), dstride)
+    if (r == 3) { if (dout_bf16) RS_LB(3, bf16_t); else RS_LB(3, float); }
+    else { if (dout_bf16) RS_LB(4, bf16_t); else RS_LB(4, float); }
+#undef RS_LB
+    return;
+  }
   const int grid = lookup::grid_for(total);
   if (dout_bf16)
     hipLaunchKernelGGL(lookup::lookup_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, p,
