@@ -130,7 +130,7 @@ def main():
                 "parallelism": f"dp{info.world_size}",
                 "ops": "stock-pytorch (reference semantics)" if a.reference_ops else "hip-kernels",
             },
-            "final_loss": round(float(loss), 4),
+            "final_loss": round(float(loss.detach()), 4),
             "inference": infer,
         }
         print(json.dumps(out), flush=True)

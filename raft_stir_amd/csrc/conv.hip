@@ -84,18 +84,115 @@ struct Args {
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Shared epilogue: acc[mt][nt][j] holds output channel m0 + mt*16 + 4*(lane>>4) + j
-// of pixel n0 + nt*16 + (lane&15).
-template <int WM, int WN>
-__device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int n0,
-                                         int lane, const int (&pb)[WN], const int (&py)[WN],
+// of flat pixel pp[nt] = (pb*H + py)*W + px (pb < 0: no pixel).  The epilogue
+// kind is a template parameter of the fragment loop (dispatched once, outside
+// it): with a runtime switch inside, the 16-fragment loops of the 4x4 wave
+// tiles were too large to unroll and the accumulators went to scratch.
+template <int E>
+__device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, int p, int pb, int py, int px,
+                                         int HW) {
+  if constexpr (E == EPI_FLOW) {  // coords (+)= delta; out2 (if set) is the source coords
+    float* crd = static_cast<float*>(a.out);
+    const float* src = a.out2 ? static_cast<const float*>(a.out2) : crd;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = cb + j;
+      if (co < a.Cout && co < 2) {
+        const size_t o = ((size_t)pb * 2 + co) * HW + (size_t)py * a.W + px;
+        crd[o] = src[o] + v[j];
+      }
+    }
+  } else if constexpr (E == EPI_GRU_ZR) {
+    if (cb < a.hd) {
+      bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
+    } else {
+      const int c = cb - a.hd;
+      const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
+      bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
+      bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float r = sigmoidf_(v[j]);
+        rh[j] = f2bf(r * bf2f(h[j]));
+        if (rs_) rs_[j] = f2bf(r);
+      }
+    }
+  } else if constexpr (E == EPI_GRU_Q) {
+    const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+    const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+    bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
+    float hv[4], zv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hv[j] = bf2f(h[j]);
+      zv[j] = bf2f(z[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float q = tanhf_(v[j]);
+      hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
+      if (qs) qs[j] = f2bf(q);
+    }
+  } else if constexpr (E == EPI_RELU_BWD) {
+    const bf16_t* act = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
+  } else if constexpr (E == EPI_ACC_F32) {
+    float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cb + j < a.Cout) o[j] += v[j];
+  } else if constexpr (E == EPI_GRU_QBWD) {
+    float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (cb < a.hd) {
+      const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+      const bf16_t* r = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+      bf16_t* drp = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float rv = bf2f(r[j]), hv = bf2f(h[j]);
+        drp[j] = f2bf(v[j] * hv * rv * (1.f - rv));
+        o[j] += v[j] * rv;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] += v[j];
+    }
+  } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE -> bf16
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (E == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+      if constexpr (E == EPI_SCALE) v[j] *= a.scale;
+    }
+    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (cb + 3 < a.Cout && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
+      uint2 pk;
+      pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+      pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+      *reinterpret_cast<uint2*>(o) = pk;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = f2bf(v[j]);
+    }
+  }
+}
+
+template <int WM, int WN, int E>
+__device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                         const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
                                          const int (&px)[WN]) {
-  const int lr = lane & 15;
   const int HW = a.H * a.W;
   const int cq = (lane >> 4) * 4;
 #pragma unroll
   for (int nt = 0; nt < WN; ++nt) {
     if (pb[nt] < 0) continue;
-    const int p = n0 + nt * 16 + lr;
 #pragma unroll
     for (int mt = 0; mt < WM; ++mt) {
       const int cb = m0 + mt * 16 + cq;
@@ -103,114 +200,40 @@ __device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM]
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
-      const bool full = cb + 3 < a.Cout;
-      switch (a.epi) {
-        case EPI_FLOW: {  // coords (+)= delta; out2 (if set) is the source coords
-          float* crd = static_cast<float*>(a.out);
-          const float* src = a.out2 ? static_cast<const float*>(a.out2) : crd;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int co = cb + j;
-            if (co < a.Cout && co < 2) {
-              const size_t o = ((size_t)pb[nt] * 2 + co) * HW + (size_t)py[nt] * a.W + px[nt];
-              crd[o] = src[o] + v[j];
-            }
-          }
-          break;
-        }
-        case EPI_GRU_ZR: {
-          if (cb < a.hd) {
-            bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
-          } else {
-            const int c = cb - a.hd;
-            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
-            bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
-            bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float r = sigmoidf_(v[j]);
-              rh[j] = f2bf(r * bf2f(h[j]));
-              if (rs_) rs_[j] = f2bf(r);
-            }
-          }
-          break;
-        }
-        case EPI_GRU_Q: {
-          const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
-          const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
-          bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-          bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
-          float hv[4], zv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            hv[j] = bf2f(h[j]);
-            zv[j] = bf2f(z[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float q = tanhf_(v[j]);
-            hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
-            if (qs) qs[j] = f2bf(q);
-          }
-          break;
-        }
-        case EPI_RELU_BWD: {
-          const bf16_t* act = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
-          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
-          break;
-        }
-        case EPI_ACC_F32: {
-          float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (cb + j < a.Cout) o[j] += v[j];
-          break;
-        }
-        case EPI_GRU_QBWD: {
-          float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-          if (cb < a.hd) {
-            const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
-            const bf16_t* r = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
-            bf16_t* drp = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float rv = bf2f(r[j]), hv = bf2f(h[j]);
-              drp[j] = f2bf(v[j] * hv * rv * (1.f - rv));
-              o[j] += v[j] * rv;
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (cb + j < a.Cout) o[j] += v[j];
-          }
-          break;
-        }
-        default: {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (a.epi == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
-            else if (a.epi == EPI_SCALE) v[j] *= a.scale;
-          }
-          bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-          if (full && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
-            uint2 pk;
-            pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-            pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-            *reinterpret_cast<uint2*>(o) = pk;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (cb + j < a.Cout) o[j] = f2bf(v[j]);
-          }
-        }
-      }
+      epi_frag<E>(a, v, cb, pp[nt], pb[nt], py[nt], px[nt], HW);
     }
   }
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                             const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
+                                             const int (&px)[WN]) {
+  switch (a.epi) {
+#define RS_EPI(E) \
+  case E: epi_loop<WM, WN, E>(a, acc, m0, lane, pp, pb, py, px); break
+    RS_EPI(EPI_FLOW);
+    RS_EPI(EPI_GRU_ZR);
+    RS_EPI(EPI_GRU_Q);
+    RS_EPI(EPI_RELU_BWD);
+    RS_EPI(EPI_ACC_F32);
+    RS_EPI(EPI_GRU_QBWD);
+    RS_EPI(EPI_RELU);
+    RS_EPI(EPI_SCALE);
+#undef RS_EPI
+    default: epi_loop<WM, WN, EPI_BIAS>(a, acc, m0, lane, pp, pb, py, px); break;
+  }
+}
+
+// Linear pixel tiles: the B columns of n-tile nt are pixels n0 + nt*16 + (lane&15).
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int n0,
+                                         int lane, const int (&pb)[WN], const int (&py)[WN],
+                                         const int (&px)[WN]) {
+  int pp[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) pp[nt] = n0 + nt * 16 + (lane & 15);
+  epilogue_pix<WM, WN>(a, acc, m0, lane, pp, pb, py, px);
 }
 
 template <int WM, int WN, int WAVES_M, int WAVES_N>
@@ -681,7 +704,7 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base
 template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
 __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
-  static_assert(STAGES >= 2 && STAGES <= 3, "STAGES");
+  static_assert(STAGES >= 2 && STAGES <= 4, "STAGES");
   constexpr int BK = 64, CPR = 8, RB = 128;
   constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
   constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
@@ -788,7 +811,10 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
     if (s < nsteps) RS_BISSUE(s);
   int buf = 0;
   for (int step = 0; step < nsteps; ++step) {
-    if (STAGES == 3 && step + 1 < nsteps) wait_vmcnt<NLD>();
+    // retire this step's copies; keep up to STAGES-2 later steps in flight
+    const int ahead = min(STAGES - 2, nsteps - 1 - step);
+    if (STAGES >= 4 && ahead >= 2) wait_vmcnt<2 * NLD>();
+    else if (STAGES >= 3 && ahead >= 1) wait_vmcnt<NLD>();
     else wait_vmcnt<0>();
     asm volatile("s_barrier" ::: "memory");
     const uint32_t so = buf * kStage;
@@ -842,6 +868,187 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
     }
   }
   epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
+// ------------------------------------------------------------------ halo (patch) variant
+// conv_buf_kernel stages a fresh BN-pixel x 64-channel tile for EVERY (tap,
+// chunk) K step: a 3x3 conv fetches each input row 9 times from L2, and at
+// the training shape the kernel runs at the L2 -> LDS rate (~11 TB/s,
+// profiles/conv_tiles_r1.md), not at the MFMA rate.  Here the pixel tile is a
+// TH x 16 patch of ONE image.  Per 64-channel chunk the block stages the
+// patch's (TH+KH-1) x (16+KW-1) halo once -- pixels outside the image read
+// past the buffer end, i.e. as zeros, so padding needs no per-tap masks --
+// and every tap reads its shifted window of it from LDS.  Per K step only the
+// weight tile is fetched; the halo costs ~1/taps of a pixel tile.
+// K walk: segment -> chunk -> tap (tap innermost).  Two-stage weight ring;
+// the halo is double-buffered and issued together with the weights of its
+// chunk's first tap (one step ahead); the buffer it overwrites was last read
+// two chunks back, i.e. before the previous step's barrier.
+template <int BM, int TH, int HCAP>
+__global__ __launch_bounds__(256) void conv_halo_kernel(Args a) {
+  constexpr int TW = 16, BN = TH * TW;
+  constexpr int WM = BM / 2 / 16, WN = BN / 2 / 16;  // 2 x 2 waves
+  constexpr int NA = BM * 8 / 256, NH = HCAP * 8 / 256;
+  constexpr int AST = BM * 8, HST = HCAP * 8;  // 16-B chunks per weight stage / halo buffer
+  constexpr int kFar = 0x7ffffff0;
+  __shared__ uint4 lds[2 * AST + 2 * HST];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int H = a.H, W = a.W, KW = a.KW, Ktot = a.Ktot;
+  const int taps = a.KH * KW;
+  const int hw = TW + KW - 1;               // halo row width
+  const int hrows = (TH + a.KH - 1) * hw;   // halo pixels (<= HCAP, host-checked)
+  const int ntx = cdiv(W, TW), npb = cdiv(H, TH) * ntx;
+  const int nct = cdiv(a.Cout, BM);
+  const int lid = a.xcd_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int bm0 = (lid % nct) * BM;
+  const int pt = lid / nct;
+  const int img = pt / npb, pq = pt - img * npb;
+  const int pty = pq / ntx;
+  const int y0 = pty * TH, x0 = (pq - pty * ntx) * TW;
+  const int m0 = bm0 + wm * WM * 16;
+
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const __amdgpu_buffer_rsrc_t rs0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s0.ptr, (short)0, a.seg_bytes[0], 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s1.ptr, (short)0, a.seg_bytes[1], 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)s2.ptr, (short)0, a.seg_bytes[2], 0x00020000);
+
+  // staging slot (thread t, instruction i) = chunk t + 256 i: row r = slot / 8,
+  // physical 16-B slot holding logical chunk (slot % 8) ^ ((r >> 1) & 7)
+  int aoff[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int id = t + 256 * i, r = id >> 3;
+    aoff[i] = ((bm0 + r) * taps * Ktot + (((id & 7) ^ ((r >> 1) & 7)) * 8)) * 2;
+  }
+  int hpix[NH], hch[NH];
+#pragma unroll
+  for (int i = 0; i < NH; ++i) {
+    const int id = t + 256 * i, r = id >> 3;
+    hch[i] = ((id & 7) ^ ((r >> 1) & 7)) * 8;
+    hpix[i] = -1;
+    if (r < hrows) {
+      const int hy = r / hw, hx = r - hy * hw;
+      const int y = y0 + hy - a.PH, x = x0 + hx - a.PW;
+      if (y >= 0 && y < H && x >= 0 && x < W) hpix[i] = (img * H + y) * W + x;
+    }
+  }
+  const int wbase = wave * 64;
+  const int nsteps =
+      taps * ((s0.C >> 6) + (a.nseg > 1 ? (s1.C >> 6) : 0) + (a.nseg > 2 ? (s2.C >> 6) : 0));
+
+  // issue-side scalar walk: segment si, channel chunk c0, tap itap
+  int si = 0, c0 = 0, kseg = 0, itap = 0, ichunk = 0, istep = 0;
+#define RS_HISSUE()                                                                                 \
+  do {                                                                                              \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                        \
+    if (itap == 0) {                                                                                \
+      const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                      \
+      const __amdgpu_buffer_rsrc_t rb = si == 0 ? rs0 : (si == 1 ? rs1 : rs2);                      \
+      uint4* hd = lds + 2 * AST + (ichunk & 1) * HST;                                               \
+      _Pragma("unroll") for (int i = 0; i < NH; ++i) {                                              \
+        const int v = hpix[i] >= 0 ? (hpix[i] * sst + c0 + hch[i]) * 2 : kFar;                      \
+        bdma16(rb, hd + wbase + 256 * i, v, 0);                                                     \
+      }                                                                                             \
+    }                                                                                               \
+    uint4* ad = lds + (istep & 1) * AST;                                                            \
+    const int asoff = (itap * Ktot + kseg + c0) * 2;                                                \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) bdma16(rw, ad + wbase + 256 * i, aoff[i], asoff); \
+    ++istep;                                                                                        \
+    if (++itap == taps) {                                                                           \
+      itap = 0;                                                                                     \
+      ++ichunk;                                                                                     \
+      c0 += 64;                                                                                     \
+      if (c0 == sC) { c0 = 0; kseg += sC; ++si; }                                                   \
+    }                                                                                               \
+  } while (0)
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lc = lane >> 4;
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0];
+  uint32_t abase[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    abase[kk] = lds0 + (uint32_t)((wm * WM * 16 + lr) * 128 + (((kk * 4 + lc) ^ ((lr >> 1) & 7)) * 16));
+  int rbn[WN];  // halo row of this lane's pixel (patch row wn*WN + nt, column lr) at tap (0, 0)
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) rbn[nt] = (wn * WN + nt) * hw + lr;
+
+  RS_HISSUE();
+  int ctap = 0, cty = 0, ctx = 0, cchunk = 0;
+  for (int step = 0; step < nsteps; ++step) {
+    wait_vmcnt<0>();
+    asm volatile("s_barrier" ::: "memory");  // step's weights + halo landed; buffers of step-1 free
+    const uint32_t so = (step & 1) * AST * 16;
+    const uint32_t hb = lds0 + (uint32_t)((2 * AST + (cchunk & 1) * HST) * 16);
+    const int toff = cty * hw + ctx;
+    uint32_t brow[WN], bsw[WN];
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt) {
+      const int row = rbn[nt] + toff;
+      brow[nt] = hb + (uint32_t)(row * 128);
+      bsw[nt] = (uint32_t)((row >> 1) & 7);
+    }
+    u32x4_t fa[2][WM], fb[2][WN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[kk][mt]) : "v"(abase[kk] + so), "i"(mt * 16 * 128)
+                     : "memory");
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(fb[kk][nt])
+                     : "v"(brow[nt] + ((((uint32_t)(kk * 4 + lc)) ^ bsw[nt]) << 4)) : "memory");
+    }
+    if (step + 1 < nsteps) RS_HISSUE();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt) asm volatile("" : "+v"(fa[kk][mt]));
+#pragma unroll
+      for (int nt = 0; nt < WN; ++nt) asm volatile("" : "+v"(fb[kk][nt]));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[kk][mt]),
+                                                                __builtin_bit_cast(bf16x8_t, fb[kk][nt]),
+                                                                acc[mt][nt], 0, 0, 0);
+    if (++ctx == KW) { ctx = 0; ++cty; }
+    if (++ctap == taps) { ctap = 0; cty = 0; ctx = 0; ++cchunk; }
+  }
+#undef RS_HISSUE
+
+  int pp[WN], pb[WN], py[WN], px[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int y = y0 + wn * WN + nt, x = x0 + lr;
+    if (y < H && x < W) {
+      pb[nt] = img;
+      py[nt] = y;
+      px[nt] = x;
+      pp[nt] = (img * H + y) * W + x;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = pp[nt] = 0;
+    }
+  }
+  epilogue_pix<WM, WN>(a, acc, m0, lane, pp, pb, py, px);
 }
 
 // ------------------------------------------------------------------ small-N variant
@@ -1045,6 +1252,14 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     return e ? atoi(e) : 1;
   }();
   a.xcd_remap = xcd_env;
+  if (L.tile >= 24) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)
+    const int TH = L.tile == 26 ? 4 : 8, BM = L.tile == 25 ? 64 : 128;
+    const dim3 grid(cdiv(L.Cout, BM) * L.B * cdiv(L.H, TH) * cdiv(L.W, 16));
+    if (L.tile == 24) hipLaunchKernelGGL((conv::conv_halo_kernel<128, 8, 192>), grid, dim3(256), 0, stream, a);
+    else if (L.tile == 25) hipLaunchKernelGGL((conv::conv_halo_kernel<64, 8, 192>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((conv::conv_halo_kernel<128, 4, 128>), grid, dim3(256), 0, stream, a);
+    return;
+  }
   if (L.tile == 5) {
     hipLaunchKernelGGL(conv::conv_smalln_kernel, dim3(cdiv(a.P, 16)), dim3(256), 0, stream, a);
   } else if (L.tile >= 2) {
@@ -1084,7 +1299,11 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
         case 16: RS_BUF(128, 64, 2); break;
         case 17: RS_BUF(64, 64, 2); break;
         case 18: RS_BUF(128, 64, 3); break;
-        default: RS_BUF(64, 64, 3); break;  // 19
+        case 19: RS_BUF(64, 64, 3); break;
+        case 20: RS_BUF(128, 128, 2); break;  // wave tile 64x64: 1.5x fewer L2 bytes per FLOP than 128x64
+        case 21: RS_BUF(64, 128, 2); break;
+        case 22: RS_BUF(128, 128, 3); break;
+        default: RS_BUF(64, 64, 4); break;    // 23: deep ring for latency-bound small grids (inference)
 #undef RS_BUF
       }
 #undef RS_GLDS

@@ -1,0 +1,57 @@
+"""ops/enc_conv.py (stride-1 3x3 encoder convs on csrc/conv.hip + csrc/conv_wgrad.hip)
+vs an fp32 PyTorch conv2d of the same bf16 operands: forward, input and weight gradients."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from raft_stir_amd.ops import enc_conv
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (128, 128), (64, 96), (96, 128)])
+@pytest.mark.parametrize("shape", [(2, 23, 31), (3, 46, 62)])
+def test_conv3x3_fwd_bwd(cuda, cin, cout, shape):
+    torch.manual_seed(0)
+    N, H, W = shape
+    conv = nn.Conv2d(cin, cout, 3, padding=1).to(cuda)
+    x = (torch.randn(N, cin, H, W, device=cuda) * 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert enc_conv.eligible(conv, x)
+    x.requires_grad_(True)
+    y = enc_conv.conv3x3(conv, x)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, padding=1)
+    yr.backward(g.float())
+
+    def rel(a, b):
+        return ((a.float() - b).abs().max() / b.abs().max()).item()
+
+    assert y.shape == yr.shape and y.dtype == torch.bfloat16
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    # weight gradient: fp32 accumulation over bf16 operands
+    assert rel(conv.weight.grad, wr.grad) < 1e-2
+
+
+def test_packed_weight_cache_tracks_updates(cuda):
+    torch.manual_seed(1)
+    conv = nn.Conv2d(64, 64, 3, padding=1).to(cuda)
+    x = torch.randn(1, 64, 9, 17, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y0 = enc_conv.conv3x3(conv, x).float()
+        conv.weight.mul_(2.0)  # in-place update (optimizer step): the packed copy must follow
+        y1 = enc_conv.conv3x3(conv, x).float()
+    torch.testing.assert_close(y1, 2 * y0, atol=2e-2, rtol=2e-2)
+
+
+def test_ineligible_shapes(cuda):
+    x = torch.randn(1, 64, 8, 8, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert not enc_conv.eligible(nn.Conv2d(64, 64, 3, padding=1, stride=2).to(cuda), x)
+    assert not enc_conv.eligible(nn.Conv2d(64, 64, 1).to(cuda), x)
+    assert not enc_conv.eligible(nn.Conv2d(64, 64, 3, padding=1).to(cuda), x.float())
+    assert not enc_conv.eligible(nn.Conv2d(64, 24, 3, padding=1).to(cuda), x)
