@@ -26,6 +26,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.fp32conv import conv_module
 from ..ops.norm import conv_norm_act
 
 
@@ -139,7 +140,7 @@ class _Encoder(nn.Module):
             x = torch.cat(list(x), dim=0)
         x = conv_norm_act(self.conv1, self.norm1, x)
         x = self.layer3(self.layer2(self.layer1(x)))
-        x = self.conv2(x)
+        x = conv_module(self.conv2, x)
         if self.training and self.dropout is not None:
             x = self.dropout(x)
         if pair:

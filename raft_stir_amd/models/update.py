@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import gru as gru_ops
+from ..ops.fp32conv import conv_module as _cv
 
 
 class FlowHead(nn.Module):
@@ -34,7 +35,7 @@ class FlowHead(nn.Module):
         self.relu = nn.ReLU(inplace=True)
 
     def forward(self, x):
-        return self.conv2(self.relu(self.conv1(x)))
+        return _cv(self.conv2, self.relu(_cv(self.conv1, x)))
 
 
 def _gru_step_reference(convz, convr, convq, h, x):
@@ -88,9 +89,9 @@ class SmallMotionEncoder(nn.Module):
         self.conv = nn.Conv2d(128, 80, 3, padding=1)
 
     def forward(self, flow, corr):
-        c = F.relu(self.convc1(corr))
-        f = F.relu(self.convf2(F.relu(self.convf1(flow))))
-        out = F.relu(self.conv(torch.cat([c, f], dim=1)))
+        c = F.relu(_cv(self.convc1, corr))
+        f = F.relu(_cv(self.convf2, F.relu(_cv(self.convf1, flow))))
+        out = F.relu(_cv(self.conv, torch.cat([c, f], dim=1)))
         return torch.cat([out, flow.to(out.dtype)], dim=1)
 
 
@@ -104,9 +105,9 @@ class BasicMotionEncoder(nn.Module):
         self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
 
     def forward(self, flow, corr):
-        c = F.relu(self.convc2(F.relu(self.convc1(corr))))
-        f = F.relu(self.convf2(F.relu(self.convf1(flow))))
-        out = F.relu(self.conv(torch.cat([c, f], dim=1)))
+        c = F.relu(_cv(self.convc2, F.relu(_cv(self.convc1, corr))))
+        f = F.relu(_cv(self.convf2, F.relu(_cv(self.convf1, flow))))
+        out = F.relu(_cv(self.conv, torch.cat([c, f], dim=1)))
         return torch.cat([out, flow.to(out.dtype)], dim=1)
 
 
@@ -146,5 +147,5 @@ class BasicUpdateBlock(nn.Module):
         net = self.gru(net, torch.cat([inp, motion], dim=1))
         delta = self.flow_head(net)
         # 0.25 scale balances the mask gradients (reference core/update.py:134)
-        mask = 0.25 * self.mask(net) if upsample else None
+        mask = 0.25 * _cv(self.mask[2], F.relu(_cv(self.mask[0], net))) if upsample else None
         return net, mask, delta

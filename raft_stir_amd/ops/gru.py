@@ -20,19 +20,16 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from . import fp32conv
 from .corr import to_nhwc, from_nhwc
 
 _CL = torch.channels_last
-
-
 def fused_available(h: torch.Tensor) -> bool:
     return _ext.use_hip(h)
 
 
 def _conv_bwd(dy, x, w, padding):
-    return torch.ops.aten.convolution_backward(
-        dy, x, w, [w.shape[0]], [1, 1], list(padding), [1, 1], False, [0, 0], 1,
-        [True, True, True])
+    return fp32conv.conv_backward(dy, x, w, (1, 1), padding)
 
 
 class _GRUPass(torch.autograd.Function):
@@ -40,10 +37,10 @@ class _GRUPass(torch.autograd.Function):
     def forward(ctx, h, x, wzr, bzr, wq, bq, padding):
         # h: (B,hd,H,W), x: (B,cin,H,W) channels_last, same dtype
         hx = torch.cat([h, x], dim=1).contiguous(memory_format=_CL)
-        zr = F.conv2d(hx, wzr, bzr, padding=padding)
+        zr = fp32conv.conv2d(hx, wzr, bzr, 1, padding)
         hn_ = to_nhwc(h)
         z, r, rhx = torch.ops.raft_stir.gru_gate_zr(to_nhwc(zr), hn_, to_nhwc(x))
-        q = F.conv2d(from_nhwc(rhx), wq, bq, padding=padding)
+        q = fp32conv.conv2d(from_nhwc(rhx), wq, bq, 1, padding)
         hn, qt = torch.ops.raft_stir.gru_gate_q(to_nhwc(q), z, hn_)
         ctx.padding = padding
         ctx.save_for_backward(hx, rhx, wzr, wq, hn_, z, r, qt)

@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from . import _ext
 from . import enc_conv
+from . import fp32conv
 
 _CL = torch.channels_last
 _FOLD_BIAS = os.environ.get("RS_FOLD_BIAS", "1") != "0"
@@ -146,5 +147,5 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
         return norm_act(norm, conv(x), relu, residual)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
         return norm_act(norm, enc_conv.conv3x3(conv, x), relu, residual, bias=conv.bias)
-    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    y = fp32conv.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return norm_act(norm, y, relu, residual, bias=conv.bias)

@@ -106,6 +106,8 @@ def test_cli_scripts(fake_root, tmp_path):
 
 
 def test_core_shim_imports():
+    # another test may have imported the reference's own core/raft.py as 'raft'
+    saved = {k: sys.modules.pop(k) for k in ("raft", "utils.utils", "utils") if k in sys.modules}
     sys.path.insert(0, os.path.join(ROOT, "core"))
     try:
         import importlib
@@ -117,3 +119,4 @@ def test_core_shim_imports():
         sys.path.remove(os.path.join(ROOT, "core"))
         for k in ("raft", "utils.utils", "utils"):
             sys.modules.pop(k, None)
+        sys.modules.update(saved)
