@@ -88,9 +88,35 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cas
 // kind is a template parameter of the fragment loop (dispatched once, outside
 // it): with a runtime switch inside, the 16-fragment loops of the 4x4 wave
 // tiles were too large to unroll and the accumulators went to scratch.
+// 4 consecutive channels per lane: one 8-byte (bf16) / 16-byte (fp32) access
+// when every epilogue base, offset and stride is a multiple of 4 elements
+// (checked once per launch, see epi_loop); the element-wise forms otherwise.
+__device__ __forceinline__ void ld4(const bf16_t* p, float (&f)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  f[0] = bf2f((bf16_t)(u.x & 0xffffu));
+  f[1] = bf2f((bf16_t)(u.x >> 16));
+  f[2] = bf2f((bf16_t)(u.y & 0xffffu));
+  f[3] = bf2f((bf16_t)(u.y >> 16));
+}
+__device__ __forceinline__ void st4(bf16_t* p, const float (&f)[4]) {
+  uint2 pk;
+  pk.x = uint32_t(f2bf(f[0])) | (uint32_t(f2bf(f[1])) << 16);
+  pk.y = uint32_t(f2bf(f[2])) | (uint32_t(f2bf(f[3])) << 16);
+  *reinterpret_cast<uint2*>(p) = pk;
+}
+__device__ __forceinline__ void acc4(float* p, const float (&f)[4]) {
+  float4 o = *reinterpret_cast<float4*>(p);
+  o.x += f[0];
+  o.y += f[1];
+  o.z += f[2];
+  o.w += f[3];
+  *reinterpret_cast<float4*>(p) = o;
+}
+
 template <int E>
 __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, int p, int pb, int py, int px,
-                                         int HW) {
+                                         int HW, bool vec) {
+  const bool full = cb + 3 < a.Cout;
   if constexpr (E == EPI_FLOW) {  // coords (+)= delta; out2 (if set) is the source coords
     float* crd = static_cast<float*>(a.out);
     const float* src = a.out2 ? static_cast<const float*>(a.out2) : crd;
@@ -105,18 +131,41 @@ __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, i
   } else if constexpr (E == EPI_GRU_ZR) {
     if (cb < a.hd) {
       bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+      float zv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) z[j] = f2bf(sigmoidf_(v[j]));
+      for (int j = 0; j < 4; ++j) zv[j] = sigmoidf_(v[j]);
+      if (vec) {
+        st4(z, zv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[j] = f2bf(zv[j]);
+      }
     } else {
       const int c = cb - a.hd;
       const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
       bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
       bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
+      float hv[4], rv[4], rhv[4];
+      if (vec) {
+        ld4(h, hv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hv[j] = bf2f(h[j]);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float r = sigmoidf_(v[j]);
-        rh[j] = f2bf(r * bf2f(h[j]));
-        if (rs_) rs_[j] = f2bf(r);
+        rv[j] = sigmoidf_(v[j]);
+        rhv[j] = rv[j] * hv[j];
+      }
+      if (vec) {
+        st4(rh, rhv);
+        if (rs_) st4(rs_, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          rh[j] = f2bf(rhv[j]);
+          if (rs_) rs_[j] = f2bf(rv[j]);
+        }
       }
     }
   } else if constexpr (E == EPI_GRU_Q) {
@@ -124,45 +173,95 @@ __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, i
     const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
     bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
     bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
-    float hv[4], zv[4];
+    float hv[4], zv[4], qv[4], nv[4];
+    if (vec) {
+      ld4(h, hv);
+      ld4(z, zv);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      hv[j] = bf2f(h[j]);
-      zv[j] = bf2f(z[j]);
+      for (int j = 0; j < 4; ++j) {
+        hv[j] = bf2f(h[j]);
+        zv[j] = bf2f(z[j]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float q = tanhf_(v[j]);
-      hn[j] = f2bf((1.f - zv[j]) * hv[j] + zv[j] * q);
-      if (qs) qs[j] = f2bf(q);
+      qv[j] = tanhf_(v[j]);
+      nv[j] = (1.f - zv[j]) * hv[j] + zv[j] * qv[j];
+    }
+    if (vec) {
+      st4(hn, nv);
+      if (qs) st4(qs, qv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hn[j] = f2bf(nv[j]);
+        if (qs) qs[j] = f2bf(qv[j]);
+      }
     }
   } else if constexpr (E == EPI_RELU_BWD) {
     const bf16_t* act = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
     bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (vec && full) {
+      float av[4], ov[4];
+      ld4(act, av);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
+      for (int j = 0; j < 4; ++j) ov[j] = av[j] > 0.f ? v[j] : 0.f;
+      st4(o, ov);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
+    }
   } else if constexpr (E == EPI_ACC_F32) {
     float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (vec && full) {
+      acc4(o, v);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (cb + j < a.Cout) o[j] += v[j];
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] += v[j];
+    }
   } else if constexpr (E == EPI_GRU_QBWD) {
     float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
     if (cb < a.hd) {
       const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
       const bf16_t* r = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
       bf16_t* drp = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb;
+      float hv[4], rv[4], dv[4], gv[4];
+      if (vec) {
+        ld4(h, hv);
+        ld4(r, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hv[j] = bf2f(h[j]);
+          rv[j] = bf2f(r[j]);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float rv = bf2f(r[j]), hv = bf2f(h[j]);
-        drp[j] = f2bf(v[j] * hv * rv * (1.f - rv));
-        o[j] += v[j] * rv;
+        dv[j] = v[j] * hv[j] * rv[j] * (1.f - rv[j]);
+        gv[j] = v[j] * rv[j];
+      }
+      if (vec) {
+        st4(drp, dv);
+        acc4(o, gv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          drp[j] = f2bf(dv[j]);
+          o[j] += gv[j];
+        }
       }
     } else {
+      if (vec && full) {
+        acc4(o, v);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (cb + j < a.Cout) o[j] += v[j];
+        for (int j = 0; j < 4; ++j)
+          if (cb + j < a.Cout) o[j] += v[j];
+      }
     }
   } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE -> bf16
 #pragma unroll
@@ -171,11 +270,8 @@ __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, i
       if constexpr (E == EPI_SCALE) v[j] *= a.scale;
     }
     bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-    if (cb + 3 < a.Cout && ((a.ooff + cb) & 3) == 0 && (a.ostr & 3) == 0) {
-      uint2 pk;
-      pk.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-      pk.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-      *reinterpret_cast<uint2*>(o) = pk;
+    if (vec && full) {
+      st4(o, v);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -190,6 +286,11 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
                                          const int (&px)[WN]) {
   const int HW = a.H * a.W;
   const int cq = (lane >> 4) * 4;
+  // wave-uniform: every epilogue tensor 4-element aligned (vector accesses)
+  const bool vec =
+      ((a.ooff | a.ostr | a.o2off | a.o2str | a.o3off | a.o3str | a.a1off | a.a1str | a.a2off | a.a2str) & 3) == 0 &&
+      (((uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.out3 | (uintptr_t)a.aux1 | (uintptr_t)a.aux2) & 15) == 0;
+  const bool bvec = a.bias && (((uintptr_t)a.bias) & 15) == 0;
 #pragma unroll
   for (int nt = 0; nt < WN; ++nt) {
     if (pb[nt] < 0) continue;
@@ -198,9 +299,17 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
       const int cb = m0 + mt * 16 + cq;
       if (cb >= a.Cout) continue;
       float v[4];
+      if (bvec && cb + 3 < a.Cout) {
+        const float4 bv = *reinterpret_cast<const float4*>(a.bias + cb);
+        v[0] = acc[mt][nt][0] + bv.x;
+        v[1] = acc[mt][nt][1] + bv.y;
+        v[2] = acc[mt][nt][2] + bv.z;
+        v[3] = acc[mt][nt][3] + bv.w;
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
-      epi_frag<E>(a, v, cb, pp[nt], pb[nt], py[nt], px[nt], HW);
+        for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
+      }
+      epi_frag<E>(a, v, cb, pp[nt], pb[nt], py[nt], px[nt], HW, vec);
     }
   }
 }

@@ -381,6 +381,27 @@ int grid_elem(size_t nvec) {
   return (int)(g < 8192 ? g : 8192);
 }
 
+// BatchNorm running-statistics update from the batch statistics (reference
+// semantics of nn.BatchNorm2d in train mode, momentum form):
+//   running_mean = (1-m) running_mean + m (mean + bias)
+//   running_var  = (1-m) running_var  + m var * n/(n-1),  var = rstd^-2 - eps
+// One launch instead of ~10 elementwise ATen kernels per BN layer.
+__global__ __launch_bounds__(256) void bn_running_kernel(const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         const float* __restrict__ bias, int C, float eps,
+                                                         float mom, float unb, float* __restrict__ rmean,
+                                                         float* __restrict__ rvar, long long* nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const float r = rstd[c];
+    const float var = fmaxf(1.f / (r * r) - eps, 0.f);
+    const float bm = mean[c] + (bias ? bias[c] : 0.f);
+    rmean[c] = (1.f - mom) * rmean[c] + mom * bm;
+    rvar[c] = (1.f - mom) * rvar[c] + mom * var * unb;
+  }
+  if (c == 0 && nbt) nbt[0] += 1;
+}
+
 }  // namespace norm
 
 // ------------------------------------------------------------------ launchers
@@ -441,6 +462,12 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
     hipLaunchKernelGGL(norm::apply_bwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
   else
     hipLaunchKernelGGL(norm::apply_bwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
+}
+
+void bn_running_launch(const float* mean, const float* rstd, const float* bias, int C, float eps, float mom,
+                       float unb, float* rmean, float* rvar, long long* nbt, hipStream_t s) {
+  hipLaunchKernelGGL(norm::bn_running_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, mean, rstd, bias, C, eps, mom,
+                     unb, rmean, rvar, nbt);
 }
 
 }  // namespace rs

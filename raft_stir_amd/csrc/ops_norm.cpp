@@ -17,6 +17,8 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
                      void* dres, hipStream_t s);
+void bn_running_launch(const float* mean, const float* rstd, const float* bias, int C, float eps, float mom,
+                       float unb, float* rmean, float* rvar, long long* nbt, hipStream_t s);
 }  // namespace rs
 
 namespace {
@@ -115,7 +117,26 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
 
 }  // namespace
 
+// In-place BatchNorm running-statistics update (see bn_running_kernel).
+void bn_running_update(const Tensor& mean, const Tensor& rstd, const c10::optional<Tensor>& bias,
+                       Tensor running_mean, Tensor running_var, c10::optional<Tensor> nbt, double eps,
+                       double momentum, int64_t n) {
+  const int64_t C = running_mean.numel();
+  check_param(mean, C, "mean");
+  check_param(rstd, C, "rstd");
+  check_param(bias, C, "bias");
+  check_param(running_mean, C, "running_mean");
+  check_param(running_var, C, "running_var");
+  if (nbt) TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "bn: num_batches_tracked");
+  const c10::DeviceGuard g(mean.device());
+  const float unb = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
+  rs::bn_running_launch(mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(bias), (int)C, (float)eps,
+                        (float)momentum, unb, running_mean.data_ptr<float>(), running_var.data_ptr<float>(),
+                        nbt ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr, stream());
+}
+
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("bn_running_update(Tensor mean, Tensor rstd, Tensor? bias, Tensor(a!) running_mean, Tensor(b!) running_var, Tensor(c!)? nbt, float eps, float momentum, int n) -> ()");
   m.def("norm_stats(Tensor x, bool per_sample, float eps) -> Tensor[]");
   m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu) -> Tensor");
   m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, bool batch_stats) -> Tensor[]");
@@ -123,6 +144,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("norm_stats", &norm_stats);
+  m.impl("bn_running_update", &bn_running_update);
   m.impl("norm_act", &norm_act);
   m.impl("norm_act_backward", &norm_act_backward);
 }

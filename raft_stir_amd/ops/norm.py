@@ -113,13 +113,20 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
         with torch.no_grad():
             mean, rstd = torch.ops.raft_stir.norm_stats(xn, False, norm.eps)
             n = x.numel() // x.shape[1]
-            var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
-            unbiased = var * (n / max(n - 1, 1))
-            m = norm.momentum
-            bmean = mean.reshape(-1) if bias is None else mean.reshape(-1) + bias.detach().float()
-            norm.running_mean.mul_(1 - m).add_(bmean, alpha=m)
-            norm.running_var.mul_(1 - m).add_(unbiased, alpha=m)
-            norm.num_batches_tracked.add_(1)
+            rm, rv = norm.running_mean, norm.running_var
+            if rm.dtype == torch.float32 and rv.dtype == torch.float32 and rm.is_contiguous() and rv.is_contiguous():
+                # one fused launch (csrc/norm.hip bn_running_kernel)
+                torch.ops.raft_stir.bn_running_update(
+                    mean.reshape(-1), rstd.reshape(-1), None if bias is None else bias.detach().float().contiguous(),
+                    rm, rv, norm.num_batches_tracked, norm.eps, norm.momentum, n)
+            else:
+                var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
+                unbiased = var * (n / max(n - 1, 1))
+                m = norm.momentum
+                bmean = mean.reshape(-1) if bias is None else mean.reshape(-1) + bias.detach().float()
+                rm.mul_(1 - m).add_(bmean, alpha=m)
+                rv.mul_(1 - m).add_(unbiased, alpha=m)
+                norm.num_batches_tracked.add_(1)
     else:
         mean = norm.running_mean.float().reshape(1, -1)
         if bias is not None:  # gamma * (x + b - mean) * rstd + beta

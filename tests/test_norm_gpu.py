@@ -63,6 +63,7 @@ def test_norm_act_fwd_bwd(cuda, kind, C, dtype, relu, use_res):
         torch.testing.assert_close(norm.bias.grad, ref_norm.bias.grad, atol=gtol * 10, rtol=gtol)
         torch.testing.assert_close(norm.running_mean, ref_norm.running_mean, atol=1e-4, rtol=1e-3)
         torch.testing.assert_close(norm.running_var, ref_norm.running_var, atol=1e-3, rtol=1e-3)
+        assert int(norm.num_batches_tracked) == int(ref_norm.num_batches_tracked)
 
 
 def test_norm_act_large_spatial(cuda):
