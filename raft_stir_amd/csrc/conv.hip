@@ -1223,51 +1223,62 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(Args a) {
 // ------------------------------------------------------------------ flow encoder
 // convf1 of the motion encoder (reference core/update.py:67,84): a 7x7 conv
 // of the 2-channel flow (= coords1 - coords0, computed here from coords1)
-// with ReLU, written as bf16 NHWC.  K = 98, so it is a VALU kernel: one
-// thread per (pixel, 8 output channels), the 7x7x2 flow window in registers.
+// with ReLU, written as bf16 NHWC.  K = 98, so it is a VALU kernel.
 // It also writes the flow itself (bf16) into its slot of the GRU input
 // buffer (reference: cat([out, flow]) in the motion encoder).
+// One wave = 64 pixels (one per lane) x 16 output channels; the channel group
+// is wave-uniform (readfirstlane), so every weight / bias read is a scalar
+// load shared by the wave and each FMA takes its weight from an SGPR.  Taps
+// outside the image contribute through a 0/1 factor (no divergent branches
+// around the scalar loads).  The previous mapping (lane = channel group)
+// re-read the 7x7x2 weights per lane (scripts/bench_small_ops.py).
 __global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__ coords, int B, int H,
                                                        int W, const float* __restrict__ w,  // [49][2][Cout]
                                                        const float* __restrict__ bias, int Cout,
                                                        bf16_t* __restrict__ out, int ostr, int ooff,
                                                        bf16_t* __restrict__ fout, int fstr, int foff) {
-  const int groups = Cout / 8;
-  const int HW = H * W;
-  const long total = (long)B * HW * groups;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int g = (int)(i % groups);
-    const long p = i / groups;
-    const int b = (int)(p / HW), q = (int)(p % HW), y = q / W, x = q % W;
-    float acc[8];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = (blockIdx.y * 4 + wave) * 16;
+  if (c0 >= Cout) return;
+  const int HW = H * W, P = B * HW;
+  const int p = blockIdx.x * 64 + lane;
+  const int pc = p < P ? p : P - 1;
+  const int b = pc / HW, q = pc - b * HW, y = q / W, x = q - y * W;
+  const float* cx = coords + (size_t)b * 2 * HW;
+  const float* cy = cx + HW;
+  float acc[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = bias[g * 8 + j];
-    const float* cx = coords + (size_t)b * 2 * HW;
-    const float* cy = cx + HW;
-    for (int ky = 0; ky < 7; ++ky) {
-      const int yy = y + ky - 3;
-      if (yy < 0 || yy >= H) continue;
-      for (int kx = 0; kx < 7; ++kx) {
-        const int xx = x + kx - 3;
-        if (xx < 0 || xx >= W) continue;
-        const float fu = cx[yy * W + xx] - (float)xx;
-        const float fv = cy[yy * W + xx] - (float)yy;
-        const float* wt = w + ((ky * 7 + kx) * 2) * Cout + g * 8;
+  for (int j = 0; j < 16; ++j) acc[j] = bias[c0 + j];
+#pragma unroll 1
+  for (int ky = 0; ky < 7; ++ky) {
+    const int yy = y + ky - 3;
+    const bool iny = yy >= 0 && yy < H;
+    const int yc = iny ? yy : y;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += fu * wt[j] + fv * wt[Cout + j];
-      }
+    for (int kx = 0; kx < 7; ++kx) {
+      const int xx = x + kx - 3;
+      const bool in = iny && xx >= 0 && xx < W;
+      const int xc = in ? xx : x;
+      const float m = in ? 1.f : 0.f;
+      const float fu = m * (cx[yc * W + xc] - (float)xc);
+      const float fv = m * (cy[yc * W + xc] - (float)yc);
+      const float* wt = w + ((ky * 7 + kx) * 2) * Cout + c0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = fmaf(fu, wt[j], fmaf(fv, wt[Cout + j], acc[j]));
     }
-    uint4 pk;
-    uint32_t u[4];
+  }
+  if (p >= P) return;
+  uint32_t u[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      u[j] = uint32_t(f2bf(fmaxf(acc[2 * j], 0.f))) | (uint32_t(f2bf(fmaxf(acc[2 * j + 1], 0.f))) << 16);
-    pk = make_uint4(u[0], u[1], u[2], u[3]);
-    *reinterpret_cast<uint4*>(out + (size_t)p * ostr + ooff + g * 8) = pk;
-    if (g == 0 && fout) {
-      fout[(size_t)p * fstr + foff] = f2bf(cx[q] - (float)x);
-      fout[(size_t)p * fstr + foff + 1] = f2bf(cy[q] - (float)y);
-    }
+  for (int j = 0; j < 8; ++j)
+    u[j] = uint32_t(f2bf(fmaxf(acc[2 * j], 0.f))) | (uint32_t(f2bf(fmaxf(acc[2 * j + 1], 0.f))) << 16);
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)p * ostr + ooff + c0);
+  o[0] = make_uint4(u[0], u[1], u[2], u[3]);
+  o[1] = make_uint4(u[4], u[5], u[6], u[7]);
+  if (c0 == 0 && fout) {
+    fout[(size_t)p * fstr + foff] = f2bf(cx[q] - (float)x);
+    fout[(size_t)p * fstr + foff + 1] = f2bf(cy[q] - (float)y);
   }
 }
 
@@ -1453,9 +1464,8 @@ void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* a
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
                      int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
                      hipStream_t stream) {
-  const long total = (long)B * H * W * (Cout / 8);
-  const int grid = (int)((total + 255) / 256 < 16384 ? (total + 255) / 256 : 16384);
-  hipLaunchKernelGGL(conv::flow_enc_kernel, dim3(grid), dim3(256), 0, stream, coords, B, H, W, w, bias,
+  const dim3 grid((unsigned)cdiv(B * H * W, 64), (unsigned)cdiv(Cout, 64));
+  hipLaunchKernelGGL(conv::flow_enc_kernel, grid, dim3(256), 0, stream, coords, B, H, W, w, bias,
                      Cout, static_cast<bf16_t*>(out), ostr, ooff, static_cast<bf16_t*>(fout), fstr, foff);
 }
 

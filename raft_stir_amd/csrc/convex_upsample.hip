@@ -7,38 +7,72 @@
 //   up[n, c, 8y+a, 8x+b] = sum_k softmax_k(mask[n, y, x, 64k + 8a + b]) * 8*flow[n, c, y+ky-1, x+kx-1]
 //   (k = 3*ky + kx, zero padding outside the coarse grid)
 //
-// One wave64 per coarse pixel: lane = 8a + b owns one of its 64 sub-pixels.
-// The mask is channels-last (the 1x1 mask-head conv writes NHWC), so the 9
-// loads of a lane are 9 coalesced 64-lane rows; the 3x3 flow neighbourhood is
-// wave-uniform.  Backward recomputes the softmax (nothing saved but inputs),
-// writes dmask in the same coalesced layout, and reduces the 9x2 flow-
-// neighbour partial sums across the wave; a second tiny kernel gathers them
-// into dflow (deterministic, no atomics).
+// Work mapping: one thread per (coarse pixel, fine row a): it owns the 8
+// sub-pixels b = 0..7 of that row, so every mask read is one 16-byte load
+// (8 bf16 of tap k) and every output write 32 contiguous bytes per channel.
+// A wave = 8 coarse pixels x 8 rows (lane = 8a + xo), a 256-thread block 32
+// consecutive coarse pixels of one coarse row (grid = (W/32, H, N): no index
+// divisions); the 8 lanes of one a write 256 contiguous bytes of a fine row.
+// The mask is channels-last (the 1x1 mask-head conv writes NHWC).  Backward
+// recomputes the softmax (nothing saved but inputs), writes dmask in the same
+// layout, and reduces the 9x2 flow-neighbour partial sums of each coarse
+// pixel over its 64 sub-pixels (8 in-thread, 8 rows by xor shuffles); a
+// second tiny kernel gathers them into dflow (deterministic, no atomics).
 
 #include "common.h"
 
 namespace rs {
 namespace cvx {
 
-constexpr int WAVES = 4;
+constexpr int XW = 8;   // coarse pixels per wave
+constexpr int WPB = 4;  // waves per block
+constexpr int XB = XW * WPB;
 
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&f)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bf2f((bf16_t)(w[i] & 0xffffu));
+    f[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16));
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float (&f)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+// p[k][b] = softmax over k of m[64k + b] (m points at row a: mask + 8a)
 template <typename MT>
-__device__ __forceinline__ void softmax9(const MT* __restrict__ m, int lane, float (&p)[9]) {
-  float mx = -INFINITY;
+__device__ __forceinline__ void softmax9x8(const MT* __restrict__ m, float (&p)[9][8]) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    p[k] = io<MT>::ld(m + 64 * k + lane);
-    mx = fmaxf(mx, p[k]);
+  for (int k = 0; k < 9; ++k) ld8(m + 64 * k, p[k]);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    float mx = p[0][b];
+#pragma unroll
+    for (int k = 1; k < 9; ++k) mx = fmaxf(mx, p[k][b]);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      p[k][b] = __expf(p[k][b] - mx);
+      s += p[k][b];
+    }
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) p[k][b] *= inv;
   }
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    p[k] = __expf(p[k] - mx);
-    s += p[k];
-  }
-  const float inv = 1.f / s;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) p[k] *= inv;
 }
 
 __device__ __forceinline__ void neighbours(const float* __restrict__ flow, int n, int y, int x,
@@ -56,62 +90,88 @@ __device__ __forceinline__ void neighbours(const float* __restrict__ flow, int n
 }
 
 template <typename MT>
-__global__ __launch_bounds__(WAVES * 64) void convex_up_fwd_kernel(
+__global__ __launch_bounds__(WPB * 64) void convex_up_fwd_kernel(
     const float* __restrict__ flow, const MT* __restrict__ mask, int N, int H, int W,
     float* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const long cp = (long)blockIdx.x * WAVES + (threadIdx.x >> 6);  // coarse pixel id
-  if (cp >= (long)N * H * W) return;
-  const int x = (int)(cp % W), y = (int)((cp / W) % H), n = (int)(cp / ((long)H * W));
-  float p[9], u[9], v[9];
-  softmax9(mask + cp * 576, lane, p);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int a = lane >> 3, x = blockIdx.x * XB + wave * XW + (lane & 7), y = blockIdx.y, n = blockIdx.z;
+  if (x >= W) return;
+  const size_t cp = ((size_t)n * H + y) * W + x;
+  float p[9][8], u[9], v[9];
+  softmax9x8(mask + cp * 576 + 8 * a, p);
   neighbours(flow, n, y, x, H, W, u, v);
-  float su = 0.f, sv = 0.f;
+  float su[8], sv[8];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    su += p[k] * u[k];
-    sv += p[k] * v[k];
+  for (int b = 0; b < 8; ++b) {
+    su[b] = 0.f;
+    sv[b] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      su[b] += p[k][b] * u[k];
+      sv[b] += p[k][b] * v[k];
+    }
   }
-  const int a = lane >> 3, b = lane & 7;
   const size_t W8 = (size_t)W * 8, plane = (size_t)H * 8 * W8;
-  const size_t o = (size_t)(8 * y + a) * W8 + 8 * x + b;
-  out[(size_t)n * 2 * plane + o] = su;
-  out[(size_t)n * 2 * plane + plane + o] = sv;
+  float* o = out + (size_t)n * 2 * plane + (size_t)(8 * y + a) * W8 + 8 * (size_t)x;
+  st8(o, su);
+  st8(o + plane, sv);
 }
 
 template <typename MT, typename GT>
-__global__ __launch_bounds__(WAVES * 64) void convex_up_bwd_kernel(
+__global__ __launch_bounds__(WPB * 64) void convex_up_bwd_kernel(
     const float* __restrict__ flow, const MT* __restrict__ mask, const GT* __restrict__ dup,
     int N, int H, int W, MT* __restrict__ dmask, float* __restrict__ partial) {
-  const int lane = threadIdx.x & 63;
-  const long cp = (long)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (cp >= (long)N * H * W) return;
-  const int x = (int)(cp % W), y = (int)((cp / W) % H), n = (int)(cp / ((long)H * W));
-  float p[9], u[9], v[9];
-  softmax9(mask + cp * 576, lane, p);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int a = lane >> 3, x0 = blockIdx.x * XB + wave * XW + (lane & 7), y = blockIdx.y, n = blockIdx.z;
+  const bool in = x0 < W;
+  const int x = in ? x0 : W - 1;  // out-of-range lanes still join the shuffles (zero gradient)
+  const size_t cp = ((size_t)n * H + y) * W + x;
+  float p[9][8], u[9], v[9], gu[8], gv[8];
+  softmax9x8(mask + cp * 576 + 8 * a, p);
   neighbours(flow, n, y, x, H, W, u, v);
-  const int a = lane >> 3, b = lane & 7;
   const size_t W8 = (size_t)W * 8, plane = (size_t)H * 8 * W8;
-  const size_t o = (size_t)(8 * y + a) * W8 + 8 * x + b;
-  const float gu = io<GT>::ld(dup + (size_t)n * 2 * plane + o);
-  const float gv = io<GT>::ld(dup + (size_t)n * 2 * plane + plane + o);
-  // softmax backward: dm_k = p_k (dp_k - sum_j p_j dp_j), dp_k = gu*u_k + gv*v_k
-  float dp[9], dot = 0.f;
+  const GT* g = dup + (size_t)n * 2 * plane + (size_t)(8 * y + a) * W8 + 8 * (size_t)x;
+  ld8(g, gu);
+  ld8(g + plane, gv);
+  if (!in) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    dp[k] = gu * u[k] + gv * v[k];
-    dot += p[k] * dp[k];
+    for (int b = 0; b < 8; ++b) gu[b] = gv[b] = 0.f;
   }
-  MT* dm = dmask + cp * 576;
+  // softmax backward: dm_k = p_k (dp_k - sum_j p_j dp_j), dp_k = gu*u_k + gv*v_k
+  float dm[9][8];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) io<MT>::st(dm + 64 * k + lane, p[k] * (dp[k] - dot));
-  // neighbour partials: d(8*flow_c[nbr_k]) = sum_lanes p_k * g_c  -> x8 for d flow
+  for (int b = 0; b < 8; ++b) {
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      dm[k][b] = gu[b] * u[k] + gv[b] * v[k];
+      dot += p[k][b] * dm[k][b];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dm[k][b] = p[k][b] * (dm[k][b] - dot);
+  }
+  if (in) {
+    MT* d = dmask + cp * 576 + 8 * a;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st8(d + 64 * k, dm[k]);
+  }
+  // neighbour partials: d(8*flow_c[nbr_k]) = sum over the 64 sub-pixels of p_k * g_c  (x8 for d flow):
+  // the 8 b in-thread, the 8 rows a (lanes 8 apart) by xor shuffles
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    float su = wave_sum(p[k] * gu);
-    float sv = wave_sum(p[k] * gv);
-    if (lane == 0) {
-      partial[cp * 18 + 2 * k + 0] = 8.f * su;
+    float su = 0.f, sv = 0.f;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      su += p[k][b] * gu[b];
+      sv += p[k][b] * gv[b];
+    }
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1) {
+      su += __shfl_xor(su, m, 64);
+      sv += __shfl_xor(sv, m, 64);
+    }
+    if (a == 0 && in) {
+      partial[cp * 18 + 2 * k] = 8.f * su;
       partial[cp * 18 + 2 * k + 1] = 8.f * sv;
     }
   }
@@ -147,7 +207,7 @@ void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, i
                           float* out, hipStream_t stream) {
   const long cps = (long)N * H * W;
   if (cps == 0) return;
-  dim3 grid((unsigned)((cps + cvx::WAVES - 1) / cvx::WAVES)), block(cvx::WAVES * 64);
+  dim3 grid((unsigned)cdiv(W, cvx::XB), (unsigned)H, (unsigned)N), block(cvx::WPB * 64);
   if (mask_bf16)
     hipLaunchKernelGGL(cvx::convex_up_fwd_kernel<bf16_t>, grid, block, 0, stream, flow,
                        static_cast<const bf16_t*>(mask), N, H, W, out);
@@ -162,7 +222,7 @@ void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, c
                           float* partial, hipStream_t stream) {
   const long cps = (long)N * H * W;
   if (cps == 0) return;
-  dim3 grid((unsigned)((cps + cvx::WAVES - 1) / cvx::WAVES)), block(cvx::WAVES * 64);
+  dim3 grid((unsigned)cdiv(W, cvx::XB), (unsigned)H, (unsigned)N), block(cvx::WPB * 64);
 #define RS_L(MT, GT)                                                                         \
   hipLaunchKernelGGL((cvx::convex_up_bwd_kernel<MT, GT>), grid, block, 0, stream, flow,     \
                      static_cast<const MT*>(mask), static_cast<const GT*>(dup), N, H, W,     \

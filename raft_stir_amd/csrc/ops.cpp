@@ -296,6 +296,9 @@ Tensor convex_upsample(const Tensor& flow, const Tensor& mask) {
   TORCH_CHECK(mask.dim() == 4 && mask.size(0) == N && mask.size(1) == H && mask.size(2) == W &&
                   mask.size(3) == 576,
               "mask must be channels-last (N,H,W,576)");
+  // the kernel reads 8 mask channels / writes 8 output floats per vector access
+  TORCH_CHECK(flow.is_contiguous() && mask.is_contiguous() && (reinterpret_cast<uintptr_t>(mask.data_ptr()) & 15) == 0,
+              "convex_upsample: contiguous flow and 16-byte aligned contiguous mask required");
   const c10::DeviceGuard guard(flow.device());
   Tensor out = at::empty({N, 2, 8 * H, 8 * W}, flow.options());
   rs::convex_up_fwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), N, H, W,
@@ -314,6 +317,10 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
   TORCH_CHECK(dup.dim() == 4 && dup.size(0) == N && dup.size(1) == 2 && dup.size(2) == 8 * H &&
                   dup.size(3) == 8 * W,
               "grad must be (N,2,8H,8W)");
+  TORCH_CHECK(flow.is_contiguous() && mask.is_contiguous() && dup.is_contiguous() &&
+                  mask.size(0) == N && mask.size(1) == H && mask.size(2) == W &&
+                  ((reinterpret_cast<uintptr_t>(mask.data_ptr()) | reinterpret_cast<uintptr_t>(dup.data_ptr())) & 15) == 0,
+              "convex_upsample_backward: contiguous, 16-byte aligned operands required");
   const c10::DeviceGuard guard(flow.device());
   Tensor dflow = at::empty_like(flow);
   Tensor dmask = at::empty_like(mask);

@@ -191,7 +191,7 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
               "flow_encode: coords must be fp32 (B,2,H,W)");
   const int B = coords.size(0), H = coords.size(2), W = coords.size(3);
   const int Cout = bias.numel();
-  TORCH_CHECK(Cout % 8 == 0, "flow_encode: Cout must be a multiple of 8");
+  TORCH_CHECK(Cout % 16 == 0, "flow_encode: Cout must be a multiple of 16");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.numel() == 98 * Cout,
               "flow_encode: w must be fp32 [49][2][Cout]");
   TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.is_contiguous(), "flow_encode: bias fp32");
