@@ -33,6 +33,10 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
                      int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
                      hipStream_t stream);
+void flowhead_fwd_launch(const void* x, int xstr, int xoff, int cin, const float* w, const float* bias, int B,
+                         int H, int W, float* crd, const float* src, hipStream_t s);
+void flowhead_dgrad_launch(const float* dflow, const float* w, int cin, int B, int H, int W, const void* act,
+                           int astr, int aoff, void* out, int ostr, int ooff, hipStream_t s);
 void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
                          int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd,
                          hipStream_t stream);
@@ -210,6 +214,52 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
                       out.data_ptr(), out.size(3), ooff, fp, fstr, foff, stream());
 }
 
+// Flow-head output conv (3x3, Cin in {128, 256} -> 2) with the coords epilogue:
+// crd = src + bias + conv(x[..., xoff:xoff+Cin]) (src defaults to crd: in place).
+// w: fp32 [2][3][3][Cin] (= conv2.weight.permute(0, 2, 3, 1)).
+void flow_head(const Tensor& x, int64_t xoff, int64_t cin, const Tensor& w, const Tensor& bias, const Tensor& crd,
+               const c10::optional<Tensor>& src) {
+  TORCH_CHECK(cin == 128 || cin == 256, "flow_head: Cin must be 128 or 256");
+  TORCH_CHECK(crd.is_cuda() && crd.is_contiguous() && crd.scalar_type() == at::kFloat && crd.dim() == 4 &&
+                  crd.size(1) == 2,
+              "flow_head: coords must be contiguous fp32 (B,2,H,W)");
+  const int B = crd.size(0), H = crd.size(2), W = crd.size(3);
+  check_nhwc(x, B, H, W, "x");
+  const int vn = cin == 256 ? 4 : 2;  // channels per lane: aligned vector loads
+  TORCH_CHECK(xoff >= 0 && xoff + cin <= x.size(3) && xoff % vn == 0 && x.size(3) % vn == 0,
+              "flow_head: x channel window");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.numel() == 18 * cin,
+              "flow_head: w must be fp32 [2][3][3][Cin]");
+  TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.numel() == 2, "flow_head: bias fp32 (2,)");
+  if (src) TORCH_CHECK(src->sizes() == crd.sizes() && src->is_contiguous() && src->scalar_type() == at::kFloat,
+                       "flow_head: src must match coords");
+  const c10::DeviceGuard guard(crd.device());
+  rs::flowhead_fwd_launch(x.data_ptr(), x.size(3), xoff, cin, w.data_ptr<float>(), bias.data_ptr<float>(), B, H, W,
+                          crd.data_ptr<float>(), src ? src->data_ptr<float>() : crd.data_ptr<float>(), stream());
+}
+
+// Its input gradient through the hidden ReLU: out[..., ooff:ooff+Cin] = (act > 0) * conv^T(dflow).
+void flow_head_dgrad(const Tensor& dflow, const Tensor& w, int64_t cin, const Tensor& act, int64_t aoff,
+                     const Tensor& out, int64_t ooff) {
+  TORCH_CHECK(cin == 128 || cin == 256, "flow_head_dgrad: Cin must be 128 or 256");
+  TORCH_CHECK(dflow.is_cuda() && dflow.is_contiguous() && dflow.scalar_type() == at::kFloat && dflow.dim() == 4 &&
+                  dflow.size(1) == 2,
+              "flow_head_dgrad: dflow must be contiguous fp32 (B,2,H,W)");
+  const int B = dflow.size(0), H = dflow.size(2), W = dflow.size(3);
+  check_nhwc(act, B, H, W, "act");
+  check_nhwc(out, B, H, W, "out");
+  const int vn = cin == 256 ? 4 : 2;
+  TORCH_CHECK(aoff >= 0 && aoff + cin <= act.size(3) && aoff % vn == 0 && act.size(3) % vn == 0,
+              "flow_head_dgrad: act channel window");
+  TORCH_CHECK(ooff >= 0 && ooff + cin <= out.size(3) && ooff % vn == 0 && out.size(3) % vn == 0,
+              "flow_head_dgrad: out channel window");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.numel() == 18 * cin,
+              "flow_head_dgrad: w must be fp32 [2][3][3][Cin]");
+  const c10::DeviceGuard guard(dflow.device());
+  rs::flowhead_dgrad_launch(dflow.data_ptr<float>(), w.data_ptr<float>(), cin, B, H, W, act.data_ptr(), act.size(3),
+                            aoff, out.data_ptr(), out.size(3), ooff, stream());
+}
+
 // dW (fp32, [>=Cout][taps][Ktot], accumulated) += sum_p dY[p][yoff + co] X[p + tap][k]
 void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
                 at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH, int64_t KW,
@@ -339,6 +389,8 @@ void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tenso
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
         "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
+  m.def("flow_head(Tensor x, int xoff, int cin, Tensor w, Tensor bias, Tensor(a!) crd, Tensor? src) -> ()");
+  m.def("flow_head_dgrad(Tensor dflow, Tensor w, int cin, Tensor act, int aoff, Tensor(a!) out, int ooff) -> ()");
   m.def("colsum(Tensor dy, int yoff, int C, Tensor(a!) db) -> ()");
   m.def("flow_wgrad(Tensor coords, Tensor df, Tensor(a!) dw, Tensor(b!) db) -> ()");
   m.def("gru_gate_bwd(Tensor(a!) dh, Tensor z, Tensor q, Tensor h, int hoff, Tensor(b!) dq, Tensor(c!) dzr) -> ()");
@@ -353,6 +405,8 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("flow_encode", &flow_encode);
+  m.impl("flow_head", &flow_head);
+  m.impl("flow_head_dgrad", &flow_head_dgrad);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("colsum", &colsum);
   m.impl("flow_wgrad", &flow_wgrad);

@@ -218,6 +218,8 @@ class FusedTrainEngine:
             ob += n
             pc.b = vals[of:of + bs.numel()]
             of += bs.numel()
+        fc = self.model.update_block.flow_head.conv2  # 2-channel output conv: csrc/flowhead.hip
+        self.flow_w32 = fc.weight.detach().float().permute(0, 2, 3, 1).contiguous()  # [2][3][3][256]
         self.f1w = vals[of:of + 49 * 2 * 128].view(7, 7, 2, 128)
         of += 49 * 2 * 128
         self.f1b = vals[of:of + 128]
@@ -310,7 +312,7 @@ class FusedTrainLoop(torch.autograd.Function):
             head = sl(S["head"], i)
             conv_fused([(hx1, 0, HD)], eng.head.w, eng.head.b, 3, 3, 512, EPI_RELU, head, 0)
             # coords_{i+1} = coords_i + delta (out of place: the history is kept for backward)
-            conv_fused([(head, 0, 256)], eng.flow.w, eng.flow.b, 3, 3, 2, EPI_FLOW, sl(C, i + 1), out2=coords)
+            R.flow_head(head, 0, 256, eng.flow_w32, eng.flow.b, sl(C, i + 1), coords)
             conv_fused([(head, 256, 256)], eng.mask2.w, eng.mask2.b, 1, 1, 576, EPI_SCALE, sl(S["mask"], i), 0,
                        scale=0.25)
         # every iteration's convex upsampling in one launch (they do not feed back)
@@ -346,7 +348,7 @@ class FusedTrainLoop(torch.autograd.Function):
             hx, hx1, head = sl(S["hx"], i), sl(S["hx"], i + 1), sl(S["head"], i)
             dm, df, dh = sl(S["d_mask"], i), sl(S["d_flow"], i), sl(S["d_head"], i)
             conv_fused([(dm, 0, 576)], eng.mask2.wd, None, 1, 1, 256, EPI_RELU_BWD, dh, 256, aux1=head, a1off=256)
-            conv_fused([(df, 0, 64)], eng.flow.wd, None, 3, 3, 256, EPI_RELU_BWD, dh, 0, aux1=head, a1off=0)
+            R.flow_head_dgrad(sl(dflow, i), eng.flow_w32, 256, head, 0, dh, 0)
             conv_fused([(dh, 0, 512)], eng.head.wd, None, 3, 3, HD, EPI_ACC_F32, G, 0)
             h_in = [(hx, 0), (sl(S["h1"], i), 0)]
             for p in (1, 0):

@@ -19,7 +19,7 @@ HIP launches over persistent channels-last buffers:
     conv z|r, q 5x1    (second SepConvGRU pass)
     conv head 3x3      h -> [flow-head hidden | mask hidden] (ReLU; one GEMM,
                        the mask half only on iterations that upsample)
-    conv flow 3x3      -> coords1 += delta   (coords update epilogue)
+    flow_head 3x3      -> coords1 += delta   (VALU kernel, csrc/flowhead.hip)
     conv mask 1x1      -> mask x 0.25        (upsampling iterations only)
     convex_upsample    (upsampling iterations only)
 
@@ -128,6 +128,9 @@ class FusedUpdate:
         f1 = ub.encoder.convf1
         self.f1_w = f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()  # [7][7][2][Cout]
         self.f1_b = f1.bias.detach().float().contiguous()
+        fc = ub.flow_head.conv2  # 2-channel output conv: VALU kernel (csrc/flowhead.hip)
+        self.flow_w32 = fc.weight.detach().float().permute(0, 2, 3, 1).contiguous()  # [2][3][3][Cin]
+        self.flow_b32 = fc.bias.detach().float().contiguous()
 
     def _reuse_storage(self, old):
         """Copy freshly packed weights into the previous tensors (same shapes),
@@ -144,7 +147,7 @@ class FusedUpdate:
                         p_.w.copy_(n_.w)
                         p_.b.copy_(n_.b)
                 self.gru = prev
-            elif name in ("f1_w", "f1_b") and isinstance(prev, torch.Tensor) and prev.shape == new.shape:
+            elif name in ("f1_w", "f1_b", "flow_w32", "flow_b32") and isinstance(prev, torch.Tensor) and prev.shape == new.shape:
                 prev.copy_(new)
                 self.__dict__[name] = prev
 
@@ -216,11 +219,11 @@ class FusedUpdate:
                            EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0)
             if small:
                 conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0)
-                conv_fused([(bufs["head"], 0, 128)], self.flow.w, self.flow.b, 3, 3, 2, EPI_FLOW, coords1)
+                torch.ops.raft_stir.flow_head(bufs["head"], 0, 128, self.flow_w32, self.flow_b32, coords1, None)
             else:
                 conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
                            bufs["head"], 0)
-                conv_fused([(bufs["head"], 0, 256)], self.flow.w, self.flow.b, 3, 3, 2, EPI_FLOW, coords1)
+                torch.ops.raft_stir.flow_head(bufs["head"], 0, 256, self.flow_w32, self.flow_b32, coords1, None)
             if not want_up:
                 continue
             flow = coords1 - coords0

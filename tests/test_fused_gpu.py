@@ -157,3 +157,33 @@ def test_fused_graph_replay(cuda):
     with torch.no_grad():
         _, upe = m(i2, i1, iters=8, test_mode=True)
     torch.testing.assert_close(up3, upe, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("cin", [128, 256])
+def test_flow_head_fwd_dgrad(cuda, cin):
+    """csrc/flowhead.hip: 3x3 Cin->2 conv with the coords epilogue, and its input
+    gradient through the hidden ReLU, vs fp32 PyTorch on the same bf16 operands."""
+    torch.manual_seed(0)
+    B, H, W = 2, 13, 21  # W not a multiple of the 8-pixel wave strip
+    act = torch.relu(torch.randn(B, H, W, cin + 64, device=cuda)).to(torch.bfloat16)
+    w = torch.randn(2, cin, 3, 3, device=cuda) * 0.05
+    b = torch.randn(2, device=cuda)
+    w32 = w.permute(0, 2, 3, 1).contiguous()
+    src = torch.randn(B, 2, H, W, device=cuda) * 10
+    crd = torch.empty_like(src)
+    torch.ops.raft_stir.flow_head(act, 64, cin, w32, b, crd, src)
+    x = act[..., 64:].float().permute(0, 3, 1, 2)
+    ref = src + torch.nn.functional.conv2d(x, w, b, padding=1)
+    torch.testing.assert_close(crd, ref, atol=2e-3, rtol=1e-4)
+    crd2 = src.clone()  # in place (src aliases crd)
+    torch.ops.raft_stir.flow_head(act, 64, cin, w32, b, crd2, None)
+    torch.testing.assert_close(crd2, ref, atol=2e-3, rtol=1e-4)
+    # dgrad through the ReLU of the hidden state
+    dflow = torch.randn(B, 2, H, W, device=cuda)
+    out = torch.zeros(B, H, W, cin + 32, device=cuda, dtype=torch.bfloat16)
+    torch.ops.raft_stir.flow_head_dgrad(dflow, w32, cin, act, 64, out, 32)
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, w, b, padding=1).backward(dflow)
+    dref = (xr.grad * (x > 0)).permute(0, 2, 3, 1)
+    torch.testing.assert_close(out[..., 32:].float(), dref, atol=2e-2, rtol=1e-2)
+    assert out[..., :32].abs().max().item() == 0
