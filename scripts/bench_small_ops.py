@@ -12,17 +12,25 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
-def timeit(fn, reps=30):
+def timeit(fn, reps=20):
+    """GPU time per call: the calls are captured in a hipGraph and replayed, so
+    host-side op dispatch (10-15 us per torch.ops call) is not measured."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(5):
+        g.replay()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) * 1000.0 / reps
+    return s.elapsed_time(e) * 1000.0 / (5 * reps)
 
 
 def main():
@@ -46,6 +54,16 @@ def main():
     err = ((out.float() - r).abs().max() / r.abs().max()).item()
     ferr = (hx[..., 254:].float() - (coords - c0).permute(0, 2, 3, 1)).abs().max().item()
     print(f"flow_encode 7x7 2->128  {us:7.1f} us  rel err {err:.2e}  flow slot err {ferr:.2e}", flush=True)
+    # flow-head output conv (3x3 256->2 + coords epilogue) and its dgrad
+    head = torch.relu(torch.randn(B, H, W, 512, device=dev)).to(torch.bfloat16)
+    w2k = (torch.randn(2, 256, 3, 3, device=dev) * 0.05).permute(0, 2, 3, 1).contiguous()
+    b2 = torch.randn(2, device=dev)
+    crd = torch.empty_like(coords)
+    us = timeit(lambda: R.flow_head(head, 0, 256, w2k, b2, crd, coords))
+    dfl = torch.randn(B, 2, H, W, device=dev)
+    dh = torch.empty(B, H, W, 512, device=dev, dtype=torch.bfloat16)
+    us2 = timeit(lambda: R.flow_head_dgrad(dfl, w2k, 256, head, 0, dh, 0))
+    print(f"flow_head 3x3 256->2     {us:7.1f} us   dgrad {us2:7.1f} us", flush=True)
     # convex upsampling, all iterations batched
     n = IT * B
     flow = torch.randn(n, 2, H, W, device=dev) * 3
