@@ -810,16 +810,30 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base
                                            0, 0);
 }
 
+// 4 or 8 waves.  8-wave tiles (256x96, 192x96, 128x96) are sized for the
+// training shape (P = 22816): one block per CU covers the whole pixel range in
+// ~one round, and every staged byte feeds 1.6x more MFMA work than the 4-wave
+// 128x64 tile with 3 blocks per CU (the kernel is L2->LDS bound there,
+// profiles/conv_tiles_r1.md).  When BN*8 chunks are not a multiple of the
+// thread count, the last B staging instruction of the surplus waves is a
+// zero-fill of a 1 KiB pad (every wave issues the same number of loads, so
+// the vmcnt bookkeeping stays uniform).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
-__global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
-  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves");
   static_assert(STAGES >= 2 && STAGES <= 4, "STAGES");
   constexpr int BK = 64, CPR = 8, RB = 128;
+  static_assert(BM % (WAVES_M * 16) == 0 && BN % (WAVES_N * 16) == 0, "wave tiles");
   constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
-  constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
+  static_assert((BM * CPR) % NT == 0, "A staging");
+  constexpr int NBC = BN * CPR;                 // B chunks per stage
+  constexpr int NA = BM * CPR / NT, NB = (NBC + NT - 1) / NT;
+  constexpr bool BPART = (NBC % NT) != 0;       // last B instruction only partly real
+  constexpr int PAD = BPART ? 64 : 0;
   constexpr int NLD = NA + NB;
   constexpr int kFar = 0x7ffffff0;  // past every buffer: reads as zero
-  __shared__ uint4 lds[STAGES][(BM + BN) * CPR];
+  __shared__ uint4 lds[STAGES][(BM + BN) * CPR + PAD];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
@@ -845,7 +859,7 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
   int aoff[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int id = t + 256 * i, r = id / CPR;
+    const int id = t + NT * i, r = id / CPR;
     aoff[i] = ((bm0 + r) * taps * Ktot + (((id % CPR) ^ ((r >> 1) & 7)) * 8)) * 2;
   }
   // pixel rows: offset (elements, stride-free) of pixel (y - PH, x - PW) and the valid-tap mask
@@ -853,12 +867,12 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
   unsigned bmask[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int id = t + 256 * i, r = id / CPR;
+    const int id = t + NT * i, r = id / CPR;
     const int p = bn0 + r;
     bch[i] = ((id % CPR) ^ ((r >> 1) & 7)) * 8;
     bmask[i] = 0u;
     bpix[i] = 0;
-    if (p < a.P) {
+    if (p < a.P && id < NBC) {
       const int b = p / HW, q = p - b * HW, y = q / W, x = q - y * W;
       bpix[i] = (b * H + y - a.PH) * W + (x - a.PW);
       for (int tp = 0, ty = 0, tx = 0; tp < taps; ++tp) {
@@ -884,11 +898,12 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
     const __amdgpu_buffer_rsrc_t rb = si == 0 ? rs0 : (si == 1 ? rs1 : rs2);                    \
     uint4* dst = lds[BUF];                                                                      \
     const int asoff = (tap * Ktot + kseg + c0) * 2;                                             \
-    _Pragma("unroll") for (int i = 0; i < NA; ++i) bdma16(rw, dst + wbase + 256 * i, aoff[i], asoff); \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i) bdma16(rw, dst + wbase + NT * i, aoff[i], asoff); \
     const int tsh = ty * W + tx;                                                                \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
       const int v = ((bmask[i] >> tap) & 1u) ? ((bpix[i] + tsh) * sst + c0 + bch[i]) * 2 : kFar; \
-      bdma16(rb, dst + BM * CPR + wbase + 256 * i, v, 0);                                       \
+      const bool pad = BPART && i == NB - 1 && wbase + NT * i >= NBC;                           \
+      bdma16(rb, dst + BM * CPR + (pad ? NBC : wbase + NT * i), v, 0);                          \
     }                                                                                           \
     c0 += BK; /* advance to the next K step */                                                  \
     if (c0 == sC) {                                                                             \
@@ -908,7 +923,7 @@ __global__ __launch_bounds__(256) void conv_buf_kernel(Args a) {
 
   const int lr = lane & 15, lc = lane >> 4;
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
-  constexpr uint32_t kStage = (BM + BN) * RB;
+  constexpr uint32_t kStage = (BM + BN) * RB + PAD * 16;
   uint32_t abase[2], bbase[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -1372,7 +1387,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     return e ? atoi(e) : 1;
   }();
   a.xcd_remap = xcd_env;
-  if (L.tile >= 24) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)
+  if (L.tile >= 24 && L.tile <= 26) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)
     const int TH = L.tile == 26 ? 4 : 8, BM = L.tile == 25 ? 64 : 128;
     const dim3 grid(cdiv(L.Cout, BM) * L.B * cdiv(L.H, TH) * cdiv(L.W, 16));
     if (L.tile == 24) hipLaunchKernelGGL((conv::conv_halo_kernel<128, 8, 192>), grid, dim3(256), 0, stream, a);
@@ -1423,7 +1438,19 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
         case 20: RS_BUF(128, 128, 2); break;  // wave tile 64x64: 1.5x fewer L2 bytes per FLOP than 128x64
         case 21: RS_BUF(64, 128, 2); break;
         case 22: RS_BUF(128, 128, 3); break;
-        default: RS_BUF(64, 64, 4); break;    // 23: deep ring for latency-bound small grids (inference)
+        case 23: RS_BUF(64, 64, 4); break;    // deep ring for latency-bound small grids (inference)
+#define RS_BUF8(BM_, BN_, ST_)                                                                       \
+  hipLaunchKernelGGL((conv::conv_buf_kernel<BM_, BN_, 4, 2, ST_>), dim3(cdiv(a.P, BN_) * cdiv(L.Cout, BM_)), \
+                     dim3(512), 0, stream, a)
+        // 8-wave tiles for the training shape (one block per CU, ~one round)
+        case 27: RS_BUF8(256, 96, 3); break;
+        case 28: RS_BUF8(128, 96, 3); break;
+        case 29: RS_BUF8(192, 96, 3); break;
+        case 30: RS_BUF8(256, 96, 2); break;
+        case 31: RS_BUF8(128, 96, 2); break;
+        case 32: RS_BUF8(256, 192, 2); break;
+        default: RS_BUF8(128, 192, 2); break;  // 33
+#undef RS_BUF8
 #undef RS_BUF
       }
 #undef RS_GLDS

@@ -10,6 +10,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence, Tuple
 
 import torch
@@ -50,17 +51,32 @@ def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
     return b.contiguous()
 
 
+# bitmask A/B switch for the 8-wave tiles; in-situ training bench (30 steps x2):
+# bit 4 (192-wide conv on the 192x96 tile) +0.4 %, bit 1 (Cout <= 128 on 128x96)
+# -1.4 %, bit 2 (Cout > 192) neutral -- default 4.
+_WIDE = int(os.environ.get("RS_CONV_WIDE", "4"))
+
+
 def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
     """Kernel variant for a conv (measured on MI355X, scripts/bench_conv.py;
     profiles/conv_tiles_r1.md):
     5 = split-K small-N (Cout <= 16); 16 / 17 = 128x64 / 64x64 tiles fed by
     buffer_load...lds DMA with a scalar K walk (every segment % 64 == 0, at
-    most 32 taps); 3/4 = 64x64 / 128x64 register-staged tiles with 32-deep K
-    steps otherwise."""
+    most 32 taps); 31 / 29 = the same kernel with 8 waves and 128x96 /
+    192x96 tiles (training shape: GRU 1x5 zr 34.7 -> 32.8 us, 3x3 256->192
+    40.2 -> 33.0 us); 3/4 = 64x64 / 128x64 register-staged tiles with 32-deep
+    K steps otherwise."""
     if cout <= 16:
         return 5
     if all(c % 64 == 0 for c in seg_chans) and taps <= 32:
         k = taps * sum(seg_chans)
+        if P >= 16384:  # training shape: 8-wave 128x96 / 192x96 tiles where they measured faster
+            if 64 < cout <= 128 and _WIDE & 1:
+                return 31
+            if cout > 192 and k >= 1024 and _WIDE & 2:
+                return 31
+            if 128 < cout <= 192 and k >= 1024 and _WIDE & 4:
+                return 29
         return 16 if (P >= 16384 and cout >= 192 and k >= 384) else 17
     big = cout >= 192 or (cout >= 126 and P >= 16384)
     return 4 if big else 3

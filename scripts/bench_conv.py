@@ -67,7 +67,7 @@ def main():
         w = torch.randn(cout, cin, kh, kw, device=dev) * 0.05
         b = torch.randn(cout, device=dev)
         out = torch.empty(B, H, W, pad_to(cout, 8), device=dev, dtype=torch.bfloat16)
-        wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
+        wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 256))
         bp = pack_bias(b)
         flop = 2.0 * P * cout * cin * kh * kw
         line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"

@@ -23,7 +23,8 @@ def _bf(x):
 
 
 @pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5), (5, 1)])
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7, 11, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7, 11, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26,
+                                  27, 28, 29, 30, 31, 32, 33])
 @pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
 def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     torch.manual_seed(0)
@@ -38,7 +39,7 @@ def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     w = torch.randn(cout, 40 + cb, kh, kw, device=cuda) * 0.1
     b = torch.randn(cout, device=cuda)
     # segment 0 reads 64 channels from a_buf at offset 0: weights for [8,48) only
-    wp = pack_weight(w, [(64, [(0, 40, 8)]), (cb, [(40, cb, 0)])], pad_to(cout, 128))
+    wp = pack_weight(w, [(64, [(0, 40, 8)]), (cb, [(40, cb, 0)])], pad_to(cout, 256))
     out = torch.full((B, H, W, 80), 7.0, device=cuda, dtype=torch.bfloat16)
     conv_fused([(a_buf, 0, 64), (b_buf, 0, cb)], wp, pack_bias(b), kh, kw, cout, epi, out, 4,
                scale=0.25, tile=tile)
