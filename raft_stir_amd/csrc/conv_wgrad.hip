@@ -256,17 +256,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
 //    SOURCE chunk and to the tr16 read address.
 // The bias gradient of the first N tile is summed from the staged dY tile in
 // LDS.
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restrict__ db) {
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float* __restrict__ db) {
   constexpr int RA = BM * 2, RB_ = BN * 2;               // bytes per staged pixel row
   constexpr int CA = BM / 8, CB = BN / 8;                // 16-B chunks per row
-  constexpr int NA = BK * CA / 256, NB = BK * CB / 256;  // DMA instructions per thread
-  constexpr int WM = BM / 2 / 16, WN = BN / 2 / 16;
+  constexpr int NT = 64 * WGM * WGN;                     // threads
+  constexpr int NA = BK * CA / NT, NB = BK * CB / NT;    // DMA instructions per thread
+  constexpr int WM = BM / WGM / 16, WN = BN / WGN / 16;  // MFMA tiles per wave
+  static_assert(NA * NT == BK * CA && NB * NT == BK * CB && NT % CA == 0, "tile / thread split");
   constexpr int kFar = 0x7ffffff0;
   constexpr int STAGE = BK * (RA + RB_);
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WGM, wn = wave / WGM;
   const int nkb = a.Ktot / BN;
   const int ntiles = a.taps * nkb, mtiles = cdiv(a.Cout, BM);
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -293,19 +295,19 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)sp, (short)0, sbytes, 0x00020000);
 
-  // staging: thread t, instruction i -> LDS chunk t + 256 i = (row, physical slot);
+  // staging: thread t, instruction i -> LDS chunk t + NT i = (row, physical slot);
   // the slot holds logical chunk slot ^ ((row & 3) << 1)
   int arow[NA], aoff[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int id = t + 256 * i, r = id / CA, pos = id % CA;
+    const int id = t + NT * i, r = id / CA, pos = id % CA;
     arow[i] = r;
     aoff[i] = ((pbeg + r) * a.ystr + a.yoff + m0 + ((pos ^ ((r & 3) << 1)) * 8)) * 2;
   }
   int bb[NB], by[NB], bx[NB], brow[NB], bch[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int id = t + 256 * i, r = id / CB, pos = id % CB;
+    const int id = t + NT * i, r = id / CB, pos = id % CB;
     brow[i] = r;
     bch[i] = cbase + ((pos ^ ((r & 3) << 1)) * 8);
     const int p = pbeg + r;
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                            \
       const int v = arow[i] < rem_ ? aoff[i] : kFar;                                            \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                 \
-          ry, (__attribute__((address_space(3))) void*)(st_ + (wbase + 256 * i) * 16), 16, v,   \
+          ry, (__attribute__((address_space(3))) void*)(st_ + (wbase + NT * i) * 16), 16, v,   \
           (S) * ystep, 0, 0);                                                                   \
     }                                                                                           \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
       const bool ok = brow[i] < rem_ && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W; \
       const int v = ok ? (((bb[i] * H + y) * W + x) * sst + bch[i]) * 2 : kFar;                 \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                 \
-          rx, (__attribute__((address_space(3))) void*)(st_ + BK * RA + (wbase + 256 * i) * 16), \
+          rx, (__attribute__((address_space(3))) void*)(st_ + BK * RA + (wbase + NT * i) * 16), \
           16, v, 0, 0, 0);                                                                      \
       bx[i] += BK;                                                                              \
       while (bx[i] >= W) { bx[i] -= W; ++by[i]; }                                               \
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
   float bsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
-  // bias: thread t sums logical chunk t % CA of rows t / CA + (256 / CA) j
+  // bias: thread t sums logical chunk t % CA of rows t / CA + (NT / CA) j
   const int bcol = t % CA;
 
   const int gi = lane & 15, g = lane >> 4;
@@ -360,12 +362,12 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
   uint32_t aaddr[WM], baddr[WN];
 #pragma unroll
   for (int mt = 0; mt < WM; ++mt) {
-    const int ch = ((wm * (BM / 2) + mt * 16) / 8 + (tp >> 1)) ^ swq;  // 16-B chunk
+    const int ch = ((wm * (BM / WGM) + mt * 16) / 8 + (tp >> 1)) ^ swq;  // 16-B chunk
     aaddr[mt] = lds0 + (8 * g + tq) * RA + ch * 16 + (tp & 1) * 8;
   }
 #pragma unroll
   for (int nt = 0; nt < WN; ++nt) {
-    const int ch = ((wn * (BN / 2) + nt * 16) / 8 + (tp >> 1)) ^ swq;
+    const int ch = ((wn * (BN / WGN) + nt * 16) / 8 + (tp >> 1)) ^ swq;
     baddr[nt] = lds0 + BK * RA + (8 * g + tq) * RB_ + ch * 16 + (tp & 1) * 8;
   }
   RS_WD_ISSUE(0, 0);
@@ -375,16 +377,16 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
     if (s + 1 < nsteps) RS_WD_ISSUE(s + 1, buf ^ 1);
     const uint32_t so = buf * STAGE;
     if (do_bias) {
-      u32x4_t bv[BK * CA / 256];
+      u32x4_t bv[BK * CA / NT];
 #pragma unroll
-      for (int j = 0; j < BK * CA / 256; ++j) {
-        const int r = t / CA + (256 / CA) * j;
+      for (int j = 0; j < BK * CA / NT; ++j) {
+        const int r = t / CA + (NT / CA) * j;
         asm volatile("ds_read_b128 %0, %1" : "=v"(bv[j])
                      : "v"(lds0 + so + r * RA + ((bcol ^ ((r & 3) << 1)) * 16)) : "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < BK * CA / 256; ++j) {
+      for (int j = 0; j < BK * CA / NT; ++j) {
         asm volatile("" : "+v"(bv[j]));
         bsum[0] += __uint_as_float(bv[j].x << 16);
         bsum[1] += __uint_as_float(bv[j].x & 0xffff0000u);
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float s = 0.f;
-        for (int u = t; u < 256; u += CA) s += red[u * 8 + j];
+        for (int u = t; u < NT; u += CA) s += red[u * 8 + j];
         const int co = m0 + t * 8 + j;
         if (co < a.Cout) atomicAdd(db + co, s);
       }
@@ -462,8 +464,8 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(Args a, float* __restric
     for (int nt = 0; nt < WN; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int co = m0 + wm * (BM / 2) + mt * 16 + (lane >> 4) * 4 + j;
-        const int k = kb + wn * (BN / 2) + nt * 16 + (lane & 15);
+        const int co = m0 + wm * (BM / WGM) + mt * 16 + (lane >> 4) * 4 + j;
+        const int k = kb + wn * (BN / WGN) + nt * 16 + (lane & 15);
         if (co < a.Cout) atomicAdd(a.dw + ((size_t)co * a.taps + tap) * a.Ktot + k, acc[mt][nt][j]);
       }
 }
@@ -575,10 +577,17 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.dw = L.dw;
   a.dy_bytes = L.dy_bytes;
   for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
-  const int bm = a.Cout > 64 ? 128 : 64;
+  // tile variant (L.bn128): 0 = 128x64 (64x64 for Cout <= 64), 1 = 128x128,
+  // 8-wave DMA tiles: 2 = 128x128, 3 = 256x128, 4 = 256x64, 5 = 64x128 (4 waves)
   bool seg128 = true;  // a 128-wide N tile must stay inside one segment
   for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
-  const int bn = (bm == 128 && seg128 && L.bn128) ? 128 : 64;
+  int var = L.bn128;
+  if (var < 0 || var > 5 || (!L.dma && var > 1)) var = 0;
+  if ((var == 1 || var == 2 || var == 3 || var == 5) && !seg128) var = 0;
+  if (var == 1 && a.Cout <= 64) var = 0;
+  const int bm = var == 3 || var == 4 ? 256 : (var == 5 ? 64 : (var == 0 && a.Cout <= 64 ? 64 : 128));
+  const int bn = var == 0 || var == 4 ? 64 : 128;
+  const int nthr = var >= 2 && var <= 4 ? 512 : 256;
   const int ntiles = a.taps * (a.Ktot / bn);
   const int mtiles = cdiv(a.Cout, bm);
   int ksplit = cdiv(2048, ntiles * mtiles);
@@ -587,12 +596,18 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   ksplit = cdiv(a.P, a.kchunk);
   dim3 grid(ntiles * mtiles * ksplit);
   if (L.dma) {
-    if (bn == 128)
-      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128>), grid, dim3(256), 0, stream, a, L.db);
-    else if (bm == 128)
-      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 64>), grid, dim3(256), 0, stream, a, L.db);
-    else
-      hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<64, 64>), grid, dim3(256), 0, stream, a, L.db);
+    switch (var) {
+      case 1: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
+      case 2: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128, 2, 4>), grid, dim3(nthr), 0, stream, a, L.db); break;
+      case 3: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 128, 4, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
+      case 4: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 64, 4, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
+      case 5: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<64, 128, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
+      default:
+        if (bm == 128)
+          hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 64, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db);
+        else
+          hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<64, 64, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db);
+    }
     return;
   }
   if (bn == 128)

@@ -271,9 +271,17 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16,
               "conv_wgrad: dy must be contiguous bf16 NHWC");
   const int Bp = dy.size(0), H = dy.size(1), W = dy.size(2);
+  static const int dma_env = [] {
+    const char* e = getenv("RS_WGRAD_DMA");
+    return e ? atoi(e) : 1;
+  }();
+  // the register-staged kernel reads whole BM-channel dY rows unguarded; the
+  // DMA kernels read through a range-checked buffer resource (rows past the
+  // tensor read as zero, channels >= Cout only feed discarded accumulators)
   const int bm = Cout > 64 ? 128 : 64;
-  TORCH_CHECK(yoff >= 0 && yoff % 8 == 0 && yoff + (Cout + bm - 1) / bm * bm <= dy.size(3),
-              "conv_wgrad: dy channel window (rounded up to ", bm, ") out of bounds");
+  TORCH_CHECK(yoff >= 0 && yoff % 8 == 0 && yoff + (dma_env ? Cout : (Cout + bm - 1) / bm * bm) <= dy.size(3),
+              "conv_wgrad: dy channel window out of bounds");
+  TORCH_CHECK(bn128 >= 0 && bn128 <= 5, "conv_wgrad: tile variant 0..5");
   if (db) TORCH_CHECK(db->is_cuda() && db->scalar_type() == at::kFloat && db->numel() >= Cout, "conv_wgrad: db fp32");
   TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size() &&
                   seg_period.size() == segs.size(),
@@ -313,10 +321,6 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   L.dy = dy.data_ptr(); L.ystr = dy.size(3); L.yoff = yoff; L.Cout = Cout;
   TORCH_CHECK(dy.numel() * 2 < (int64_t(1) << 31), "conv_wgrad: dY tensor must be < 2 GiB");
   L.dy_bytes = (unsigned)(dy.numel() * 2);
-  static const int dma_env = [] {
-    const char* e = getenv("RS_WGRAD_DMA");
-    return e ? atoi(e) : 1;
-  }();
   L.dma = dma_env;
   L.nseg = segs.size();
   L.Bp = Bp; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.Ktot = Ktot;

@@ -375,20 +375,23 @@ class FusedTrainLoop(torch.autograd.Function):
         hxs = S["hx"][:n]
 
         def wg(pc, dy, yoff, segs, bn128=0):
-            # weight gradient + fused bias gradient (column sums of dY); 128-wide
-            # N tiles where they measured faster (scripts/bench_conv.py --wgrad)
+            # weight gradient + fused bias gradient (column sums of dY); tile
+            # variant per conv where it measured faster (scripts/bench_conv.py
+            # --wgrad 12 at the training shape: 8-wave 256x64 for the 3x3
+            # 256->192 conv 475 -> 397 us and GRU z|r 404 -> 374 us, 8-wave
+            # 128x128 for the 128->512 head 472 -> 425 us)
             R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
                          [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db, bn128)
 
         wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
         wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
-        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)])
+        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)], 2)
         hins = [hxs, S["h1"]]
         for p in range(2):
-            wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
+            wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)], 4)
             wg(eng.q[p], S["d_q"][p], 0, [(S["rh"][p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
         wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)])
-        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)])
+        wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], 4)
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)

@@ -48,10 +48,12 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--wgrad", type=int, default=0, help="also bench wgrad with this many iterations batched")
-    ap.add_argument("--tiles", type=int, nargs="+", default=[5, 6, 7, 8])
+    ap.add_argument("--tiles", type=int, nargs="*", default=[5, 6, 7, 8])
     ap.add_argument("--only", nargs="+", default=None, help="shape names to run")
     ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5],
+                    help="wgrad tile variants (csrc/conv_wgrad.hip wgrad_launch)")
     a = ap.parse_args()
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
@@ -61,7 +63,7 @@ def main():
     P = B * H * W
     tot = {}
     for name, cin, cout, kh, kw in SHAPES:
-        if a.only and name not in a.only:
+        if (a.only and name not in a.only) or not a.tiles:
             continue
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
         w = torch.randn(cout, cin, kh, kw, device=dev) * 0.05
@@ -112,10 +114,19 @@ def main():
             db = torch.zeros(cout, device=dev)
             flop = 2.0 * n * H * W * cout * cin * kh * kw
             line = f"wgrad {name:8s} K(px)={n * H * W:7d} M={cout:4d} N={cin * kh * kw:5d} |"
-            for bn128 in (0, 1):
+            ref = None
+            for v in a.wvars:
+                def run():
+                    dw.zero_(); db.zero_()
+                    torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [n * H * W], kh, kw, dw, db, v)
+                run()
+                got = torch.cat([dw[:cout].flatten(), db[:cout]])
+                if ref is None:
+                    ref = got.clone()
+                err = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-6)).item()
                 us = timeit(lambda: torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [n * H * W], kh, kw,
-                                                                     dw, db, bn128), max(5, a.reps // 5))
-                line += f" bn128={bn128} {us:8.1f}us {flop / us / 1e6:6.1f}TF |"
+                                                                     dw, db, v), max(5, a.reps // 5))
+                line += f" v{v} {us:8.1f}us {flop / us / 1e6:6.1f}TF rel={err:.1g} |"
             print(line, flush=True)
 
 

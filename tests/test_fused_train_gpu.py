@@ -46,6 +46,30 @@ def test_wgrad_batched_with_broadcast_segment(cuda, k):
     torch.testing.assert_close(dw3[:cout], want, atol=5e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cout,k", [(70, (3, 3)), (200, (1, 5)), (320, (1, 1))])
+def test_wgrad_tile_variants(cuda, var, cout, k):
+    """Every wgrad tile variant (4- and 8-wave DMA tiles, 64..256 x 64..128)
+    vs fp32 PyTorch, ragged Cout against the M tile, multi-segment input,
+    ragged pixel count against the 64-pixel K step, fused bias gradient."""
+    torch.manual_seed(var)
+    iters, B, H, W = 3, 2, 11, 13
+    kh, kw = k
+    xa = torch.randn(iters * B, H, W, 128, device=cuda).to(torch.bfloat16)
+    xb = torch.randn(B, H, W, 128, device=cuda).to(torch.bfloat16)          # broadcast over iterations
+    dy = torch.randn(iters * B, H, W, pad_to(cout, 8), device=cuda).to(torch.bfloat16)
+    dw = torch.zeros(cout, kh * kw, 256, device=cuda)
+    db = torch.zeros(cout, device=cuda)
+    torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [xa, xb], [0, 0], [128, 128], [iters * B * H * W, B * H * W],
+                                   kh, kw, dw, db, var)
+    x = torch.cat([xa, xb.repeat(iters, 1, 1, 1)], -1).float().permute(0, 3, 1, 2)
+    w = torch.zeros(cout, 256, kh, kw, device=cuda, requires_grad=True)
+    F.conv2d(x, w, padding=(kh // 2, kw // 2)).backward(dy[..., :cout].float().permute(0, 3, 1, 2))
+    want = w.grad.permute(0, 2, 3, 1).reshape(cout, kh * kw, 256)
+    torch.testing.assert_close(dw, want, atol=5e-2, rtol=1e-2)
+    torch.testing.assert_close(db, dy[..., :cout].float().sum((0, 1, 2)), atol=5e-2, rtol=1e-3)
+
+
 def test_flow_wgrad(cuda):
     torch.manual_seed(1)
     n, H, W = 4, 10, 13
