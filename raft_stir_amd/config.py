@@ -10,6 +10,7 @@ fills the same attributes) but resolve it once into an immutable
 from __future__ import annotations
 
 import argparse
+import os
 from dataclasses import dataclass, asdict
 
 
@@ -27,6 +28,7 @@ class RAFTConfig:
     # engine knobs (not in the reference): kernel choices for the GPU path
     fused_gru: bool = True             # fused HIP gate kernels in the ConvGRU
     fused_train: bool = True           # whole-loop fused training engine (full RAFT, bf16)
+    overlap_encoders: bool = True      # context encoder on a second HIP stream (GPU)
     corr_dtype: str = "float32"        # storage dtype of the all-pairs pyramid
 
     @property
@@ -67,6 +69,7 @@ def resolve_config(args=None, **overrides) -> RAFTConfig:
         corr_levels=4,
         fused_gru=bool(_get(args, "fused_gru", True)),
         fused_train=bool(_get(args, "fused_train", True)),
+        overlap_encoders=bool(_get(args, "overlap_encoders", os.environ.get("RS_OVERLAP_ENCODERS", "1") != "0")),
         corr_dtype=str(_get(args, "corr_dtype", "float32")),
         **dims,
     )

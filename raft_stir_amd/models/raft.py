@@ -40,6 +40,9 @@ from .fused_train import FusedTrainEngine, FusedTrainLoop
 from .update import BasicUpdateBlock, SmallUpdateBlock
 
 
+_SIDE_STREAMS = {}  # device index -> second HIP stream for the context encoder
+
+
 class RAFT(nn.Module):
     def __init__(self, args=None, **overrides):
         super().__init__()
@@ -78,6 +81,13 @@ class RAFT(nn.Module):
             self.__dict__["_fused"] = eng
         return eng
 
+    @staticmethod
+    def _side_stream(dev):
+        st = _SIDE_STREAMS.get(dev.index)
+        if st is None:
+            st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+        return st
+
     def freeze_bn(self):
         for m in self.modules():
             if isinstance(m, nn.BatchNorm2d):
@@ -113,7 +123,24 @@ class RAFT(nn.Module):
         # once per forward instead of once per iteration (and its gradient
         # accumulates over the 12 iterations before a single cast back).
         gru_ops.begin_forward()
+        # The context encoder (batch B) and the feature encoder + correlation
+        # volume (batch 2B) are independent until the update loop: run cnet on
+        # a second HIP stream so its small kernels (norm finalize, bias, ReLU
+        # tails) fill the gaps of the fnet chain.  Autograd replays each
+        # backward op on its forward op's stream, so the two encoder backward
+        # passes overlap the same way (the engine inserts the cross-stream
+        # waits).  Under hipGraph capture the fork/join becomes two parallel
+        # branches of the inference graph.
+        side = None
+        if gpu and self.cfg.overlap_encoders:
+            side = self._side_stream(dev)
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
         with self._autocast(dev):
+            if side is not None:
+                with torch.cuda.stream(side):
+                    cnet = self.cnet(image1)
+                image1.record_stream(side)  # main-stream block read on side (kept by cnet's backward)
             fmap1, fmap2 = self.fnet([image1, image2])
             # The reference casts the features to fp32 (core/raft.py:102-103).
             # Under bf16 autocast they are exactly representable in bf16, so the
@@ -126,7 +153,11 @@ class RAFT(nn.Module):
             corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
                             radius=self.cfg.corr_radius, out_dtype=corr_dtype)
 
-            cnet = self.cnet(image1)
+            if side is None:
+                cnet = self.cnet(image1)
+            else:
+                main.wait_stream(side)
+                cnet.record_stream(main)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)
