@@ -45,6 +45,8 @@ autocast training (which used fp16).
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from ..ops import _ext
@@ -224,6 +226,9 @@ class FusedTrainEngine:
         of += 49 * 2 * 128
         self.f1b = vals[of:of + 128]
 
+    def side_stream(self, dev):
+        return self.model._side_stream(dev) if self.model.cfg.overlap_encoders else None
+
     def grad_buffers(self, dev):
         """One zero-filled fp32 buffer holding every packed gradient accumulator."""
         M = self._maps
@@ -290,14 +295,23 @@ class FusedTrainLoop(torch.autograd.Function):
         sl(C, 0).copy_(coords1.detach())
         c0 = coords0.detach().float().contiguous()
         inpb = S["inp"]
+        # flow branch (flow encoder + convf2) on the second HIP stream, parallel
+        # to lookup + convc1 + convc2; disjoint channels of `mot`, joined before
+        # the conv that reads it
+        main, side = torch.cuda.current_stream(dev), eng.side_stream(dev)
         for i in range(iters):
             hx, hx1 = sl(S["hx"], i), sl(S["hx"], i + 1)
             coords = sl(C, i)
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                R.flow_encode(coords, f1w, f1b, sl(S["f1"], i), 0, hx, 254)
+                conv_fused([(sl(S["f1"], i), 0, 128)], eng.f2.w, eng.f2.b, 3, 3, 64, EPI_RELU, sl(S["mot"], i), 192)
             R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
-            R.flow_encode(coords, f1w, f1b, sl(S["f1"], i), 0, hx, 254)
             conv_fused([(sl(S["corr"], i), 0, CORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, 256, EPI_RELU, sl(S["c1"], i))
             conv_fused([(sl(S["c1"], i), 0, 256)], eng.c2.w, eng.c2.b, 3, 3, 192, EPI_RELU, sl(S["mot"], i), 0)
-            conv_fused([(sl(S["f1"], i), 0, 128)], eng.f2.w, eng.f2.b, 3, 3, 64, EPI_RELU, sl(S["mot"], i), 192)
+            if side is not None:
+                main.wait_stream(side)
             conv_fused([(sl(S["mot"], i), 0, 256)], eng.cv.w, eng.cv.b, 3, 3, 126, EPI_RELU, hx, HD)
             h_in = [(hx, 0), (sl(S["h1"], i), 0)]
             h_out = [(sl(S["h1"], i), 0), (hx1, 0)]
@@ -332,6 +346,7 @@ class FusedTrainLoop(torch.autograd.Function):
         dev = c0.device
         n = iters * B
         sl = lambda t, i: t[i * B:(i + 1) * B]
+        main, side = torch.cuda.current_stream(dev), eng.side_stream(dev)
         if st.gpyr is None:
             st.gpyr = [torch.zeros_like(p) for p in st.pyr]
         G = S["G"]
@@ -364,11 +379,16 @@ class FusedTrainLoop(torch.autograd.Function):
             dc2f2 = sl(S["d_c2f2"], i)
             conv_fused([(dcv, 0, 128)], eng.cv.wd, None, 3, 3, 256, EPI_RELU_BWD, dc2f2, 0, aux1=sl(S["mot"], i))
             dc1 = sl(S["d_c1"], i)
+            if side is not None:  # convf2 dgrad (only feeds the flow-encoder wgrad) on the side stream
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                conv_fused([(dc2f2, 192, 64)], eng.f2.wd, None, 3, 3, 128, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
+                           aux1=sl(S["f1"], i))
             conv_fused([(dc2f2, 0, 192)], eng.c2.wd, None, 3, 3, 256, EPI_RELU_BWD, dc1, 0, aux1=sl(S["c1"], i))
-            conv_fused([(dc2f2, 192, 64)], eng.f2.wd, None, 3, 3, 128, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
-                       aux1=sl(S["f1"], i))
             conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, S["d_corr"], 0)
             R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, S["d_corr"])
+        if side is not None:
+            main.wait_stream(side)
 
         # ---------------- weight / bias gradients, batched over all iterations
         gbuf, dwf, dbf = eng.grad_buffers(dev)

@@ -185,15 +185,28 @@ class FusedUpdate:
         st = getattr(corr_fn, "state", None)  # None: on-the-fly correlation
         small = self.model.cfg.small
         preds, flow_up = [], None
+        # flow branch (flow encoder + convf2) on the second HIP stream, parallel
+        # to the correlation branch (lookup + convc1 + convc2): at batch 1 each
+        # of these convs fills only part of the 256 CUs.  Both write disjoint
+        # channel ranges of `mot`; joined before the conv that reads it.
+        main = torch.cuda.current_stream(coords1.device)
+        side = self.model._side_stream(coords1.device) if (not small and self.model.cfg.overlap_encoders) else None
         for itr in range(iters):
             want_up = (not test_mode) or itr == iters - 1
+            if side is not None:
+                side.wait_stream(main)  # coords1 of the previous iteration
+                with torch.cuda.stream(side):
+                    torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
+                    conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                               bufs["mot"], 192)
             if st is not None:
                 torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
             else:  # memory-efficient path: correlate the pooled fmap2 pyramid on the fly
                 c = torch.ops.raft_stir.corr_otf(corr_fn.f1, corr_fn.f2s, coords1, corr_fn.radius, corr_fn.scale,
                                                  True)
                 bufs["corr"][..., :c.shape[-1]].copy_(c)
-            torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
+            if side is None:
+                torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
             cp = self.corr_pad
             if small:
                 conv_fused([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
@@ -207,8 +220,11 @@ class FusedUpdate:
                            bufs["c1"], 0)
                 conv_fused([(bufs["c1"], 0, 256)], self.convc2.w, self.convc2.b, 3, 3, 192, EPI_RELU,
                            bufs["mot"], 0)
-                conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
-                           bufs["mot"], 192)
+                if side is None:
+                    conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                               bufs["mot"], 192)
+                else:
+                    main.wait_stream(side)
                 conv_fused([(bufs["mot"], 0, 256)], self.conv.w, self.conv.b, 3, 3, 126, EPI_RELU,
                            hx, self.off_mot)
             for zr, q in self.gru:
