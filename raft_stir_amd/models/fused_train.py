@@ -226,8 +226,11 @@ class FusedTrainEngine:
         of += 49 * 2 * 128
         self.f1b = vals[of:of + 128]
 
-    def side_stream(self, dev):
-        return self.model._side_stream(dev) if self.model.cfg.overlap_encoders else None
+    def side_stream(self, dev, slot: int = 0, flow: bool = False):
+        from .raft import OVERLAP
+        if not self.model.cfg.overlap_encoders or (flow and not OVERLAP["flow"]):
+            return None
+        return self.model._side_stream(dev, slot)
 
     def grad_buffers(self, dev):
         """One zero-filled fp32 buffer holding every packed gradient accumulator."""
@@ -280,9 +283,31 @@ class FusedTrainEngine:
         return S
 
 
+class DeferGrads(torch.autograd.Function):
+    """Identity on the update-block parameters, applied at the START of the
+    RAFT forward (before the encoders).  Its backward therefore has the
+    lowest autograd priority of the step and runs after the encoder backward
+    passes: FusedTrainLoop.backward launches the iteration-batched weight
+    gradients on the second HIP stream and returns at once, the encoders'
+    backward runs on the main stream concurrently, and this node joins the
+    streams before the gradients reach AccumulateGrad / DDP hooks / the
+    optimizer."""
+
+    @staticmethod
+    def forward(ctx, stream, *params):
+        ctx.stream = stream
+        return tuple(p.view_as(p) for p in params)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        dev = next(g.device for g in grads if g is not None)
+        torch.cuda.current_stream(dev).wait_stream(ctx.stream)
+        return (None, *grads)
+
+
 class FusedTrainLoop(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, *params):
+    def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, defer, *params):
         B, _, H, W = coords1.shape
         dev = coords1.device
         eng.pack(dev)
@@ -298,7 +323,7 @@ class FusedTrainLoop(torch.autograd.Function):
         # flow branch (flow encoder + convf2) on the second HIP stream, parallel
         # to lookup + convc1 + convc2; disjoint channels of `mot`, joined before
         # the conv that reads it
-        main, side = torch.cuda.current_stream(dev), eng.side_stream(dev)
+        main, side = torch.cuda.current_stream(dev), eng.side_stream(dev, flow=True)
         for i in range(iters):
             hx, hx1 = sl(S["hx"], i), sl(S["hx"], i + 1)
             coords = sl(C, i)
@@ -334,6 +359,7 @@ class FusedTrainLoop(torch.autograd.Function):
         flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
         up = R.convex_upsample(flows, S["mask"])
         ctx.eng, ctx.state, ctx.S, ctx.iters = eng, corr_state, S, iters
+        ctx.defer = bool(defer) and eng.side_stream(dev) is not None
         ctx.c0 = c0
         ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
         return up
@@ -346,7 +372,10 @@ class FusedTrainLoop(torch.autograd.Function):
         dev = c0.device
         n = iters * B
         sl = lambda t, i: t[i * B:(i + 1) * B]
-        main, side = torch.cuda.current_stream(dev), eng.side_stream(dev)
+        main = torch.cuda.current_stream(dev)
+        # deferred: convf2 dgrad + all weight gradients on their own stream
+        # (joined by DeferGrads.backward); else convf2 dgrad on the side stream
+        side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
         if st.gpyr is None:
             st.gpyr = [torch.zeros_like(p) for p in st.pyr]
         G = S["G"]
@@ -387,11 +416,30 @@ class FusedTrainLoop(torch.autograd.Function):
             conv_fused([(dc2f2, 0, 192)], eng.c2.wd, None, 3, 3, 256, EPI_RELU_BWD, dc1, 0, aux1=sl(S["c1"], i))
             conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, S["d_corr"], 0)
             R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, S["d_corr"])
-        if side is not None:
-            main.wait_stream(side)
+        d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
+        d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
         # ---------------- weight / bias gradients, batched over all iterations
         gbuf, dwf, dbf = eng.grad_buffers(dev)
+        if ctx.defer:  # on the weight-gradient stream, joined by DeferGrads.backward
+            side.wait_stream(main)
+            gbuf.record_stream(side)
+            wstream = torch.cuda.stream(side)
+        else:
+            if side is not None:
+                main.wait_stream(side)
+            wstream = contextlib.nullcontext()
+        with wstream:
+            grads = FusedTrainLoop._wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
+        if ctx.defer:
+            for gr in grads:
+                gr.record_stream(main)
+        token_grad = torch.zeros((), device=dev)
+        return (None, None, token_grad, d_net, d_inp, None, None, None, None, *grads)
+
+    @staticmethod
+    def _wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):
+        inpb = S["inp"]
         hxs = S["hx"][:n]
 
         def wg(pc, dy, yoff, segs, bn128=0):
@@ -415,9 +463,5 @@ class FusedTrainLoop(torch.autograd.Function):
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
-        grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype)
-                 for gr, p in zip(eng.unpack_grads(gbuf), eng.params)]
-        d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
-        d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
-        token_grad = torch.zeros((), device=dev)
-        return (None, None, token_grad, d_net, d_inp, None, None, None, *grads)
+        return [gr if gr.dtype == p.dtype else gr.to(p.dtype)
+                for gr, p in zip(eng.unpack_grads(gbuf), eng.params)]

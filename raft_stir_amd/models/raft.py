@@ -36,11 +36,32 @@ from ..ops.upsample import convex_upsample, upflow8
 from .corr import CorrBlock, AlternateCorrBlock
 from .extractor import BasicEncoder, SmallEncoder
 from .fused_update import FusedUpdate
-from .fused_train import FusedTrainEngine, FusedTrainLoop
+from .fused_train import DeferGrads, FusedTrainEngine, FusedTrainLoop
 from .update import BasicUpdateBlock, SmallUpdateBlock
 
 
-_SIDE_STREAMS = {}  # device index -> second HIP stream for the context encoder
+class _StreamHandoff(torch.autograd.Function):
+    """Identity moving a tensor produced on `side` to the current stream.
+    Marks the forward value as used by the current stream and the incoming
+    gradient (allocated on the current stream) as used by `side`, where the
+    producer's backward consumes it, so the caching allocator never hands
+    either block to the other stream while a kernel still reads it."""
+
+    @staticmethod
+    def forward(ctx, x, side):
+        ctx.side = side
+        x.record_stream(torch.cuda.current_stream(x.device))
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g.record_stream(ctx.side)
+        return g, None
+
+
+_SIDE_STREAMS = {}  # (device index, slot) -> extra HIP stream
+# per-mechanism switches of the multi-stream schedule (all gated by cfg.overlap_encoders)
+OVERLAP = {"cnet": True, "flow": True, "defer": True}
 
 
 class RAFT(nn.Module):
@@ -82,10 +103,11 @@ class RAFT(nn.Module):
         return eng
 
     @staticmethod
-    def _side_stream(dev):
-        st = _SIDE_STREAMS.get(dev.index)
+    def _side_stream(dev, slot: int = 0):
+        """slot 0: context encoder / flow branch; slot 1: deferred weight gradients."""
+        st = _SIDE_STREAMS.get((dev.index, slot))
         if st is None:
-            st = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+            st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev)
         return st
 
     def freeze_bn(self):
@@ -132,7 +154,12 @@ class RAFT(nn.Module):
         # waits).  Under hipGraph capture the fork/join becomes two parallel
         # branches of the inference graph.
         side = None
-        if gpu and self.cfg.overlap_encoders:
+        dparams = None
+        if (gpu and self.cfg.overlap_encoders and OVERLAP["defer"] and self.training and torch.is_grad_enabled() and mixed
+                and self.cfg.fused_train and not self.cfg.small and not test_mode):
+            # update-block weight gradients overlap the encoder backward (see DeferGrads)
+            dparams = DeferGrads.apply(self._side_stream(dev, 1), *self._train_engine().params)
+        if gpu and self.cfg.overlap_encoders and OVERLAP["cnet"]:
             side = self._side_stream(dev)
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
@@ -157,7 +184,7 @@ class RAFT(nn.Module):
                 cnet = self.cnet(image1)
             else:
                 main.wait_stream(side)
-                cnet.record_stream(main)
+                cnet = _StreamHandoff.apply(cnet, side)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)
@@ -169,7 +196,8 @@ class RAFT(nn.Module):
             if not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn):
                 eng = self._train_engine()
                 up = FusedTrainLoop.apply(eng, corr_fn.state, corr_fn.token, net, inp, coords0, coords1,
-                                          iters, *eng.params)
+                                          iters, dparams is not None,
+                                          *(dparams if dparams is not None else eng.params))
                 # consecutive views of one tensor: the fused loss reads it whole
                 return list(up.view(iters, *coords1.shape[:1], *up.shape[1:]).unbind(0))
 
