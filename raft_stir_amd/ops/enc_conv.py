@@ -9,7 +9,7 @@ the GPU bf16 path they run here instead of MIOpen:
   dgrad   : the same kernel on dY with the transposed, spatially flipped
             weight (a stride-1 'same' conv's input gradient is a conv)
   wgrad   : csrc/conv_wgrad.hip (split-K over pixels, fp32 accumulation);
-            channel counts it does not cover (96) use MIOpen's wgrad
+            96 input channels as two overlapping 64-channel segments
 
 Measured on MI355X at the Chairs training shape (scripts/bench_encoder_conv.py):
 fwd + dgrad + wgrad of one conv per shape 2.01 ms (MIOpen) -> 1.35 ms.
@@ -39,6 +39,21 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
     if cout <= 64:
         return 21                  # 64 co x 128 px buffer-DMA tile
     return 16 if P >= 40000 else 17
+
+
+_WGRAD_DMA = os.environ.get("RS_WGRAD_DMA", "1") != "0"
+
+
+def _wgrad_covers(cin: int, cout: int) -> bool:
+    """csrc/conv_wgrad.hip handles this conv's weight gradient: input
+    channels in 64-wide segments (a multiple of 32 >= 64 via overlapping
+    segments); the buffer-DMA kernel range-checks the dY rows of a partial
+    128-channel M tile, the register-staged one needs whole tiles."""
+    if cin % 32 or cin < 64 or cout % 32:
+        return False
+    if _WGRAD_DMA:
+        return True
+    return cin % 64 == 0 and cout % 64 == 0 and (cout <= 64 or cout % 128 == 0)
 
 
 def eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -115,11 +130,20 @@ class _Conv3x3(torch.autograd.Function):
             conv_fused([(dyn, 0, cout)], wd, None, 3, 3, cin, EPI_BIAS, dxn, 0, tile=choose_enc_tile(P, cout, cin))
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            if cin % 64 == 0 and cout % 64 == 0 and (cout <= 64 or cout % 128 == 0):
-                acc = torch.zeros(pad_to(cout, 128), 9, cin, device=x.device, dtype=torch.float32)
-                torch.ops.raft_stir.conv_wgrad(dyn, 0, cout, [xn], [0], [cin], [P], 3, 3, acc, None, 0)
-                dw = acc[:cout].view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(weight.dtype)
-            else:  # channel counts the wgrad kernel does not tile (96): MIOpen
+            if _wgrad_covers(cin, cout):
+                # the kernel tiles input channels in 64-wide segments: an odd
+                # multiple of 32 (96) is covered by two OVERLAPPING segments,
+                # [0, cin-32) and [cin-64, cin), whose dW columns are spliced
+                segs = [(0, cin)] if cin % 64 == 0 else [(0, cin - 32), (cin - 64, 64)]
+                ktot = sum(c for _, c in segs)
+                acc = torch.zeros(pad_to(cout, 128), 9, ktot, device=x.device, dtype=torch.float32)
+                torch.ops.raft_stir.conv_wgrad(dyn, 0, cout, [xn] * len(segs), [o for o, _ in segs],
+                                               [c for _, c in segs], [P] * len(segs), 3, 3, acc, None, 0)
+                acc = acc[:cout]
+                if len(segs) > 1:
+                    acc = torch.cat([acc[..., :cin - 32], acc[..., cin:cin + 32]], -1)
+                dw = acc.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(weight.dtype)
+            else:  # channel counts the wgrad kernel does not tile: MIOpen
                 dw = torch.ops.aten.convolution_backward(
                     dyn.permute(0, 3, 1, 2), x, weight.to(torch.bfloat16), None, [1, 1], [1, 1], [1, 1], False,
                     [0, 0], 1, [False, True, False])[1].to(weight.dtype)

@@ -91,15 +91,25 @@ def main():
             best_f = tf if best_f is None else min(best_f, tf)
             best_d = td if best_d is None else min(best_d, td)
         t_ww = None
-        if cin % 64 == 0:
-            dw = torch.zeros(pad_to(cout, 128), 9, cin, device=dev)
-            for bn128 in (0, 1):
-                t = timeit(lambda: (dw.zero_(), torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [P], 3, 3,
-                                                                               dw, None, bn128)), a.reps)
+        if cin % 32 == 0 and cin >= 64:
+            # 64-wide input-channel segments; 96 = two overlapping segments (ops/enc_conv.py)
+            segs = [(0, cin)] if cin % 64 == 0 else [(0, cin - 32), (cin - 64, 64)]
+            kt = sum(c for _, c in segs)
+            dw = torch.zeros(pad_to(cout, 128), 9, kt, device=dev)
+
+            def wg(v):
+                torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x] * len(segs), [o for o, _ in segs],
+                                               [c for _, c in segs], [P] * len(segs), 3, 3, dw, None, v)
+            for v in (0, 1, 2, 4):
+                t = timeit(lambda: (dw.zero_(), wg(v)), a.reps)
+                line += f" wg v{v} {t:7.1f} |"
                 t_ww = t if t_ww is None else min(t_ww, t)
             dw.zero_()
-            torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [P], 3, 3, dw, None, 0)
-            got = dw[:cout].view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+            wg(0)
+            acc = dw[:cout]
+            if len(segs) > 1:
+                acc = torch.cat([acc[..., :cin - 32], acc[..., cin:cin + 32]], -1)
+            got = acc.reshape(cout, 3, 3, cin).permute(0, 3, 1, 2)
             ew = ((got - ref_dw).abs().max() / ref_dw.abs().max()).item()
             line += f" wgrad {t_ww:7.1f} (rel {ew:.1e}) |"
         if best_f is not None:
