@@ -276,7 +276,7 @@ class FusedTrainEngine:
                 d_mask=torch.zeros(n, H, W, 640, device=dev, dtype=torch.bfloat16),
                 d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
                 d_head=e(n, 512), d_zr=[e(n, 256), e(n, 256)], d_q=[e(n, HD), e(n, HD)], d_conv=e(n, 128),
-                d_c2f2=e(n, 256), d_c1=e(n, 256), d_f1=e(n, 128), d_corr=e(B, CORR_PAD),
+                d_c2f2=e(n, 256), d_c1=e(n, 256), d_f1=e(n, 128), d_corr=e(n, CORR_PAD),
                 G=torch.empty(B, H, W, 384, device=dev),
             )
             self._bufs = {key: S}  # one shape at a time (training crops are fixed)
@@ -376,6 +376,7 @@ class FusedTrainLoop(torch.autograd.Function):
         # deferred: convf2 dgrad + all weight gradients on their own stream
         # (joined by DeferGrads.backward); else convf2 dgrad on the side stream
         side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
+        lside = eng.side_stream(dev, 0) if ctx.defer else None
         if st.gpyr is None:
             st.gpyr = [torch.zeros_like(p) for p in st.pyr]
         G = S["G"]
@@ -414,8 +415,16 @@ class FusedTrainLoop(torch.autograd.Function):
                 conv_fused([(dc2f2, 192, 64)], eng.f2.wd, None, 3, 3, 128, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
                            aux1=sl(S["f1"], i))
             conv_fused([(dc2f2, 0, 192)], eng.c2.wd, None, 3, 3, 256, EPI_RELU_BWD, dc1, 0, aux1=sl(S["c1"], i))
-            conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, S["d_corr"], 0)
-            R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, S["d_corr"])
+            dcorr = sl(S["d_corr"], i)
+            conv_fused([(dc1, 0, 256)], eng.c1.wd, None, 1, 1, CORR_PAD, EPI_BIAS, dcorr, 0)
+            # the pyramid-gradient scatter only feeds the correlation backward after the
+            # loop: on its own stream (per-iteration d_corr slots, in-order accumulation)
+            if lside is not None:
+                lside.wait_stream(main)
+            with torch.cuda.stream(lside) if lside is not None else contextlib.nullcontext():
+                R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+        if lside is not None:
+            main.wait_stream(lside)
         d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
         d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
