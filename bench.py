@@ -5,9 +5,13 @@ RCCL), plus Sintel-resolution (1088x436, padded 1088x440) 12-iteration
 inference FPS on rank 0.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-it is launched under torch.distributed.run (one rank per GPU).  W untimed
-steps, then exactly K timed steps bracketed by barrier + synchronize; the
-MAX time over ranks is reported; rank 0 prints ONE JSON line.
+the driver launches it under torch.distributed.run (one rank per GPU, RCCL).
+Started directly with ``--gpus N>1`` (no WORLD_SIZE in the environment) it
+re-launches itself the same way as a CHILD process before anything touches
+the GPU and relays the child's exit code; rank 0's JSON line is the output.
+W untimed steps, then exactly K timed steps bracketed by barrier +
+synchronize; the MAX time over ranks is reported; rank 0 prints ONE JSON
+line.  ``--device cpu`` runs the same step on CPU ranks over gloo (tests).
 
 value = total image pairs / s over all N GPUs (weak scaling: fixed per-GPU
 batch).  BASELINE.md publishes no training throughput (vs_baseline null for
@@ -45,14 +49,40 @@ def parse():
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--infer-reps", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo ranks on the CPU (plumbing tests; reference-op path)")
     ap.add_argument("--reference-ops", action="store_true",
                     help="A/B baseline: run the model on stock PyTorch-ROCm ops only "
                          "(reference semantics: matmul volume, grid_sample lookup, unfused GRU)")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` without a launcher: run N ranks under torch.distributed.run
+    as a child process (this process never initialises HIP) and relay its
+    output and exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     from raft_stir_amd.config import make_args
     from raft_stir_amd.models import RAFT
     from raft_stir_amd.parallel import dist as rdist
@@ -63,13 +93,21 @@ def main():
     if a.reference_ops:
         from raft_stir_amd.ops import _ext
         _ext.reference_mode().__enter__()
-    info = rdist.init_distributed()
-    dev = torch.device("cuda", info.local_rank)
-    torch.cuda.set_device(dev)
+    cpu = a.device == "cpu"
+    info = rdist.init_distributed(backend="gloo" if cpu else None)
+    if info.world_size != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={info.world_size}")
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", info.local_rank)
+        torch.cuda.set_device(dev)
     torch.manual_seed(1234)
 
-    margs = make_args(small=a.small, mixed_precision=not a.fp32)
-    model = RAFT(margs).to(dev).to(memory_format=torch.channels_last)
+    margs = make_args(small=a.small, mixed_precision=not a.fp32 and not cpu)
+    model = RAFT(margs).to(dev)
+    if not cpu:
+        model = model.to(memory_format=torch.channels_last)
     model.train()
     ddp = rdist.wrap_ddp(model, device=dev)
     targs = argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
@@ -88,14 +126,15 @@ def main():
         scheduler.step()
         return loss
 
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
     for _ in range(a.warmup):
         step()
     rdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     rdist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = rdist.all_reduce_max(elapsed, device=dev)
@@ -103,7 +142,7 @@ def main():
     pairs_per_s = a.batch * info.world_size * a.steps / elapsed
 
     infer = None
-    if info.is_main and not a.no_infer:
+    if info.is_main and not a.no_infer and not cpu:
         infer = bench_inference(model, dev, a)
 
     if info.is_main:
@@ -118,8 +157,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if a.fp32 else "bf16",
-            "data": "synthetic (FlyingChairs-shaped 368x496 pairs, random-init weights)",
+            "dtype": "fp32" if (a.fp32 or cpu) else "bf16",
+            "data": f"synthetic (FlyingChairs-shaped {H}x{W} pairs, random-init weights)",
             "config": {
                 "model": "RAFT-small" if a.small else "RAFT (raft-things config, 5.26M params)",
                 "global_batch": a.batch * info.world_size,
@@ -128,7 +167,11 @@ def main():
                 "image_size": [H, W],
                 "iters": a.iters,
                 "parallelism": f"dp{info.world_size}",
-                "ops": "stock-pytorch (reference semantics)" if a.reference_ops else "hip-kernels",
+                "ops": "stock-pytorch (reference semantics)" if (a.reference_ops or cpu) else "hip-kernels",
+                "grad_allreduce": ("none" if info.world_size == 1 else
+                                   "rccl: packed update-block buffer + DDP encoder buckets"
+                                   if getattr(model.__dict__.get("_fused_train"), "grad_group", None)
+                                   else f"{info.backend} DDP buckets"),
             },
             "final_loss": round(float(loss.detach()), 4),
             "inference": infer,

@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from PIL import Image  # noqa: E402
 
-from raft_stir_amd.cli_common import default_device, load_image, load_model  # noqa: E402
+from raft_stir_amd.cli_common import add_model_args, default_device, load_image, load_model  # noqa: E402
 from raft_stir_amd.data import frame_utils  # noqa: E402
 from raft_stir_amd.utils import flow_viz  # noqa: E402
 from raft_stir_amd.utils.padder import InputPadder  # noqa: E402
@@ -57,6 +57,7 @@ def demo(args):
 
 if __name__ == "__main__":
     parser = argparse.ArgumentParser()
+    add_model_args(parser)
     parser.add_argument("--model", help="restore checkpoint")
     parser.add_argument("--path", help="dataset for evaluation")
     parser.add_argument("--small", action="store_true", help="use small model")

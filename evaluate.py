@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import torch  # noqa: E402
 
-from raft_stir_amd.cli_common import load_model  # noqa: E402
+from raft_stir_amd.cli_common import add_model_args, load_model  # noqa: E402
 from raft_stir_amd.eval.evaluate import (  # noqa: E402,F401
     create_kitti_submission, create_sintel_submission, validate_chairs, validate_kitti,
     validate_sintel)
@@ -20,6 +20,7 @@ from raft_stir_amd.eval.evaluate import (  # noqa: E402,F401
 
 def main(argv=None):
     parser = argparse.ArgumentParser()
+    add_model_args(parser)
     parser.add_argument("--model", help="restore checkpoint")
     parser.add_argument("--dataset", help="dataset for evaluation: chairs | sintel | kitti")
     parser.add_argument("--small", action="store_true", help="use small model")

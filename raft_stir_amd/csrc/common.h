@@ -55,11 +55,3 @@ __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, 
 
 }  // namespace rs
 
-#define RS_HIP_CHECK(expr)                                                        \
-  do {                                                                            \
-    hipError_t _e = (expr);                                                       \
-    if (_e != hipSuccess) {                                                       \
-      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, \
-              __LINE__);                                                          \
-    }                                                                             \
-  } while (0)

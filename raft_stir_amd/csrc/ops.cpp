@@ -7,7 +7,7 @@
 // stream, so the ops compose with torch streams and hipGraph capture.
 
 #include <ATen/ATen.h>
-#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include "host_common.h"
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
@@ -59,7 +59,7 @@ namespace {
 
 using at::Tensor;
 
-hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+hipStream_t cur_stream() { return rs::current_stream(); }
 
 void check_gpu(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -106,6 +106,7 @@ std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t leve
   }
   rs::corr_volume_launch(f1.data_ptr(), f2.data_ptr(), is_bf16(f1), B, N1, H2, W2, C, levels, ptrs,
                          Hs, Ws, (float)scale, cur_stream());
+  RS_CHECK_LAUNCH();
   return outs;
 }
 
@@ -144,6 +145,7 @@ Tensor corr_lookup(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t
   for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
   rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
                              out.data_ptr(), out_bf16, cur_stream(), 0);
+  RS_CHECK_LAUNCH();
   return out;
 }
 
@@ -168,6 +170,7 @@ void corr_lookup_into(const std::vector<Tensor>& pyr, const Tensor& coords, int6
   for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
   rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
                              out.data_ptr(), is_bf16(out), cur_stream(), out.size(3));
+  RS_CHECK_LAUNCH();
 }
 
 void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords, int64_t radius,
@@ -188,6 +191,7 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
   for (int l = 0; l < levels; ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
                              dout.data_ptr(), is_bf16(dout), cur_stream(), dout.size(3));
+  RS_CHECK_LAUNCH();
 }
 
 void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
@@ -199,6 +203,7 @@ void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
+  RS_CHECK_LAUNCH();
 }
 
 // Same fold, written as bf16 into `out` (B, N1, H0, W0) instead of in place:
@@ -215,6 +220,7 @@ void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Ten
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
   rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), out.data_ptr());
+  RS_CHECK_LAUNCH();
 }
 
 // ---------------------------------------------------------------- on-the-fly corr
@@ -254,6 +260,7 @@ Tensor corr_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& c
   rs::corr_otf_fwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
                           B, H1 * W1, C, radius, (float)scale, out.data_ptr(), out_bf16,
                           cur_stream());
+  RS_CHECK_LAUNCH();
   return out;
 }
 
@@ -282,6 +289,7 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
   rs::corr_otf_bwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
                           B, H1 * W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
                           df1.data_ptr<float>(), d, cur_stream());
+  RS_CHECK_LAUNCH();
   return res;
 }
 
@@ -303,6 +311,7 @@ Tensor convex_upsample(const Tensor& flow, const Tensor& mask) {
   Tensor out = at::empty({N, 2, 8 * H, 8 * W}, flow.options());
   rs::convex_up_fwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), N, H, W,
                            out.data_ptr<float>(), cur_stream());
+  RS_CHECK_LAUNCH();
   return out;
 }
 
@@ -328,6 +337,7 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
   rs::convex_up_bwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), dup.data_ptr(),
                            is_bf16(dup), N, H, W, dmask.data_ptr(), dflow.data_ptr<float>(),
                            partial.data_ptr<float>(), cur_stream());
+  RS_CHECK_LAUNCH();
   return {dflow, dmask};
 }
 
@@ -352,6 +362,7 @@ std::vector<Tensor> gru_gate_zr(const Tensor& zr, const Tensor& h, const Tensor&
   Tensor rhx = at::empty(sz, h.options());
   rs::gru_gate_zr_launch(is_bf16(h), zr.data_ptr(), h.data_ptr(), x.data_ptr(), P, hd, cin,
                          z.data_ptr(), r.data_ptr(), rhx.data_ptr(), cur_stream());
+  RS_CHECK_LAUNCH();
   return {z, r, rhx};
 }
 
@@ -366,6 +377,7 @@ std::vector<Tensor> gru_gate_q(const Tensor& q, const Tensor& z, const Tensor& h
   Tensor hn = at::empty_like(h), qt = at::empty_like(h);
   rs::gru_gate_q_launch(is_bf16(h), q.data_ptr(), z.data_ptr(), h.data_ptr(), pixels(h),
                         h.size(-1), hn.data_ptr(), qt.data_ptr(), cur_stream());
+  RS_CHECK_LAUNCH();
   return {hn, qt};
 }
 
@@ -388,6 +400,7 @@ std::vector<Tensor> gru_bwd_q(const Tensor& dhn, const Tensor& z, const Tensor& 
   rs::gru_bwd_q_launch(is_bf16(h), dhn.data_ptr(), is_bf16(dhn), z.data_ptr(), h.data_ptr(),
                        qt.data_ptr(), P, hd, dq.data_ptr(), dzr.data_ptr(), dh.data_ptr<float>(),
                        cur_stream());
+  RS_CHECK_LAUNCH();
   return {dq, dzr, dh};
 }
 
@@ -404,6 +417,7 @@ void gru_bwd_r(const Tensor& drhx, const Tensor& h, const Tensor& r, const Tenso
   const c10::DeviceGuard guard(h.device());
   rs::gru_bwd_r_launch(is_bf16(h), drhx.data_ptr(), h.data_ptr(), r.data_ptr(), P, hd, cin,
                        dzr.data_ptr(), cur_stream());
+  RS_CHECK_LAUNCH();
 }
 
 std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Tensor& r,
@@ -426,6 +440,7 @@ std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Ten
   Tensor dx = at::empty(sz, r.options());
   rs::gru_bwd_fin_launch(is_bf16(r), dhd.data_ptr<float>(), drhx.data_ptr(), r.data_ptr(),
                          dhx.data_ptr(), P, hd, cin, dh.data_ptr(), dx.data_ptr(), cur_stream());
+  RS_CHECK_LAUNCH();
   return {dh, dx};
 }
 

@@ -2,7 +2,7 @@
 // convolution (csrc/conv.hip).  All shape, alignment and bounds checks happen
 // here on the host; the kernel assumes them.
 #include <ATen/ATen.h>
-#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include "host_common.h"
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
@@ -65,7 +65,7 @@ using at::Tensor;
 
 constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8;
 
-hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+hipStream_t stream() { return rs::current_stream(); }
 
 void check_nhwc(const Tensor& t, int B, int H, int W, const char* n, at::ScalarType dt = at::kBFloat16) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, n, ": contiguous NHWC GPU tensor required");
@@ -188,6 +188,7 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
   rs::conv_launch(L, stream());
+  RS_CHECK_LAUNCH();
 }
 
 // convf1 of the motion encoder from coords1 (flow = coords1 - grid), ReLU, bf16
@@ -216,6 +217,7 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
   const c10::DeviceGuard guard(coords.device());
   rs::flow_enc_launch(coords.data_ptr<float>(), B, H, W, w.data_ptr<float>(), bias.data_ptr<float>(), Cout,
                       out.data_ptr(), out.size(3), ooff, fp, fstr, foff, stream());
+  RS_CHECK_LAUNCH();
 }
 
 // Flow-head output conv (3x3, Cin in {128, 256} -> 2) with the coords epilogue:
@@ -240,6 +242,7 @@ void flow_head(const Tensor& x, int64_t xoff, int64_t cin, const Tensor& w, cons
   const c10::DeviceGuard guard(crd.device());
   rs::flowhead_fwd_launch(x.data_ptr(), x.size(3), xoff, cin, w.data_ptr<float>(), bias.data_ptr<float>(), B, H, W,
                           crd.data_ptr<float>(), src ? src->data_ptr<float>() : crd.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
 }
 
 // Its input gradient through the hidden ReLU: out[..., ooff:ooff+Cin] = (act > 0) * conv^T(dflow).
@@ -262,6 +265,7 @@ void flow_head_dgrad(const Tensor& dflow, const Tensor& w, int64_t cin, const Te
   const c10::DeviceGuard guard(dflow.device());
   rs::flowhead_dgrad_launch(dflow.data_ptr<float>(), w.data_ptr<float>(), cin, B, H, W, act.data_ptr(), act.size(3),
                             aoff, out.data_ptr(), out.size(3), ooff, stream());
+  RS_CHECK_LAUNCH();
 }
 
 // dW (fp32, [>=Cout][taps][Ktot], accumulated) += sum_p dY[p][yoff + co] X[p + tap][k]
@@ -328,6 +332,7 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   L.db = db ? db->data_ptr<float>() : nullptr;
   L.bn128 = bn128;
   rs::wgrad_launch(L, stream());
+  RS_CHECK_LAUNCH();
 }
 
 void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
@@ -337,6 +342,7 @@ void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
   const c10::DeviceGuard guard(dy.device());
   const int P = dy.numel() / dy.size(-1);
   rs::colsum_launch(dy.data_ptr(), dy.size(-1), yoff, C, P, db.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
 }
 
 void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const Tensor& db) {
@@ -355,6 +361,7 @@ void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const 
   const c10::DeviceGuard guard(coords.device());
   rs::flow_wgrad_launch(coords.data_ptr<float>(), Bp, H, W, df.data_ptr(), df.size(3), Cout, dw.data_ptr<float>(),
                         db.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
 }
 
 // One ConvGRU pass backward through the gates (see csrc/conv.hip gru_gate_bwd_kernel).
@@ -375,6 +382,7 @@ void gru_gate_bwd(const Tensor& dh, const Tensor& z, const Tensor& q, const Tens
   const c10::DeviceGuard guard(z.device());
   rs::gru_gate_bwd_launch(dh.data_ptr<float>(), dh.size(-1), z.data_ptr(), hd, q.data_ptr(), q.size(-1), h.data_ptr(),
                           h.size(-1), hoff, dq.data_ptr(), dq.size(-1), dzr.data_ptr(), dzr.size(-1), P, hd, stream());
+  RS_CHECK_LAUNCH();
 }
 
 // out = G[:, goff:goff+n] * (act[:, aoff:aoff+n] > 0) (zero-padded to out's width); G[:, goff:goff+nz] = 0
@@ -390,6 +398,7 @@ void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tenso
   const c10::DeviceGuard guard(out.device());
   rs::relu_take_launch(G.data_ptr<float>(), G.size(-1), goff, n, nz, act.data_ptr(), act.size(-1), aoff, out.data_ptr(),
                        out.size(-1), P, stream());
+  RS_CHECK_LAUNCH();
 }
 
 }  // namespace

@@ -1,6 +1,6 @@
 // torch.ops.raft_stir.seq_loss / seq_loss_backward (csrc/loss.hip).
 #include <ATen/ATen.h>
-#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include "host_common.h"
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
@@ -17,7 +17,7 @@ void seq_loss_bwd_launch(const float* preds, const float* gt, const float* valid
 namespace {
 using at::Tensor;
 
-hipStream_t stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+hipStream_t stream() { return rs::current_stream(); }
 
 void check(const Tensor& preds, const Tensor& gt, const Tensor& valid) {
   TORCH_CHECK(preds.is_cuda() && gt.is_cuda() && valid.is_cuda(), "seq_loss: GPU tensors expected");
@@ -46,6 +46,7 @@ Tensor seq_loss(const Tensor& preds, const Tensor& gt, const Tensor& valid, doub
   rs::seq_loss_fwd_launch(preds.data_ptr<float>(), gt.data_ptr<float>(), valid.data_ptr<float>(), N, B, HW,
                           (float)gamma, (float)max_flow, partial.data_ptr<float>(), nb, out.data_ptr<float>(),
                           stream());
+  RS_CHECK_LAUNCH();
   return out;
 }
 
@@ -61,6 +62,7 @@ Tensor seq_loss_backward(const Tensor& grad_out, const Tensor& preds, const Tens
   Tensor go = grad_out.contiguous();
   rs::seq_loss_bwd_launch(preds.data_ptr<float>(), gt.data_ptr<float>(), valid.data_ptr<float>(), N, B, HW,
                           (float)gamma, (float)max_flow, go.data_ptr<float>(), grad.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
   return grad;
 }
 }  // namespace

@@ -1,6 +1,6 @@
 // torch.ops.raft_stir.norm_* : fused NHWC normalisation + activation (csrc/norm.hip).
 #include <ATen/ATen.h>
-#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include "host_common.h"
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
@@ -24,7 +24,7 @@ void bn_running_launch(const float* mean, const float* rstd, const float* bias, 
 namespace {
 using at::Tensor;
 
-hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+hipStream_t stream() { return rs::current_stream(); }
 
 // x: (B, H, W, C) contiguous (an NCHW-shaped channels_last tensor is passed as
 // its NHWC permute by the Python side).
@@ -61,6 +61,7 @@ std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps) {
   Tensor mean = at::empty({G, C}, fo), rstd = at::empty({G, C}, fo);
   rs::norm_stats_launch(bf, x.data_ptr(), B, P, C, G, (float)eps, ws.data_ptr<float>(),
                         mean.data_ptr<float>(), rstd.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
   return {mean, rstd};
 }
 
@@ -81,6 +82,7 @@ Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
   rs::norm_fwd_launch(x.scalar_type() == at::kBFloat16, x.data_ptr(), res ? res->data_ptr() : nullptr,
                       mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
                       G, relu, y.data_ptr(), stream());
+  RS_CHECK_LAUNCH();
   return y;
 }
 
@@ -112,6 +114,7 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
                       mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
                       G, relu, batch_stats, ws.data_ptr<float>(), s1.data_ptr<float>(),
                       s2.data_ptr<float>(), dx.data_ptr(), res ? dres.data_ptr() : nullptr, stream());
+  RS_CHECK_LAUNCH();
   return {dx, dres, s1, s2};
 }
 
@@ -133,6 +136,7 @@ void bn_running_update(const Tensor& mean, const Tensor& rstd, const c10::option
   rs::bn_running_launch(mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(bias), (int)C, (float)eps,
                         (float)momentum, unb, running_mean.data_ptr<float>(), running_var.data_ptr<float>(),
                         nbt ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr, stream());
+  RS_CHECK_LAUNCH();
 }
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {

@@ -115,7 +115,12 @@ def validate_chairs(model, iters=24, root="datasets/FlyingChairs_release/data",
         epe = torch.sum((flow_pr[0] - flow_gt.to(run.dev)) ** 2, dim=0).sqrt()
         sum_epe += epe.double().sum()
         count += epe.numel()
-    epe = float(sum_epe) / max(count, 1)
+    if count == 0:
+        # an empty/missing split must not report a perfect EPE of 0 (the
+        # reference crashes in np.concatenate here; validate_sintel/kitti
+        # likewise report nothing for absent data)
+        raise FileNotFoundError(f"no FlyingChairs validation pairs under {root!r}")
+    epe = float(sum_epe) / count
     print("Validation Chairs EPE: %f" % epe)
     return {"chairs": epe}
 

@@ -139,6 +139,28 @@ class FusedTrainEngine:
         self.params += [self.f1.weight, self.f1.bias]
         self._bufs = {}
         self._maps = None
+        self.grad_group = None     # (process group, world size): packed gradient all-reduce
+        self.trace = None          # optional list: ("packed_allreduce", ...) events (tests)
+
+    def attach_grad_group(self, group, world_size: int):
+        """Data parallelism: all-reduce (average) the packed update-block
+        gradient buffer over ``group`` from the weight-gradient stream, as one
+        collective overlapping the encoder backward (parallel/dist.py)."""
+        self.grad_group = (group, int(world_size))
+
+    def reduce_packed(self, gbuf):
+        """Average ``gbuf`` over the attached group.  Issued on the CURRENT
+        stream (the weight-gradient stream when deferred): the process group's
+        RCCL stream waits for it, and ``work.wait()`` makes the current stream
+        -- not the host, not the main stream -- wait for the collective."""
+        import torch.distributed as dist
+        group, ws = self.grad_group
+        if ws > 1:
+            gbuf.mul_(1.0 / ws)
+        work = dist.all_reduce(gbuf, group=group, async_op=True)
+        if self.trace is not None:
+            self.trace.append(("packed_allreduce", gbuf.numel()))
+        work.wait()
 
     def _build_maps(self, dev):
         """Static gather maps: packing every update-block weight for the fused
@@ -254,12 +276,17 @@ class FusedTrainEngine:
         return out
 
     @staticmethod
+    def config_capable(cfg) -> bool:
+        """The configuration half of ``eligible`` (no tensors needed)."""
+        return (bool(cfg.mixed_precision) and cfg.fused_gru and not cfg.small and not cfg.alternate_corr
+                and getattr(cfg, "fused_train", True))
+
+    @staticmethod
     def eligible(model, image, corr_fn) -> bool:
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
-                and model.cfg.mixed_precision and model.cfg.fused_gru and not model.cfg.small
+                and FusedTrainEngine.config_capable(model.cfg)
                 and getattr(corr_fn, "hip", False) and getattr(corr_fn, "state", None) is not None
-                and _ext.use_hip(image)
-                and getattr(model.cfg, "fused_train", True))
+                and _ext.use_hip(image))
 
     def buffers(self, B, H, W, iters, dev):
         key = (B, H, W, iters, dev)
@@ -439,7 +466,11 @@ class FusedTrainLoop(torch.autograd.Function):
                 main.wait_stream(side)
             wstream = contextlib.nullcontext()
         with wstream:
-            grads = FusedTrainLoop._wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
+            FusedTrainLoop._wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
+            if eng.grad_group is not None:  # data parallel: one RCCL all-reduce of the packed buffer
+                eng.reduce_packed(gbuf)
+            grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype)
+                     for gr, p in zip(eng.unpack_grads(gbuf), eng.params)]
         if ctx.defer:
             for gr in grads:
                 gr.record_stream(main)
@@ -472,5 +503,3 @@ class FusedTrainLoop(torch.autograd.Function):
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
-        return [gr if gr.dtype == p.dtype else gr.to(p.dtype)
-                for gr, p in zip(eng.unpack_grads(gbuf), eng.params)]

@@ -201,6 +201,14 @@ class RAFT(nn.Module):
                 # consecutive views of one tensor: the fused loss reads it whole
                 return list(up.view(iters, *coords1.shape[:1], *up.shape[1:]).unbind(0))
 
+            eng_t = self.__dict__.get("_fused_train")
+            if (eng_t is not None and eng_t.grad_group is not None and not test_mode and self.training
+                    and torch.is_grad_enabled()):
+                # DDP ignores the update-block parameters: only the fused engine reduces them
+                raise RuntimeError("data-parallel RAFT was wrapped for the fused training engine, "
+                                   "but this step is not eligible for it (update-block gradients "
+                                   "would not be all-reduced)")
+
             if FusedUpdate.eligible(self, image1, corr_fn):
                 eng = self._fused_engine()
                 coords1, preds, flow_up = eng.run(net, inp, corr_fn, coords0, coords1, iters, test_mode)

@@ -7,12 +7,24 @@ process per GPU:
 
 * ``torch.distributed`` backend ``nccl`` (= RCCL on ROCm) for GPUs, ``gloo``
   for CPU ranks (tests);
-* gradients all-reduced in buckets by DDP hooks *during* backward on DDP's
-  communication stream, overlapping the unrolled 12-iteration backward.
-  RAFT's 21 MB of fp32 gradients are split into ~5 MB buckets so the first
-  all-reduces start while the encoder backward is still running; on an
-  8 x MI355X node a ring over the 7 xGMI links moves ~37 MB per rank per step,
-  well under 1 % of a training step;
+* gradients all-reduced *during* backward, in two parts:
+  - the update block (~57 % of RAFT's 21 MB of fp32 gradients) is trained by
+    the fused engine (models/fused_train.py), whose weight gradients land in
+    ONE packed fp32 buffer on the weight-gradient HIP stream.  That buffer is
+    all-reduced as a single RCCL collective issued from that stream the
+    moment the last iteration-batched wgrad GEMM is queued -- i.e. while the
+    encoder backward is still running on the main stream -- and DDP is told
+    to ignore those parameters;
+  - the encoder gradients go through DDP's reducer buckets (hooks on
+    AccumulateGrad, ~5 MB buckets, RCCL stream), which fire as the encoder
+    backward produces them.
+  On an 8 x MI355X node a ring over the 7 xGMI links moves ~37 MB per rank
+  per step -- a fraction of a millisecond -- and nothing of it sits at the
+  end of backward except the last encoder bucket.
+  Stream budget per process (GPU_MAX_HW_QUEUES = 4): main, side 0 (context
+  encoder / flow branch / pyramid-gradient scatter), side 1 (weight
+  gradients + the packed all-reduce issue point), and the process group's
+  RCCL stream;
 * the loss is computed on each rank (no prediction gather at all);
 * BatchNorm stays un-synced (reference behaviour) with buffers broadcast from
   rank 0 like DataParallel's replica-0 semantics.
@@ -49,10 +61,11 @@ def env_info() -> DistInfo:
                     local_rank=int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
-    """Initialise from torchrun-style env vars; no-op for a single process."""
+def init_distributed(backend: str | None = None, timeout_s: int = 600, force: bool = False) -> DistInfo:
+    """Initialise from torchrun-style env vars; no-op for a single process
+    unless ``force`` (a world of one, e.g. to exercise RCCL on one GPU)."""
     info = env_info()
-    if info.world_size <= 1:
+    if info.world_size <= 1 and not force:
         return info
     use_gpu = torch.cuda.is_available() and backend != "gloo"
     if backend is None:
@@ -85,17 +98,46 @@ def barrier():
 
 
 def wrap_ddp(model, device=None, bucket_cap_mb: float = 5.0, broadcast_buffers: bool = True,
-             static_graph: bool = False):
-    """DistributedDataParallel with RAFT-sized buckets (no-op single process)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+             static_graph: bool = False, force: bool = False, packed_update_grads: bool | None = None):
+    """DistributedDataParallel with RAFT-sized buckets.
+
+    No-op for a single process unless ``force`` (wraps a world of one, so the
+    DDP/RCCL path can be exercised on one GPU).  ``packed_update_grads``
+    (default: whenever the fused training engine will train the update
+    block) hands the update-block gradients to the engine's packed
+    all-reduce and makes DDP ignore those parameters (module docstring)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return model
+    if dist.get_world_size() == 1 and not force:
         return model
     from torch.nn.parallel import DistributedDataParallel as DDP
+    if packed_update_grads is None:
+        packed_update_grads = _fused_train_capable(model, device)
+    if packed_update_grads:
+        eng = model._train_engine()
+        ids = {id(p) for p in eng.params}
+        names = [n for n, p in model.named_parameters() if id(p) in ids]
+        # DDP does not broadcast ignored parameters: replicate them from rank 0 here
+        with torch.no_grad():
+            for p in eng.params:
+                dist.broadcast(p.data, 0)
+        DDP._set_params_and_buffers_to_ignore_for_model(model, names)
+        eng.attach_grad_group(dist.group.WORLD, dist.get_world_size())
     kw = dict(bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
               gradient_as_bucket_view=True, static_graph=static_graph)
     if device is not None and device.type == "cuda":
         kw["device_ids"] = [device.index]
         kw["output_device"] = device.index
     return DDP(model, **kw)
+
+
+def _fused_train_capable(model, device) -> bool:
+    """Will RAFT training on ``device`` run through the fused training engine?"""
+    cfg = getattr(model, "cfg", None)
+    if cfg is None or not hasattr(model, "_train_engine") or device is None or device.type != "cuda":
+        return False
+    from ..models.fused_train import FusedTrainEngine
+    return FusedTrainEngine.config_capable(cfg)
 
 
 def unwrap(model):

@@ -164,6 +164,42 @@ def load_resume(path: str, model, optimizer=None, scheduler=None, scaler=None,
     return obj
 
 
+def rank_rng_path(path: str, rank: int) -> str:
+    return f"{path}.rank{rank}.rng"
+
+
+def save_rank_rng(path: str, rank: int, generators: Optional[dict] = None):
+    """Per-rank RNG sidecar of a resume file: every rank's own CPU/CUDA/numpy/
+    python RNG streams plus named extra generators (e.g. the --add_noise
+    generator), so a resumed multi-rank run continues each rank's streams
+    instead of giving every rank rank 0's."""
+    rng = _rng_state()
+    rng["numpy"] = _np_state_to_safe(rng["numpy"])
+    py = rng["python"]
+    rng["python"] = [py[0], list(py[1]), py[2]]
+    rng["generators"] = {k: g.get_state() for k, g in (generators or {}).items()}
+    _atomic_save({"format": "raft_stir_amd.rank_rng/1", "rank": int(rank), "rng": rng}, rank_rng_path(path, rank))
+
+
+def load_rank_rng(path: str, rank: int, generators: Optional[dict] = None) -> bool:
+    """Restore this rank's sidecar (written by save_rank_rng); False if absent."""
+    side = rank_rng_path(path, rank)
+    if not os.path.exists(side):
+        return False
+    obj = torch.load(side, map_location="cpu", weights_only=True)
+    assert obj.get("format", "").startswith("raft_stir_amd.rank_rng") and obj["rank"] == rank, side
+    rng = dict(obj["rng"])
+    gens = rng.pop("generators", {})
+    rng["numpy"] = _np_state_from_safe(rng["numpy"])
+    py = rng["python"]
+    rng["python"] = (py[0], tuple(py[1]), py[2])
+    _set_rng_state(rng)
+    for k, g in (generators or {}).items():
+        if k in gens:
+            g.set_state(gens[k])
+    return True
+
+
 def latest_resume(directory: str, name: str = "") -> Optional[str]:
     pats = glob.glob(os.path.join(directory, f"{name}*resume_*.pt"))
     best, best_step = None, -1

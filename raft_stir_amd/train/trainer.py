@@ -132,6 +132,11 @@ def train(args):
     optimizer, scheduler = fetch_optimizer(args, model)
     scaler = torch.amp.GradScaler("cuda", enabled=False)  # bf16 needs no loss scaling
 
+    noise_gen = None
+    if args.add_noise:
+        noise_gen = torch.Generator(device=dev)
+        noise_gen.manual_seed(args.seed * 7919 + info.rank)
+    generators = {"noise": noise_gen} if noise_gen is not None else {}
     start_step, start_epoch, start_batch = 0, 0, 0
     resume_path = ckpt.latest_resume(args.ckpt_dir, args.name) if args.resume == "auto" else args.resume
     if resume_path:
@@ -140,6 +145,8 @@ def train(args):
         start_step = int(obj["step"])
         start_epoch = int(obj["extra"].get("epoch", 0))
         start_batch = int(obj["extra"].get("batch", 0))
+        # each rank's own RNG streams (+ the noise generator) from its sidecar
+        ckpt.load_rank_rng(resume_path, info.rank, generators)
         if info.is_main:
             print(f"resumed from {resume_path} at step {start_step}")
 
@@ -150,10 +157,6 @@ def train(args):
                     pairs_per_step=per_rank * info.world_size, reduce_fn=rdist.all_reduce_mean,
                     start_step=start_step)
 
-    noise_gen = None
-    if args.add_noise:
-        noise_gen = torch.Generator(device=dev)
-        noise_gen.manual_seed(args.seed * 7919 + info.rank)
     fused_opt = any(g.get("fused") for g in optimizer.param_groups)
     params = [p for p in model.parameters() if p.requires_grad]
     skipped = torch.zeros((), device=dev)
@@ -203,10 +206,11 @@ def train(args):
                 raise NonFiniteError(f"{int(consecutive)} consecutive non-finite steps")
 
             if total_steps % args.val_freq == args.val_freq - 1:
+                resume_file = os.path.join(args.ckpt_dir, "%s_resume_%d.pt" % (args.name, total_steps + 1))
+                ckpt.save_rank_rng(resume_file, info.rank, generators)
                 if info.is_main:
                     ckpt.save_weights(model, os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name)))
-                    ckpt.save_resume(os.path.join(args.ckpt_dir, "%s_resume_%d.pt" % (args.name, total_steps + 1)),
-                                     model, optimizer, scheduler, scaler, step=total_steps + 1,
+                    ckpt.save_resume(resume_file, model, optimizer, scheduler, scaler, step=total_steps + 1,
                                      extra={"epoch": epoch, "batch": batch_in_epoch})
                     results = run_validation(model, args)
                     logger.write_dict(results)

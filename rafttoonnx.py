@@ -6,8 +6,8 @@ onnx package is installed), plus the bare-model exports
 
 Defaults match the reference's hard-coded values (models/raft-small.pth,
 demo-frames, RAFT-small), but unlike the reference the CLI flags are honoured
-(defect B12), the export images are in [0, 255], and a missing checkpoint
-falls back to random-init weights.
+(defect B12) and the export images are in [0, 255].  A missing checkpoint is
+an error unless ``--random_init`` is given (then random-init weights).
 """
 import argparse
 import glob
@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import torch  # noqa: E402
 
-from raft_stir_amd.cli_common import load_image, load_model  # noqa: E402
+from raft_stir_amd.cli_common import add_model_args, load_image, load_model  # noqa: E402
 from raft_stir_amd.export.pointtrack import (NUMITERS, POINTCOUNT, RaftPointTrack, _FlowOnly,  # noqa: E402
                                              export_onnx, export_pointtrack, export_torchscript,
                                              onnx_available)
@@ -58,6 +58,7 @@ def convertmodelpointtrack(args, device):
 
 if __name__ == "__main__":
     parser = argparse.ArgumentParser()
+    add_model_args(parser)
     parser.add_argument("--model", default="models/raft-small.pth", help="restore checkpoint")
     parser.add_argument("--path", default="demo-frames", help="frames for the demo-shape export")
     parser.add_argument("--small", action=argparse.BooleanOptionalAction, default=True)

@@ -34,6 +34,12 @@ def test_validate_all(fake_root, small_model):
     assert set(res) == {"kitti-epe", "kitti-f1"} and 0 <= res["kitti-f1"] <= 100
 
 
+def test_chairs_empty_root_raises(tmp_path, small_model):
+    (tmp_path / "split.txt").write_text("")
+    with pytest.raises(FileNotFoundError):
+        ev.validate_chairs(small_model, iters=2, root=str(tmp_path / "none"), split_file=str(tmp_path / "split.txt"))
+
+
 def test_chairs_epe_matches_manual(fake_root, small_model):
     from raft_stir_amd.data import datasets
     r = str(fake_root)
@@ -91,18 +97,23 @@ def test_cli_scripts(fake_root, tmp_path):
     frames = sorted(glob.glob(f"{r}/Sintel/training/clean/alley/*.png"))
     res = subprocess.run([sys.executable, os.path.join(ROOT, "demo.py"), "--small", "--path",
                           os.path.dirname(frames[0]), "--iters", "2", "--out", str(tmp_path / "demo"),
-                          "--model", str(tmp_path / "missing.pth")],
+                          "--model", str(tmp_path / "missing.pth"), "--random_init"],
                          env=env, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-2000:]
     assert len(glob.glob(str(tmp_path / "demo" / "*_flow.png"))) == 2
     res = subprocess.run([sys.executable, os.path.join(ROOT, "evaluate.py"), "--small", "--dataset", "kitti",
-                          "--data_root", r, "--iters", "2"], env=env, capture_output=True, text=True, timeout=600)
+                          "--data_root", r, "--iters", "2", "--random_init"], env=env, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0 and "Validation KITTI" in res.stdout, res.stderr[-2000:]
     res = subprocess.run([sys.executable, os.path.join(ROOT, "rafttoonnx.py"), "--path", os.path.dirname(frames[0]),
-                          "--model", str(tmp_path / "missing.pth"), "--out", str(tmp_path / "exp")],
+                          "--model", str(tmp_path / "missing.pth"), "--random_init", "--out", str(tmp_path / "exp")],
                          env=env, capture_output=True, text=True, timeout=900)
     assert res.returncode == 0, res.stderr[-2000:]
     assert os.path.exists(tmp_path / "exp" / "raft_pointtrackSTIR.pt")
+    # without --random_init a missing checkpoint is an error (reference CLIs load strictly)
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "evaluate.py"), "--small", "--dataset", "kitti",
+                          "--data_root", r, "--model", str(tmp_path / "typo.pth")], env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode != 0 and "typo.pth" in res.stderr
 
 
 def test_core_shim_imports():

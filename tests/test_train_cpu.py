@@ -41,6 +41,36 @@ def test_resume_after_fault_is_exact(tmp_path):
         torch.testing.assert_close(b[k], a[k], atol=0, rtol=0, msg=k)
 
 
+def test_resume_with_noise_is_exact(tmp_path):
+    """--add_noise draws from its own generator: its state (and every rank's
+    RNG) lives in the per-rank sidecar, so a resumed run continues the noise
+    stream instead of restarting it from the seed."""
+    extra = ["--num_steps", "5", "--add_noise"]
+    ref_path = _run(tmp_path / "a", "nz", extra)
+    with pytest.raises(trainer.InjectedFault):
+        _run(tmp_path / "b", "nz", extra + ["--fault_at_step", "4"])
+    assert os.path.exists(ckpt.rank_rng_path(str(tmp_path / "b" / "ck" / "nz_resume_3.pt"), 0))
+    res_path = _run(tmp_path / "b", "nz", extra + ["--resume", "auto"])
+    a = torch.load(ref_path, weights_only=True)
+    b = torch.load(res_path, weights_only=True)
+    for k in a:
+        torch.testing.assert_close(b[k], a[k], atol=0, rtol=0, msg=k)
+
+
+def test_rank_rng_sidecar_roundtrip(tmp_path):
+    p = str(tmp_path / "r_resume_1.pt")
+    g = torch.Generator().manual_seed(5)
+    torch.manual_seed(11)
+    ckpt.save_rank_rng(p, 3, {"noise": g})
+    want_t, want_g = torch.rand(4), torch.rand(4, generator=g)
+    torch.manual_seed(99)
+    g2 = torch.Generator().manual_seed(0)
+    assert ckpt.load_rank_rng(p, 3, {"noise": g2})
+    torch.testing.assert_close(torch.rand(4), want_t, atol=0, rtol=0)
+    torch.testing.assert_close(torch.rand(4, generator=g2), want_g, atol=0, rtol=0)
+    assert not ckpt.load_rank_rng(p, 4)
+
+
 def test_resume_file_contents(tmp_path):
     from raft_stir_amd.config import make_args
     from raft_stir_amd.models import RAFT
