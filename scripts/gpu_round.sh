@@ -4,10 +4,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD FAILED; tail -30 gpurun_out/build.log; exit 1; }
+test -f raft_stir_amd/_C.so && test -f raft_stir_amd/_host.so || { echo "prebuilt extension missing: run the build on the CPU first"; exit 1; }
 STEP=${1:-all}
 if [[ $STEP == all || $STEP == tests ]]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -40 gpurun_out/pytest_gpu.log; [[ $rc -ne 0 ]] && exit $rc
 fi
 if [[ $STEP == all || $STEP == smoke ]]; then
