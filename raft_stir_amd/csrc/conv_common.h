@@ -1,0 +1,449 @@
+// Shared pieces of the implicit-GEMM convolution kernels (conv.hip, conv_hx.hip):
+// epilogue kinds, the launch-argument block, the fused epilogues and the
+// staging helpers (buffer / global LDS-DMA, counted vmcnt waits, XCD remap).
+#pragma once
+#include "common.h"
+
+#include <stdlib.h>
+
+namespace rs {
+namespace conv {
+
+enum Epi : int {
+  EPI_BIAS = 0,
+  EPI_RELU = 1,
+  EPI_SCALE = 2,   // (acc + b) * scale
+  EPI_GRU_ZR = 3,  // co < hd: z -> out ; co >= hd: r*h -> out2 (r -> out3 if set)
+  EPI_GRU_Q = 4,   // h' = (1-z) h + z tanh(acc + b) -> out (q~ -> out2 if set)
+  EPI_FLOW = 5,    // coords (fp32 NCHW) = (out2 ? out2 : coords) + acc + b   (co < 2)
+  // backward (dgrad) epilogues
+  EPI_RELU_BWD = 6,  // out(bf16) = v * (aux1 > 0)            (through the producer's ReLU)
+  EPI_ACC_F32 = 7,   // out(fp32) += v                        (gradient accumulation)
+  EPI_GRU_QBWD = 8,  // co < hd: drh = v -> out2(bf16)[co] = drh*h*r*(1-r) (dr_pre), out[co] += drh*r
+                     // co >= hd: out(fp32)[co] += v          (h = aux1, r = aux2)
+};
+
+struct Seg {
+  const bf16_t* ptr;
+  int C;       // channels read (multiple of 32)
+  int stride;  // row stride in elements (multiple of 8)
+};
+
+struct Args {
+  Seg seg[3];
+  int nseg;
+  const bf16_t* w;  // [Cout_pad][taps][Ktot]
+  const float* bias;
+  int B, H, W, P;
+  int KH, KW, PH, PW;
+  int Cout, Ktot;
+  int epi;
+  float scale;
+  int hd;
+  // outputs (element strides/offsets)
+  void* out;
+  int ostr, ooff;
+  void* out2;
+  int o2str, o2off;
+  void* out3;
+  int o3str, o3off;
+  // aux inputs (bf16 NHWC)
+  const bf16_t* aux1;  // h
+  int a1str, a1off;
+  const bf16_t* aux2;  // z
+  int a2str, a2off;
+  int xcd_remap;  // conv_glds_kernel: remap block ids so each XCD walks contiguous tiles
+  unsigned seg_bytes[3];
+  unsigned w_bytes;
+};
+
+__device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// Shared epilogue: acc[mt][nt][j] holds output channel m0 + mt*16 + 4*(lane>>4) + j
+// of flat pixel pp[nt] = (pb*H + py)*W + px (pb < 0: no pixel).  The epilogue
+// kind is a template parameter of the fragment loop (dispatched once, outside
+// it): with a runtime switch inside, the 16-fragment loops of the 4x4 wave
+// tiles were too large to unroll and the accumulators went to scratch.
+// 4 consecutive channels per lane: one 8-byte (bf16) / 16-byte (fp32) access
+// when every epilogue base, offset and stride is a multiple of 4 elements
+// (checked once per launch, see epi_loop); the element-wise forms otherwise.
+__device__ __forceinline__ void ld4(const bf16_t* p, float (&f)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  f[0] = bf2f((bf16_t)(u.x & 0xffffu));
+  f[1] = bf2f((bf16_t)(u.x >> 16));
+  f[2] = bf2f((bf16_t)(u.y & 0xffffu));
+  f[3] = bf2f((bf16_t)(u.y >> 16));
+}
+__device__ __forceinline__ void st4(bf16_t* p, const float (&f)[4]) {
+  uint2 pk;
+  pk.x = uint32_t(f2bf(f[0])) | (uint32_t(f2bf(f[1])) << 16);
+  pk.y = uint32_t(f2bf(f[2])) | (uint32_t(f2bf(f[3])) << 16);
+  *reinterpret_cast<uint2*>(p) = pk;
+}
+__device__ __forceinline__ void acc4(float* p, const float (&f)[4]) {
+  float4 o = *reinterpret_cast<float4*>(p);
+  o.x += f[0];
+  o.y += f[1];
+  o.z += f[2];
+  o.w += f[3];
+  *reinterpret_cast<float4*>(p) = o;
+}
+
+template <int E>
+__device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, int p, int pb, int py, int px,
+                                         int HW, bool vec) {
+  const bool full = cb + 3 < a.Cout;
+  if constexpr (E == EPI_FLOW) {  // coords (+)= delta; out2 (if set) is the source coords
+    float* crd = static_cast<float*>(a.out);
+    const float* src = a.out2 ? static_cast<const float*>(a.out2) : crd;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = cb + j;
+      if (co < a.Cout && co < 2) {
+        const size_t o = ((size_t)pb * 2 + co) * HW + (size_t)py * a.W + px;
+        crd[o] = src[o] + v[j];
+      }
+    }
+  } else if constexpr (E == EPI_GRU_ZR) {
+    if (cb < a.hd) {
+      bf16_t* z = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+      float zv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zv[j] = sigmoidf_(v[j]);
+      if (vec) {
+        st4(z, zv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[j] = f2bf(zv[j]);
+      }
+    } else {
+      const int c = cb - a.hd;
+      const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + c;
+      bf16_t* rh = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + c;
+      bf16_t* rs_ = a.out3 ? static_cast<bf16_t*>(a.out3) + (size_t)p * a.o3str + a.o3off + c : nullptr;
+      float hv[4], rv[4], rhv[4];
+      if (vec) {
+        ld4(h, hv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hv[j] = bf2f(h[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rv[j] = sigmoidf_(v[j]);
+        rhv[j] = rv[j] * hv[j];
+      }
+      if (vec) {
+        st4(rh, rhv);
+        if (rs_) st4(rs_, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          rh[j] = f2bf(rhv[j]);
+          if (rs_) rs_[j] = f2bf(rv[j]);
+        }
+      }
+    }
+  } else if constexpr (E == EPI_GRU_Q) {
+    const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+    const bf16_t* z = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+    bf16_t* hn = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    bf16_t* qs = a.out2 ? static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb : nullptr;
+    float hv[4], zv[4], qv[4], nv[4];
+    if (vec) {
+      ld4(h, hv);
+      ld4(z, zv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hv[j] = bf2f(h[j]);
+        zv[j] = bf2f(z[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      qv[j] = tanhf_(v[j]);
+      nv[j] = (1.f - zv[j]) * hv[j] + zv[j] * qv[j];
+    }
+    if (vec) {
+      st4(hn, nv);
+      if (qs) st4(qs, qv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hn[j] = f2bf(nv[j]);
+        if (qs) qs[j] = f2bf(qv[j]);
+      }
+    }
+  } else if constexpr (E == EPI_RELU_BWD) {
+    const bf16_t* act = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (vec && full) {
+      float av[4], ov[4];
+      ld4(act, av);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ov[j] = av[j] > 0.f ? v[j] : 0.f;
+      st4(o, ov);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = f2bf(bf2f(act[j]) > 0.f ? v[j] : 0.f);
+    }
+  } else if constexpr (E == EPI_ACC_F32) {
+    float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (vec && full) {
+      acc4(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] += v[j];
+    }
+  } else if constexpr (E == EPI_GRU_QBWD) {
+    float* o = static_cast<float*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (cb < a.hd) {
+      const bf16_t* h = a.aux1 + (size_t)p * a.a1str + a.a1off + cb;
+      const bf16_t* r = a.aux2 + (size_t)p * a.a2str + a.a2off + cb;
+      bf16_t* drp = static_cast<bf16_t*>(a.out2) + (size_t)p * a.o2str + a.o2off + cb;
+      float hv[4], rv[4], dv[4], gv[4];
+      if (vec) {
+        ld4(h, hv);
+        ld4(r, rv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hv[j] = bf2f(h[j]);
+          rv[j] = bf2f(r[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dv[j] = v[j] * hv[j] * rv[j] * (1.f - rv[j]);
+        gv[j] = v[j] * rv[j];
+      }
+      if (vec) {
+        st4(drp, dv);
+        acc4(o, gv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          drp[j] = f2bf(dv[j]);
+          o[j] += gv[j];
+        }
+      }
+    } else {
+      if (vec && full) {
+        acc4(o, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (cb + j < a.Cout) o[j] += v[j];
+      }
+    }
+  } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE -> bf16
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (E == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+      if constexpr (E == EPI_SCALE) v[j] *= a.scale;
+    }
+    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    if (vec && full) {
+      st4(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = f2bf(v[j]);
+    }
+  }
+}
+
+template <int WM, int WN, int E>
+__device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                         const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
+                                         const int (&px)[WN]) {
+  const int HW = a.H * a.W;
+  const int cq = (lane >> 4) * 4;
+  // wave-uniform: every epilogue tensor 4-element aligned (vector accesses)
+  const bool vec =
+      ((a.ooff | a.ostr | a.o2off | a.o2str | a.o3off | a.o3str | a.a1off | a.a1str | a.a2off | a.a2str) & 3) == 0 &&
+      (((uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.out3 | (uintptr_t)a.aux1 | (uintptr_t)a.aux2) & 15) == 0;
+  const bool bvec = a.bias && (((uintptr_t)a.bias) & 15) == 0;
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    if (pb[nt] < 0) continue;
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt) {
+      const int cb = m0 + mt * 16 + cq;
+      if (cb >= a.Cout) continue;
+      float v[4];
+      if (bvec && cb + 3 < a.Cout) {
+        const float4 bv = *reinterpret_cast<const float4*>(a.bias + cb);
+        v[0] = acc[mt][nt][0] + bv.x;
+        v[1] = acc[mt][nt][1] + bv.y;
+        v[2] = acc[mt][nt][2] + bv.z;
+        v[3] = acc[mt][nt][3] + bv.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
+      }
+      epi_frag<E>(a, v, cb, pp[nt], pb[nt], py[nt], px[nt], HW, vec);
+    }
+  }
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                             const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
+                                             const int (&px)[WN]) {
+  switch (a.epi) {
+#define RS_EPI(E) \
+  case E: epi_loop<WM, WN, E>(a, acc, m0, lane, pp, pb, py, px); break
+    RS_EPI(EPI_FLOW);
+    RS_EPI(EPI_GRU_ZR);
+    RS_EPI(EPI_GRU_Q);
+    RS_EPI(EPI_RELU_BWD);
+    RS_EPI(EPI_ACC_F32);
+    RS_EPI(EPI_GRU_QBWD);
+    RS_EPI(EPI_RELU);
+    RS_EPI(EPI_SCALE);
+#undef RS_EPI
+    default: epi_loop<WM, WN, EPI_BIAS>(a, acc, m0, lane, pp, pb, py, px); break;
+  }
+}
+
+// Linear pixel tiles: the B columns of n-tile nt are pixels n0 + nt*16 + (lane&15).
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int n0,
+                                         int lane, const int (&pb)[WN], const int (&py)[WN],
+                                         const int (&px)[WN]) {
+  int pp[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) pp[nt] = n0 + nt * 16 + (lane & 15);
+  epilogue_pix<WM, WN>(a, acc, m0, lane, pp, pb, py, px);
+}
+
+template <int WM, int WN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_kernel(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int m0 = (blockIdx.y * WAVES_M + wm) * WM * 16;  // first output channel of this wave
+  const int n0 = (blockIdx.x * WAVES_N + wn) * WN * 16;  // first pixel of this wave
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const int taps = a.KH * a.KW;
+  const int HW = a.H * a.W;
+
+  // pixel coordinates of this lane's B columns
+  int pb[WN], py[WN], px[WN];
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    const int p = n0 + nt * 16 + lr;
+    if (p < a.P) {
+      pb[nt] = p / HW;
+      const int q = p - pb[nt] * HW;
+      py[nt] = q / a.W;
+      px[nt] = q - py[nt] * a.W;
+    } else {
+      pb[nt] = -1;
+      py[nt] = px[nt] = 0;
+    }
+  }
+  // weight row pointers of this lane's A rows
+  const bf16_t* wrow[WM];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+    wrow[mt] = a.w + (size_t)(m0 + mt * 16 + lr) * taps * a.Ktot + lk;
+
+  f32x4_t acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // flattened K steps: (segment, tap, 32-channel chunk).  Segment fields are
+  // selected with wave-uniform compares (no dynamic indexing of the kernarg
+  // array, which would go through scratch).
+  const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
+  const int e1 = taps * (s0.C >> 5);
+  const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 5) : 0);
+  const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 5) : 0);
+
+  // plain locals: a lambda capturing the byval kernarg struct by reference
+  // would force a copy of it into scratch.
+  const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+#define RS_CONV_LOAD(STEP, FA, FB)                                                           \
+  do {                                                                                       \
+    const int step_ = (STEP);                                                                \
+    const int si = (step_ >= e1) + (step_ >= e2);                                            \
+    const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);                       \
+    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                 \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                 \
+    const int kseg = si == 0 ? 0 : (si == 1 ? s0.C : s0.C + s1.C);                           \
+    const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                          \
+    const int chunks = sC >> 5;                                                              \
+    const int tap = local / chunks;                                                          \
+    const int c0 = (local - tap * chunks) * 32;                                              \
+    const int dy = tap / KW - PH, dx = tap % KW - PW;                                        \
+    _Pragma("unroll") for (int mt = 0; mt < WM; ++mt)                                        \
+      FA[mt] = ld16(wrow[mt] + (size_t)tap * Ktot + kseg + c0);                              \
+    _Pragma("unroll") for (int nt = 0; nt < WN; ++nt) {                                      \
+      const int yy = py[nt] + dy, xx = px[nt] + dx;                                          \
+      const bool ok = pb[nt] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;                 \
+      FB[nt] = ok ? ld16(sp + ((size_t)(pb[nt] * H + yy) * W + xx) * sst + c0 + lk) : zero;  \
+    }                                                                                        \
+  } while (0)
+
+#define RS_CONV_MMA(FA, FB)                                                                       \
+  _Pragma("unroll") for (int mt = 0; mt < WM; ++mt)                                               \
+    _Pragma("unroll") for (int nt = 0; nt < WN; ++nt)                                             \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                                      \
+          __builtin_bit_cast(bf16x8_t, FA[mt]), __builtin_bit_cast(bf16x8_t, FB[nt]), acc[mt][nt], \
+          0, 0, 0)
+
+  uint4 fa0[WM], fb0[WN], fa1[WM], fb1[WN];
+  RS_CONV_LOAD(0, fa0, fb0);
+  int step = 0;
+  for (; step + 2 <= nsteps; step += 2) {
+    RS_CONV_LOAD(step + 1, fa1, fb1);
+    RS_CONV_MMA(fa0, fb0);
+    if (step + 2 < nsteps) RS_CONV_LOAD(step + 2, fa0, fb0);
+    RS_CONV_MMA(fa1, fb1);
+  }
+  if (step < nsteps) {
+    RS_CONV_MMA(fa0, fb0);
+  }
+#undef RS_CONV_LOAD
+#undef RS_CONV_MMA
+
+  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+}
+
+// staging helpers
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(const void* src, uint4* lds_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)src, (__attribute__((address_space(3))) void*)lds_base, 16,
+      0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, soff,
+                                           0, 0);
+}
+
+}  // namespace conv
+
+// conv_hx.hip: launch one of the pipelined halo tiles 34-39 (grid over Cout tiles x patches)
+void conv_hx_launch(const conv::Args& a, int tile, hipStream_t stream);
+}  // namespace rs

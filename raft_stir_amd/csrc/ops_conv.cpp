@@ -107,7 +107,13 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 33, "conv_fused: tile must be in [0,33]");
+  TORCH_CHECK(tile >= 0 && tile <= 41, "conv_fused: tile must be in [0,41]");
+  if (tile >= 34) {  // pipelined halo tiles: ring depth <= taps, halo within the LDS slot, 16-wide patches
+    const int S = (tile == 35 || tile == 38) ? 3 : 4;
+    const int TH = (tile == 36 || tile == 37) ? 4 : 8, HCAP = (tile == 36 || tile == 37) ? 128 : 192;
+    TORCH_CHECK(KH * KW >= S, "conv_fused: halo tile ", tile, " needs at least ", S, " taps");
+    TORCH_CHECK((TH + KH - 1) * (16 + KW - 1) <= HCAP, "conv_fused: kernel too large for halo tile ", tile);
+  }
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-33) support at most 32 taps");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
   if (tile >= 24 && tile <= 26) {  // halo tiles: the (TH+KH-1) x (16+KW-1) halo must fit the LDS buffer
@@ -117,7 +123,10 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13) || tile == 16 ||
                      tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
-  const int tileM = tile == 0 ? 32
+  const int tileM = (tile == 35 || tile == 37) ? 128
+                    : (tile == 34 || tile == 36 || tile == 38 || tile >= 40) ? 64
+                    : tile == 39 ? 32
+                    : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
                     : (bm128 || bm128w) ? 128 : (tile == 5 ? 16 : 64);

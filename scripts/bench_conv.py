@@ -29,15 +29,36 @@ SHAPES = [
 ]
 
 
+GRAPH = True  # --no-graph: time eager launches (includes host dispatch)
+
+
 def timeit(fn, reps):
+    """GPU time per call.  The reps are captured in one hipGraph so the host
+    dispatch of the op (~10 us of Python + TORCH_CHECKs per call) does not
+    hide the kernel time at small shapes."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            with torch.cuda.graph(g, stream=st):
+                for _ in range(reps):
+                    fn()
+        torch.cuda.current_stream().wait_stream(st)
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        e.record()
+    else:
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) * 1000.0 / reps
 
@@ -52,9 +73,12 @@ def main():
     ap.add_argument("--only", nargs="+", default=None, help="shape names to run")
     ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of one hipGraph")
     ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5],
                     help="wgrad tile variants (csrc/conv_wgrad.hip wgrad_launch)")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = not a.no_graph
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
     _ext.load(raise_on_error=True)
