@@ -6,7 +6,9 @@ TORCH_LIBRARY registration) as host C++ against the installed PyTorch-ROCm
 headers, and everything is linked into one shared object next to this file,
 so it travels with the repository snapshot to the GPU box.
 
-Usage:  python -m raft_stir_amd.build [--force] [--jobs N] [--debug]
+Usage:  python -m raft_stir_amd.build [--force] [--jobs N] [--debug] [--asan]
+(--asan: CPU AddressSanitizer + UBSan build of the host data library,
+``_host_asan.so``, and a run of tests/test_data_cpu.py against it.)
 Incremental: objects are rebuilt when their source, ``common.h`` or the flag
 set changes.
 """
@@ -28,6 +30,7 @@ BUILD = os.path.join(os.path.dirname(PKG), "build", "hip")
 OUT = os.path.join(PKG, "_C.so")
 HOST_CSRC = os.path.join(PKG, "csrc_host")
 HOST_OUT = os.path.join(PKG, "_host.so")
+HOST_ASAN_OUT = os.path.join(PKG, "_host_asan.so")
 ARCH = os.environ.get("RAFT_STIR_ARCH", "gfx950")
 
 
@@ -122,25 +125,33 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
     return OUT
 
 
-def build_host(force: bool = False, debug: bool = False, verbose: bool = False) -> str:
-    """Build the CPU-only data-pipeline library ``_host.so`` (g++, zlib)."""
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=undefined"]
+
+
+def build_host(force: bool = False, debug: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
+    """Build the CPU-only data-pipeline library ``_host.so`` (g++, zlib).
+    ``sanitize``: an AddressSanitizer + UBSan build, ``_host_asan.so`` (host
+    code only; loaded with the sanitizer runtimes preloaded, see run_asan)."""
     inc, lib, abi = _torch_paths()
     srcs = sorted(os.path.join(HOST_CSRC, f) for f in os.listdir(HOST_CSRC) if f.endswith(".cpp"))
     flags = ["-std=c++17", "-fPIC", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-             "-Wno-deprecated-declarations"] + (["-O0", "-g"] if debug else ["-O3"])
+             "-Wno-deprecated-declarations"]
+    flags += SAN_FLAGS if sanitize else (["-O0", "-g"] if debug else ["-O3"])
     flags += [f"-I{p}" for p in inc]
+    out_path = HOST_ASAN_OUT if sanitize else HOST_OUT
     h = hashlib.sha1(json.dumps(flags).encode())
     for s in srcs:
         with open(s, "rb") as f:
             h.update(f.read())
-    stamp = os.path.join(BUILD, "_host.sha1")
+    stamp = os.path.join(BUILD, "_host_asan.sha1" if sanitize else "_host.sha1")
     os.makedirs(BUILD, exist_ok=True)
-    if not force and os.path.exists(HOST_OUT) and os.path.exists(stamp):
+    if not force and os.path.exists(out_path) and os.path.exists(stamp):
         with open(stamp) as f:
             if f.read().strip() == h.hexdigest():
-                return HOST_OUT
+                return out_path
     cxx = shutil.which("g++") or shutil.which("c++")
-    tmp = HOST_OUT + ".tmp"
+    tmp = out_path + ".tmp"
     cmd = [cxx] + flags + srcs + [f"-L{lib}", "-ltorch_cpu", "-lc10", f"-Wl,-rpath,{lib}", "-lz",
                                   "-o", tmp]
     if verbose:
@@ -148,10 +159,34 @@ def build_host(force: bool = False, debug: bool = False, verbose: bool = False) 
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"host build failed\n{res.stdout}\n{res.stderr}")
-    os.replace(tmp, HOST_OUT)
+    os.replace(tmp, out_path)
     with open(stamp, "w") as f:
         f.write(h.hexdigest())
-    return HOST_OUT
+    return out_path
+
+
+def sanitizer_env(lib_path: str) -> dict:
+    """Environment for a python process that loads the sanitized host library:
+    the ASan/UBSan runtimes preloaded (the interpreter itself is not
+    instrumented), leak checking off (CPython's arenas), stop at the first
+    error, and RAFT_STIR_HOST_LIB pointing the loader at ``lib_path``."""
+    cxx = shutil.which("g++") or shutil.which("c++")
+    rt = [subprocess.run([cxx, f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
+          for n in ("libasan.so", "libubsan.so")]
+    env = dict(os.environ)
+    env["LD_PRELOAD"] = ":".join([r for r in rt if os.path.isabs(r)] + ([env["LD_PRELOAD"]] if env.get("LD_PRELOAD") else []))
+    env["ASAN_OPTIONS"] = "detect_leaks=0:halt_on_error=1:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
+    env["RAFT_STIR_HOST_LIB"] = lib_path
+    return env
+
+
+def run_asan(tests=("tests/test_data_cpu.py",), extra=()) -> int:
+    """Build _host_asan.so and run the host-op tests against it (CPU only)."""
+    path = build_host(sanitize=True)
+    root = os.path.dirname(PKG)
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", *tests, *extra]
+    return subprocess.call(cmd, cwd=root, env=sanitizer_env(path))
 
 
 def build_all(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = False):
@@ -164,7 +199,11 @@ def main(argv=None):
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--asan", action="store_true",
+                    help="build the AddressSanitizer+UBSan host library and run the data tests against it")
     a = ap.parse_args(argv)
+    if a.asan:
+        return run_asan()
     print(build_all(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose))
 
 

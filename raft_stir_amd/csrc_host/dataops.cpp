@@ -66,6 +66,7 @@ at::Tensor png_decode(const at::Tensor& data) {
     const uint8_t* body = p + off + 8;
     TORCH_CHECK(off + 12 + int64_t(len) <= n, "png_decode: truncated chunk");
     if (!std::memcmp(type, "IHDR", 4)) {
+      TORCH_CHECK(len >= 13, "png_decode: short IHDR");
       W = be32(body); H = be32(body + 4);
       depth = body[8]; ctype = body[9]; interlace = body[12];
     } else if (!std::memcmp(type, "IDAT", 4)) {
@@ -88,6 +89,9 @@ at::Tensor png_decode(const at::Tensor& data) {
   }
   const int bps = depth / 8;               // bytes per sample
   const int bpp = C * bps;                 // bytes per pixel (filter unit)
+  // untrusted header: bound the allocation (and keep every size in 32 bits for zlib)
+  TORCH_CHECK(W <= (1u << 16) && H <= (1u << 16) && uint64_t(W) * H * bpp + H <= (uint64_t(1) << 31),
+              "png_decode: image ", W, "x", H, " too large");
   const size_t stride = size_t(W) * bpp;
   std::vector<uint8_t> raw((stride + 1) * H);
   z_stream zs{};
@@ -98,7 +102,8 @@ at::Tensor png_decode(const at::Tensor& data) {
   zs.avail_out = uInt(raw.size());
   int zr = inflate(&zs, Z_FINISH);
   inflateEnd(&zs);
-  TORCH_CHECK(zr == Z_STREAM_END || zs.avail_out == 0, "png_decode: corrupt zlib stream");
+  TORCH_CHECK((zr == Z_STREAM_END || zr == Z_OK || zr == Z_BUF_ERROR) && zs.avail_out == 0,
+              "png_decode: corrupt or truncated image data");
   std::vector<uint8_t> img(stride * H);
   for (uint32_t y = 0; y < H; ++y) {
     const uint8_t* src = raw.data() + y * (stride + 1);

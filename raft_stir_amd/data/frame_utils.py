@@ -35,8 +35,8 @@ def _host_ops():
     if _HOST[0] is None:
         try:
             import torch
-            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                "_host.so")
+            path = os.environ.get("RAFT_STIR_HOST_LIB") or os.path.join(
+                os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_host.so")
             if os.path.exists(path) and os.environ.get("RAFT_STIR_NO_HOST") != "1":
                 torch.ops.load_library(path)
                 _HOST[0] = torch.ops.raft_stir_host

@@ -108,6 +108,62 @@ def test_png_decoders_agree_with_pil(tmp_path):
         assert np.array_equal(pyd.astype(np.int64), want.astype(np.int64)), name
 
 
+def _png_bytes(tmp_path):
+    rs = np.random.RandomState(5)
+    im = rs.randint(0, 255, (17, 23, 3)).astype(np.uint8)
+    Image.fromarray(im).save(tmp_path / "x.png")
+    return open(tmp_path / "x.png", "rb").read()
+
+
+def _chunk(typ, body):
+    import struct
+    import zlib
+    return struct.pack(">I", len(body)) + typ + body + struct.pack(">I", zlib.crc32(typ + body) & 0xffffffff)
+
+
+def test_png_corrupt_inputs_raise(tmp_path):
+    """The native decoder parses untrusted files (reference: cv2.imread in
+    core/utils/frame_utils.py:102-107): every malformed input must raise,
+    never read out of bounds or allocate from a bogus header.  The same cases
+    run under AddressSanitizer + UBSan in tests/test_sanitize_cpu.py."""
+    import struct
+    import zlib
+    dec = fu._host_ops().png_decode
+
+    def t(b):  # a fresh torch allocation of exactly len(b) bytes (ASan sees its bounds)
+        return torch.tensor(np.frombuffer(bytes(b), np.uint8)) if len(b) else torch.empty(0, dtype=torch.uint8)
+    good = _png_bytes(tmp_path)
+    assert dec(t(good)).shape == (17, 23, 3)
+    sig = good[:8]
+    ihdr = lambda w, h, d=8, c=2: _chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, d, c, 0, 0, 0))
+    raw = zlib.compress(b"\x00" + b"\x01" * 9)
+    cases = [good[:n] for n in (0, 5, 8, 12, 20, 33, 40, len(good) // 2, len(good) - 13)]
+    cases += [
+        sig + _chunk(b"IHDR", b"\x00\x00\x00\x03"),                          # short IHDR
+        sig + ihdr(1 << 30, 1 << 30) + _chunk(b"IDAT", raw) + _chunk(b"IEND", b""),  # bogus huge size
+        sig + ihdr(70000, 2) + _chunk(b"IDAT", raw) + _chunk(b"IEND", b""),
+        sig + ihdr(3, 1) + _chunk(b"IDAT", b"not zlib at all") + _chunk(b"IEND", b""),
+        sig + ihdr(3, 1) + _chunk(b"IDAT", zlib.compress(b"\x00\x01")) + _chunk(b"IEND", b""),  # short data
+        sig + ihdr(3, 1) + _chunk(b"IDAT", zlib.compress(b"\x07" + b"\x01" * 9)) + _chunk(b"IEND", b""),  # filter 7
+        sig + ihdr(3, 1, d=4) + _chunk(b"IDAT", raw) + _chunk(b"IEND", b""),  # bit depth 4
+        sig + ihdr(3, 1, c=3) + _chunk(b"IDAT", raw) + _chunk(b"IEND", b""),  # palette
+        sig + _chunk(b"IDAT", raw) + _chunk(b"IEND", b""),                      # no IHDR
+        sig + struct.pack(">I", 0xFFFFFFF0) + b"IDAT",                         # chunk length past the end
+    ]
+    for i, c in enumerate(cases):
+        with pytest.raises(RuntimeError):
+            dec(t(c))
+    # a valid file with one flipped byte either decodes or raises -- never crashes
+    rs = np.random.RandomState(0)
+    for _ in range(200):
+        b = bytearray(good)
+        b[rs.randint(8, len(b))] ^= 1 << rs.randint(8)
+        try:
+            dec(t(b))
+        except RuntimeError:
+            pass
+
+
 def test_resize_semantics():
     # half-pixel centres + edge clamp: 2x upsampling of [0, 10] -> [0, 2.5, 7.5, 10]
     x = np.array([[0.0, 10.0]], np.float32)[..., None]
