@@ -962,6 +962,10 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     else hipLaunchKernelGGL((conv::conv_halo_kernel<128, 4, 128>), grid, dim3(256), 0, stream, a);
     return;
   }
+  if (L.tile >= 42 && L.tile <= 47) {  // lean unrolled-tap tiles (conv_v2.hip)
+    conv_v2_launch(a, L.tile, stream);
+    return;
+  }
   if (L.tile >= 34 && L.tile <= 41) {  // pipelined halo tiles (conv_hx.hip)
     conv_hx_launch(a, L.tile, stream);
     return;

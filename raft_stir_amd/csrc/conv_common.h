@@ -446,4 +446,6 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base
 
 // conv_hx.hip: launch one of the pipelined halo tiles 34-39 (grid over Cout tiles x patches)
 void conv_hx_launch(const conv::Args& a, int tile, hipStream_t stream);
+// conv_v2.hip: tiles 42-45 (3x3 / 1x5 / 5x1 only); false if the kernel size is not instantiated
+bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream);
 }  // namespace rs

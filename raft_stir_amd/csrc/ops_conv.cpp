@@ -107,8 +107,11 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 41, "conv_fused: tile must be in [0,41]");
-  if (tile >= 34) {  // pipelined halo tiles: ring depth <= taps, halo within the LDS slot, 16-wide patches
+  TORCH_CHECK(tile >= 0 && tile <= 47, "conv_fused: tile must be in [0,47]");
+  if (tile >= 42)
+    TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
+                "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
+  if (tile >= 34 && tile <= 41) {  // pipelined halo tiles: ring depth <= taps, halo within the LDS slot, 16-wide patches
     const int S = (tile == 35 || tile == 38) ? 3 : 4;
     const int TH = (tile == 36 || tile == 37) ? 4 : 8, HCAP = (tile == 36 || tile == 37) ? 128 : 192;
     TORCH_CHECK(KH * KW >= S, "conv_fused: halo tile ", tile, " needs at least ", S, " taps");
@@ -123,8 +126,9 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
   const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13) || tile == 16 ||
                      tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
-  const int tileM = (tile == 35 || tile == 37) ? 128
-                    : (tile == 34 || tile == 36 || tile == 38 || tile >= 40) ? 64
+  const int tileM = (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
+                    : (tile == 35 || tile == 37) ? 128
+                    : (tile == 34 || tile == 36 || tile == 38 || tile == 40 || tile == 41) ? 64
                     : tile == 39 ? 32
                     : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256

@@ -82,6 +82,30 @@ def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
     return 4 if big else 3
 
 
+# Measured per-call tile table (scripts/tune_conv.py on MI355X): the kernel
+# variant with the lowest graph-timed latency for every conv_fused call of the
+# training step and of inference at the benchmark shapes, keyed by
+# tune_key().  Calls not in the table use the choose_tile heuristic.
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "conv_tuning.json")
+_TUNED: dict | None = None
+_RECORD: list | None = None  # scripts/tune_conv.py: conv_fused calls are appended here
+
+
+def tune_key(B: int, H: int, W: int, cout: int, chans, kh: int, kw: int, epi: int) -> str:
+    return f"{B}x{H}x{W}|{cout}|{','.join(str(int(c)) for c in chans)}|{kh}x{kw}|{epi}"
+
+
+def tuned_tiles() -> dict:
+    global _TUNED
+    if _TUNED is None:
+        _TUNED = {}
+        if os.environ.get("RS_CONV_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+            import json
+            with open(_TUNED_PATH) as f:
+                _TUNED = {k: int(v) for k, v in json.load(f).get("tiles", {}).items()}
+    return _TUNED
+
+
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
                aux2=None, a2off=0, tile=None):
@@ -89,8 +113,14 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
+    if _RECORD is not None:
+        _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
+                            scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile))
     if tile is None:
         t0 = tensors[0]
-        tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans, kh * kw)
+        tile = tuned_tiles().get(tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi))
+        if tile is None:
+            tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans, kh * kw)
     torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                    out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)
