@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--infer-reps", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
+    ap.add_argument("--corr-dtype", default="auto", choices=["auto", "float32", "bfloat16"],
+                    help="all-pairs pyramid storage; auto = bf16 under bf16 autocast (EPE-drift gate: "
+                         "tests/test_model_gpu.py::test_bf16_pyramid_epe_drift)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo ranks on the CPU (plumbing tests; reference-op path)")
     ap.add_argument("--reference-ops", action="store_true",
@@ -64,6 +67,11 @@ def _free_port() -> int:
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def model_cfg_pyr(model) -> str:
+    m = model.module if hasattr(model, "module") else model
+    return "bf16" if str(m.cfg.pyr_dtype).endswith("bfloat16") else "fp32"
 
 
 def launch_ranks(a) -> int:
@@ -104,7 +112,7 @@ def main():
         torch.cuda.set_device(dev)
     torch.manual_seed(1234)
 
-    margs = make_args(small=a.small, mixed_precision=not a.fp32 and not cpu)
+    margs = make_args(small=a.small, mixed_precision=not a.fp32 and not cpu, corr_dtype=a.corr_dtype)
     model = RAFT(margs).to(dev)
     if not cpu:
         model = model.to(memory_format=torch.channels_last)
@@ -168,6 +176,7 @@ def main():
                 "iters": a.iters,
                 "parallelism": f"dp{info.world_size}",
                 "ops": "stock-pytorch (reference semantics)" if (a.reference_ops or cpu) else "hip-kernels",
+                "corr_pyramid": "fp32" if (a.reference_ops or cpu) else str(model_cfg_pyr(model)),
                 "grad_allreduce": ("none" if info.world_size == 1 else
                                    "rccl: packed update-block buffer + DDP encoder buckets"
                                    if getattr(model.__dict__.get("_fused_train"), "grad_group", None)

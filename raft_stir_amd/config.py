@@ -29,7 +29,16 @@ class RAFTConfig:
     fused_gru: bool = True             # fused HIP gate kernels in the ConvGRU
     fused_train: bool = True           # whole-loop fused training engine (full RAFT, bf16)
     overlap_encoders: bool = True      # context encoder on a second HIP stream (GPU)
-    corr_dtype: str = "float32"        # storage dtype of the all-pairs pyramid
+    # storage dtype of the all-pairs pyramid: "float32" (reference, core/corr.py:58),
+    # "bfloat16" (half the volume bytes; needs bf16 autocast features), or "auto"
+    # (bf16 storage exactly when mixed_precision)
+    corr_dtype: str = "float32"
+
+    @property
+    def pyr_dtype(self):
+        import torch
+        bf = self.corr_dtype in ("bfloat16", "bf16") or (self.corr_dtype == "auto" and self.mixed_precision)
+        return torch.bfloat16 if bf else torch.float32
 
     @property
     def corr_planes(self) -> int:
@@ -70,7 +79,7 @@ def resolve_config(args=None, **overrides) -> RAFTConfig:
         fused_gru=bool(_get(args, "fused_gru", True)),
         fused_train=bool(_get(args, "fused_train", True)),
         overlap_encoders=bool(_get(args, "overlap_encoders", os.environ.get("RS_OVERLAP_ENCODERS", "1") != "0")),
-        corr_dtype=str(_get(args, "corr_dtype", "float32")),
+        corr_dtype=str(_get(args, "corr_dtype", os.environ.get("RS_CORR_DTYPE", "float32"))),
         **dims,
     )
     cfg.update(overrides)

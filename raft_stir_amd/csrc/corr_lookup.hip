@@ -30,18 +30,23 @@
 namespace rs {
 namespace lookup {
 
+// Pyramid levels: element (b*N1 + pix, y, x) of level l at p[l] + pix*S[l] + y*W[l] + x
+// (S = row pitch >= H*W).  Pyr elements are fp32 or bf16 (template PT of the
+// forward kernels, RAFTConfig.corr_dtype); the gradient pyramid is fp32.
 struct Pyr {
-  const float* p[4];
+  const void* p[4];
   int H[4];
   int W[4];
+  int S[4];
 };
 struct PyrMut {
   float* p[4];
   int H[4];
   int W[4];
+  int S[4];
 };
 
-template <typename OutT>
+template <typename PT, typename OutT>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(Pyr pyr, int levels,
                                                          const float* __restrict__ coords, int B,
                                                          int H1, int W1, int r,
@@ -68,18 +73,18 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(Pyr pyr, int levels,
     const float fx = x - x0f, fy = y - y0f;
     const int x0 = (int)x0f, y0 = (int)y0f;
     const int H = pyr.H[l], W = pyr.W[l];
-    const float* row = pyr.p[l] + pix * (size_t)H * W;
+    const PT* row = static_cast<const PT*>(pyr.p[l]) + pix * (size_t)pyr.S[l];
     float v = 0.f;
     const bool xin0 = x0 >= 0 && x0 < W, xin1 = x0 + 1 >= 0 && x0 + 1 < W;
     if (y0 >= 0 && y0 < H) {
-      const float* rr = row + (size_t)y0 * W;
-      if (xin0) v += (1.f - fx) * (1.f - fy) * rr[x0];
-      if (xin1) v += fx * (1.f - fy) * rr[x0 + 1];
+      const PT* rr = row + (size_t)y0 * W;
+      if (xin0) v += (1.f - fx) * (1.f - fy) * io<PT>::ld(rr + x0);
+      if (xin1) v += fx * (1.f - fy) * io<PT>::ld(rr + x0 + 1);
     }
     if (y0 + 1 >= 0 && y0 + 1 < H) {
-      const float* rr = row + (size_t)(y0 + 1) * W;
-      if (xin0) v += (1.f - fx) * fy * rr[x0];
-      if (xin1) v += fx * fy * rr[x0 + 1];
+      const PT* rr = row + (size_t)(y0 + 1) * W;
+      if (xin0) v += (1.f - fx) * fy * io<PT>::ld(rr + x0);
+      if (xin1) v += fx * fy * io<PT>::ld(rr + x0 + 1);
     }
     io<OutT>::st(out + idx, v);
   }
@@ -126,7 +131,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrMut gpyr, int levels
         acc += wx * wy * io<GT>::ld(g + i * D + j);
       }
     }
-    float* dst = gpyr.p[l] + pix * (size_t)H * W + (size_t)Y * W + X;
+    float* dst = gpyr.p[l] + pix * (size_t)gpyr.S[l] + (size_t)Y * W + X;
     *dst += acc;
   }
 }
@@ -145,6 +150,10 @@ __device__ __forceinline__ auto lvl_ptr(const P& pyr, int l) {
   return l == 0 ? pyr.p[0] : (l == 1 ? pyr.p[1] : (l == 2 ? pyr.p[2] : pyr.p[3]));
 }
 template <typename P>
+__device__ __forceinline__ int lvl_S(const P& pyr, int l) {
+  return l == 0 ? pyr.S[0] : (l == 1 ? pyr.S[1] : (l == 2 ? pyr.S[2] : pyr.S[3]));
+}
+template <typename P>
 __device__ __forceinline__ int lvl_H(const P& pyr, int l) {
   return l == 0 ? pyr.H[0] : (l == 1 ? pyr.H[1] : (l == 2 ? pyr.H[2] : pyr.H[3]));
 }
@@ -153,7 +162,7 @@ __device__ __forceinline__ int lvl_W(const P& pyr, int l) {
   return l == 0 ? pyr.W[0] : (l == 1 ? pyr.W[1] : (l == 2 ? pyr.W[2] : pyr.W[3]));
 }
 
-template <int R, typename OutT>
+template <int R, typename PT, typename OutT>
 __global__ __launch_bounds__(256) void lookup_fwd_wave_kernel(Pyr pyr, int levels, const float* __restrict__ coords,
                                                               int N1, int P, OutT* __restrict__ out, int ostride) {
   constexpr int D = 2 * R + 1, K2 = D * D, E = D + 1, E2 = E * E;
@@ -174,11 +183,11 @@ __global__ __launch_bounds__(256) void lookup_fwd_wave_kernel(Pyr pyr, int level
     fys[l] = cy - by;
     const int X0 = (int)bx - R, Y0 = (int)by - R;
     const int H = lvl_H(pyr, l), W = lvl_W(pyr, l);
-    const float* row = lvl_ptr(pyr, l) + (size_t)pix * H * W;
+    const PT* row = static_cast<const PT*>(lvl_ptr(pyr, l)) + (size_t)pix * lvl_S(pyr, l);
     for (int idx = lane; idx < E2; idx += 64) {
       const int c = idx / E, a = idx - c * E;
       const int X = X0 + a, Y = Y0 + c;
-      win[w][l][idx] = (X >= 0 && X < W && Y >= 0 && Y < H) ? row[(size_t)Y * W + X] : 0.f;
+      win[w][l][idx] = (X >= 0 && X < W && Y >= 0 && Y < H) ? io<PT>::ld(row + (size_t)Y * W + X) : 0.f;
     }
   }
   // each wave only touches its own LDS slice: a wave-level ordering point suffices
@@ -225,7 +234,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_wave_kernel(PyrMut gpyr, int l
     const float fx = cx - bx, fy = cy - by;
     const int X0 = (int)bx - R, Y0 = (int)by - R;
     const int H = lvl_H(gpyr, l), W = lvl_W(gpyr, l);
-    float* row = lvl_ptr(gpyr, l) + (size_t)pix * H * W;
+    float* row = lvl_ptr(gpyr, l) + (size_t)pix * lvl_S(gpyr, l);
     const float* G = gs[w][l];  // G[i * D + j], i: x tap, j: y tap
     for (int idx = lane; idx < E2; idx += 64) {
       const int c = idx / E, a = idx - c * E;  // cell (x = a, y = c), x fastest
@@ -256,7 +265,8 @@ __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, lon
     const int x = (int)(idx % W0);
     const int y = (int)((idx / W0) % H0);
     const long row = idx / ((long)H0 * W0);
-    float v = g.p[0][idx];
+    const size_t o0 = row * (size_t)g.S[0] + (size_t)y * W0 + x;
+    float v = g.p[0][o0];
     float w = 1.f;
 #pragma unroll
     for (int l = 1; l < 4; ++l) {
@@ -264,12 +274,12 @@ __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, lon
       w *= 0.25f;
       const int yl = y >> l, xl = x >> l;
       if (yl < g.H[l] && xl < g.W[l])
-        v += w * g.p[l][row * (size_t)g.H[l] * g.W[l] + (size_t)yl * g.W[l] + xl];
+        v += w * g.p[l][row * (size_t)g.S[l] + (size_t)yl * g.W[l] + xl];
     }
     if (out_bf16)
-      out_bf16[idx] = f2bf(v * scale);  // GEMM operand for the fmap gradients
+      out_bf16[idx] = f2bf(v * scale);  // GEMM operand for the fmap gradients (compact rows)
     else
-      g.p[0][idx] = v * scale;
+      g.p[0][o0] = v * scale;
   }
 }
 
@@ -281,14 +291,15 @@ inline int grid_for(long total) {
 
 }  // namespace lookup
 
-void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* Ws, int levels,
-                            const float* coords, int B, int H1, int W1, int r, void* out,
+void corr_lookup_fwd_launch(const void* const* pyr, bool pyr_bf16, const int* Hs, const int* Ws, const int* Ss,
+                            int levels, const float* coords, int B, int H1, int W1, int r, void* out,
                             bool out_bf16, hipStream_t stream, int ostride) {
   lookup::Pyr p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? pyr[l] : nullptr;
     p.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = l < levels ? Ws[l] : 0;
+    p.S[l] = l < levels ? Ss[l] : 0;
   }
   const int CH = levels * (2 * r + 1) * (2 * r + 1);
   if (ostride <= 0) ostride = CH;
@@ -297,24 +308,30 @@ void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* W
   const long P = (long)B * H1 * W1;
   if ((r == 3 || r == 4) && P < (1L << 30)) {
     const dim3 g((unsigned)((P + 3) / 4));
-#define RS_LF(R_, T_)                                                                                    \
-  hipLaunchKernelGGL((lookup::lookup_fwd_wave_kernel<R_, T_>), g, dim3(256), 0, stream, p, levels, coords, \
+#define RS_LF(R_, PT_, T_)                                                                                    \
+  hipLaunchKernelGGL((lookup::lookup_fwd_wave_kernel<R_, PT_, T_>), g, dim3(256), 0, stream, p, levels, coords, \
                      H1 * W1, (int)P, static_cast<T_*>(out), ostride)
-    if (r == 3) { if (out_bf16) RS_LF(3, bf16_t); else RS_LF(3, float); }
-    else { if (out_bf16) RS_LF(4, bf16_t); else RS_LF(4, float); }
+#define RS_LF2(R_)                                                              \
+  do {                                                                          \
+    if (pyr_bf16) { if (out_bf16) RS_LF(R_, bf16_t, bf16_t); else RS_LF(R_, bf16_t, float); } \
+    else { if (out_bf16) RS_LF(R_, float, bf16_t); else RS_LF(R_, float, float); } \
+  } while (0)
+    if (r == 3) RS_LF2(3);
+    else RS_LF2(4);
+#undef RS_LF2
 #undef RS_LF
     return;
   }
   const int grid = lookup::grid_for(total);
-  if (out_bf16)
-    hipLaunchKernelGGL(lookup::lookup_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<bf16_t*>(out), total, ostride);
-  else
-    hipLaunchKernelGGL(lookup::lookup_fwd_kernel<float>, dim3(grid), dim3(256), 0, stream, p,
-                       levels, coords, B, H1, W1, r, static_cast<float*>(out), total, ostride);
+#define RS_LG(PT_, T_)                                                                                     \
+  hipLaunchKernelGGL((lookup::lookup_fwd_kernel<PT_, T_>), dim3(grid), dim3(256), 0, stream, p, levels, coords, \
+                     B, H1, W1, r, static_cast<T_*>(out), total, ostride)
+  if (pyr_bf16) { if (out_bf16) RS_LG(bf16_t, bf16_t); else RS_LG(bf16_t, float); }
+  else { if (out_bf16) RS_LG(float, bf16_t); else RS_LG(float, float); }
+#undef RS_LG
 }
 
-void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
+void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride) {
   if (dstride <= 0) dstride = levels * (2 * r + 1) * (2 * r + 1);
@@ -323,6 +340,7 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
     p.p[l] = l < levels ? gpyr[l] : nullptr;
     p.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = l < levels ? Ws[l] : 0;
+    p.S[l] = l < levels ? Ss[l] : 0;
   }
   const long total = (long)B * H1 * W1 * levels * (2 * r + 2) * (2 * r + 2);
   if (total == 0) return;
@@ -346,13 +364,14 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, in
                        levels, coords, B, H1, W1, r, static_cast<const float*>(dout), total, dstride);
 }
 
-void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
+void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
                           float scale, hipStream_t stream, void* out_bf16) {
   lookup::PyrMut p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? gpyr[l] : nullptr;
     p.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = l < levels ? Ws[l] : 0;
+    p.S[l] = l < levels ? Ss[l] : 0;
   }
   const long total = rows * Hs[0] * Ws[0];
   if (total == 0) return;

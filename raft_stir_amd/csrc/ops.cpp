@@ -18,15 +18,15 @@
 
 namespace rs {
 void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1, int H2, int W2,
-                        int C, int levels, float* const* out, const int* Hs, const int* Ws,
-                        float scale, hipStream_t stream);
-void corr_lookup_fwd_launch(const float* const* pyr, const int* Hs, const int* Ws, int levels,
-                            const float* coords, int B, int H1, int W1, int r, void* out,
+                        int C, int levels, void* const* out, const int* Hs, const int* Ws, const int* Ss,
+                        bool out_bf16, void* ws, float scale, hipStream_t stream);
+void corr_lookup_fwd_launch(const void* const* pyr, bool pyr_bf16, const int* Hs, const int* Ws, const int* Ss,
+                            int levels, const float* coords, int B, int H1, int W1, int r, void* out,
                             bool out_bf16, hipStream_t stream, int ostride);
-void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels,
+void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride);
-void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, int levels, long rows,
+void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
                           float scale, hipStream_t stream, void* out_bf16 = nullptr);
 bool corr_otf_supported_channels(int C);
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
@@ -83,7 +83,10 @@ void level_sizes(int H, int W, int levels, int* Hs, int* Ws) {
 }
 
 // ---------------------------------------------------------------- corr volume
-std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t levels, double scale) {
+// Pyramid levels are (B, N1, H_l, W_l) views whose (b, i) rows start at a
+// padded pitch S_l = round_up(H_l*W_l, 64) elements (128-B aligned rows for the
+// flat volume kernel's whole-line stores); fp32, or bf16 when out_bf16.
+std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t levels, double scale, bool out_bf16) {
   check_gpu(f1, "f1");
   check_gpu(f2, "f2");
   check_dtype(f1, {at::kFloat, at::kBFloat16}, "f1");
@@ -98,27 +101,47 @@ std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t leve
   int Hs[4], Ws[4];
   level_sizes(H2, W2, levels, Hs, Ws);
   for (int l = 0; l < levels; ++l) TORCH_CHECK(Hs[l] > 0 && Ws[l] > 0, "pyramid level ", l, " is empty");
+  TORCH_CHECK(!out_bf16 || is_bf16(f1), "corr_volume: a bf16 pyramid needs bf16 feature maps");
   std::vector<Tensor> outs;
-  float* ptrs[4];
+  void* ptrs[4];
+  int Ss[4];
+  const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;
   for (int l = 0; l < levels; ++l) {
-    outs.push_back(at::empty({B, N1, Hs[l], Ws[l]}, f1.options().dtype(at::kFloat)));
-    ptrs[l] = outs.back().data_ptr<float>();
+    Ss[l] = (Hs[l] * Ws[l] + 63) / 64 * 64;
+    Tensor store = at::empty({(int64_t)B * N1 * Ss[l]}, f1.options().dtype(odt));
+    outs.push_back(store.as_strided({B, N1, Hs[l], Ws[l]}, {(int64_t)N1 * Ss[l], Ss[l], Ws[l], 1}));
+    ptrs[l] = store.data_ptr();
+  }
+  Tensor ws;
+  if (is_bf16(f1) && levels > 1) {
+    int64_t n = 0;
+    for (int l = 1; l < levels; ++l) n += (int64_t)B * Hs[l] * Ws[l] * C;
+    ws = at::empty({n}, f1.options());
   }
   rs::corr_volume_launch(f1.data_ptr(), f2.data_ptr(), is_bf16(f1), B, N1, H2, W2, C, levels, ptrs,
-                         Hs, Ws, (float)scale, cur_stream());
+                         Hs, Ws, Ss, out_bf16, ws.defined() ? ws.data_ptr() : nullptr, (float)scale, cur_stream());
   RS_CHECK_LAUNCH();
   return outs;
 }
 
-void check_pyr(const std::vector<Tensor>& pyr, int B, int N1, int* Hs, int* Ws) {
+// Pyramid level l: (B, N1, H_l, W_l) with unit x stride, row stride W_l and a
+// (b, i) row pitch S_l >= H_l*W_l (corr_volume pads it; plain contiguous tensors
+// have S_l = H_l*W_l).  Every level one dtype: fp32 (gradients: always) or bf16.
+void check_pyr(const std::vector<Tensor>& pyr, int B, int N1, int* Hs, int* Ws, int* Ss, bool allow_bf16 = false) {
   TORCH_CHECK(!pyr.empty() && pyr.size() <= 4, "pyramid must have 1..4 levels");
   for (size_t l = 0; l < pyr.size(); ++l) {
-    check_gpu(pyr[l], "pyramid level");
-    check_dtype(pyr[l], {at::kFloat}, "pyramid level");
+    TORCH_CHECK(pyr[l].is_cuda(), "pyramid level must be a GPU tensor");  // rows may be padded (strides below)
+    if (allow_bf16) check_dtype(pyr[l], {at::kFloat, at::kBFloat16}, "pyramid level");
+    else check_dtype(pyr[l], {at::kFloat}, "pyramid level");
+    TORCH_CHECK(pyr[l].scalar_type() == pyr[0].scalar_type(), "pyramid levels must share one dtype");
     TORCH_CHECK(pyr[l].dim() == 4 && pyr[l].size(0) == B && pyr[l].size(1) == N1,
                 "pyramid level ", l, " must be (B, H1*W1, H_l, W_l)");
     Hs[l] = pyr[l].size(2);
     Ws[l] = pyr[l].size(3);
+    Ss[l] = pyr[l].stride(1);
+    TORCH_CHECK(pyr[l].stride(3) == 1 && pyr[l].stride(2) == Ws[l] && Ss[l] >= Hs[l] * Ws[l] &&
+                    pyr[l].stride(0) == (int64_t)N1 * Ss[l],
+                "pyramid level ", l, ": rows must be dense (pitch >= H*W)");
   }
 }
 
@@ -133,18 +156,18 @@ Tensor corr_lookup(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t
                    bool out_bf16) {
   check_coords(coords);
   const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
-  int Hs[4], Ws[4];
-  check_pyr(pyr, B, H1 * W1, Hs, Ws);
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(pyr, B, H1 * W1, Hs, Ws, Ss, true);
   TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
   const c10::DeviceGuard guard(coords.device());
   const int levels = pyr.size();
   const int D = 2 * radius + 1;
   Tensor out = at::empty({B, H1, W1, levels * D * D},
                          coords.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
-  const float* ptrs[4];
-  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
-  rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
-                             out.data_ptr(), out_bf16, cur_stream(), 0);
+  const void* ptrs[4];
+  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr();
+  rs::corr_lookup_fwd_launch(ptrs, is_bf16(pyr[0]), Hs, Ws, Ss, levels, coords.data_ptr<float>(), B, H1, W1,
+                             radius, out.data_ptr(), out_bf16, cur_stream(), 0);
   RS_CHECK_LAUNCH();
   return out;
 }
@@ -155,8 +178,8 @@ void corr_lookup_into(const std::vector<Tensor>& pyr, const Tensor& coords, int6
                       const Tensor& out) {
   check_coords(coords);
   const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
-  int Hs[4], Ws[4];
-  check_pyr(pyr, B, H1 * W1, Hs, Ws);
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(pyr, B, H1 * W1, Hs, Ws, Ss, true);
   TORCH_CHECK(radius >= 0 && radius <= 4, "radius must be in [0,4]");
   const int levels = pyr.size();
   const int D = 2 * radius + 1;
@@ -166,10 +189,10 @@ void corr_lookup_into(const std::vector<Tensor>& pyr, const Tensor& coords, int6
                   out.size(3) >= levels * D * D,
               "out must be (B,H1,W1,>=levels*(2r+1)^2)");
   const c10::DeviceGuard guard(coords.device());
-  const float* ptrs[4];
-  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr<float>();
-  rs::corr_lookup_fwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
-                             out.data_ptr(), is_bf16(out), cur_stream(), out.size(3));
+  const void* ptrs[4];
+  for (int l = 0; l < levels; ++l) ptrs[l] = pyr[l].data_ptr();
+  rs::corr_lookup_fwd_launch(ptrs, is_bf16(pyr[0]), Hs, Ws, Ss, levels, coords.data_ptr<float>(), B, H1, W1,
+                             radius, out.data_ptr(), is_bf16(out), cur_stream(), out.size(3));
   RS_CHECK_LAUNCH();
 }
 
@@ -177,8 +200,8 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
                           const Tensor& dout) {
   check_coords(coords);
   const int B = coords.size(0), H1 = coords.size(2), W1 = coords.size(3);
-  int Hs[4], Ws[4];
-  check_pyr(gpyr, B, H1 * W1, Hs, Ws);
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(gpyr, B, H1 * W1, Hs, Ws, Ss);
   const int levels = gpyr.size();
   const int D = 2 * radius + 1;
   check_gpu(dout, "dout");
@@ -189,7 +212,7 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
   const c10::DeviceGuard guard(coords.device());
   float* ptrs[4];
   for (int l = 0; l < levels; ++l) ptrs[l] = gpyr[l].data_ptr<float>();
-  rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, levels, coords.data_ptr<float>(), B, H1, W1, radius,
+  rs::corr_lookup_bwd_launch(ptrs, Hs, Ws, Ss, levels, coords.data_ptr<float>(), B, H1, W1, radius,
                              dout.data_ptr(), is_bf16(dout), cur_stream(), dout.size(3));
   RS_CHECK_LAUNCH();
 }
@@ -197,12 +220,12 @@ void corr_lookup_backward(const std::vector<Tensor>& gpyr, const Tensor& coords,
 void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
   TORCH_CHECK(!gpyr.empty() && gpyr.size() <= 4, "pyramid must have 1..4 levels");
   const int B = gpyr[0].size(0), N1 = gpyr[0].size(1);
-  int Hs[4], Ws[4];
-  check_pyr(gpyr, B, N1, Hs, Ws);
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(gpyr, B, N1, Hs, Ws, Ss);
   const c10::DeviceGuard guard(gpyr[0].device());
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
-  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -211,15 +234,15 @@ void pyr_grad_fold(const std::vector<Tensor>& gpyr, double scale) {
 void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Tensor& out) {
   TORCH_CHECK(!gpyr.empty() && gpyr.size() <= 4, "pyramid must have 1..4 levels");
   const int B = gpyr[0].size(0), N1 = gpyr[0].size(1);
-  int Hs[4], Ws[4];
-  check_pyr(gpyr, B, N1, Hs, Ws);
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(gpyr, B, N1, Hs, Ws, Ss);
   check_gpu(out, "out");
   check_dtype(out, {at::kBFloat16}, "out");
   TORCH_CHECK(out.is_contiguous() && out.numel() == gpyr[0].numel(), "pyr_grad_fold_bf16: out shape");
   const c10::DeviceGuard guard(gpyr[0].device());
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
-  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), out.data_ptr());
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), out.data_ptr());
   RS_CHECK_LAUNCH();
 }
 
@@ -447,7 +470,7 @@ std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Ten
 }  // namespace
 
 TORCH_LIBRARY(raft_stir, m) {
-  m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale) -> Tensor[]");
+  m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale, bool out_bf16=False) -> Tensor[]");
   m.def("corr_lookup(Tensor[] pyr, Tensor coords, int radius, bool out_bf16) -> Tensor");
   m.def("corr_lookup_into(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_lookup_backward(Tensor(a!)[] gpyr, Tensor coords, int radius, Tensor dout) -> ()");

@@ -15,8 +15,9 @@ from ..ops import reference as ref
 
 
 class CorrBlock(AllPairsCorr):
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32):
-        super().__init__(fmap1, fmap2, num_levels=num_levels, radius=radius, out_dtype=out_dtype)
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32, pyr_dtype=torch.float32):
+        super().__init__(fmap1, fmap2, num_levels=num_levels, radius=radius, out_dtype=out_dtype,
+                         pyr_dtype=pyr_dtype)
 
     @staticmethod
     def corr(fmap1, fmap2):

@@ -405,7 +405,7 @@ class FusedTrainLoop(torch.autograd.Function):
         side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
         lside = eng.side_stream(dev, 0) if ctx.defer else None
         if st.gpyr is None:
-            st.gpyr = [torch.zeros_like(p) for p in st.pyr]
+            st.gpyr = st.zero_grads()
         G = S["G"]
         G.zero_()
         inpb = S["inp"]

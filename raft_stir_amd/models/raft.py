@@ -177,8 +177,9 @@ class RAFT(nn.Module):
                 fmap1, fmap2 = fmap1.float(), fmap2.float()
             corr_dtype = torch.bfloat16 if mixed else torch.float32
             block = AlternateCorrBlock if self.cfg.alternate_corr else CorrBlock
+            kw = {} if self.cfg.alternate_corr else dict(pyr_dtype=self.cfg.pyr_dtype)
             corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
-                            radius=self.cfg.corr_radius, out_dtype=corr_dtype)
+                            radius=self.cfg.corr_radius, out_dtype=corr_dtype, **kw)
 
             if side is None:
                 cnet = self.cnet(image1)

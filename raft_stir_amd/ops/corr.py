@@ -32,15 +32,20 @@ from . import reference as ref
 
 
 class CorrState:
-    __slots__ = ("pyr", "gpyr", "levels", "radius", "scale", "shape")
+    __slots__ = ("pyr", "gpyr", "levels", "radius", "scale", "shape", "pyr_bf16")
 
-    def __init__(self, levels: int, radius: int):
+    def __init__(self, levels: int, radius: int, pyr_bf16: bool = False):
         self.pyr: Optional[List[torch.Tensor]] = None
         self.gpyr: Optional[List[torch.Tensor]] = None
         self.levels = levels
         self.radius = radius
         self.scale = 1.0
         self.shape = None
+        self.pyr_bf16 = pyr_bf16  # bf16 pyramid storage (RAFTConfig.corr_dtype)
+
+    def zero_grads(self) -> List[torch.Tensor]:
+        """Dense fp32 gradient pyramid (contiguous rows), whatever the storage of pyr."""
+        return [torch.zeros(p.shape, device=p.device, dtype=torch.float32) for p in self.pyr]
 
 
 def to_nhwc(x: torch.Tensor) -> torch.Tensor:
@@ -58,7 +63,8 @@ class _CorrVolume(torch.autograd.Function):
     def forward(ctx, f1, f2, state: CorrState):
         # f1: (B,N1,C), f2: (B,H2,W2,C) contiguous, fp32 or bf16
         state.scale = 1.0 / math.sqrt(f1.shape[-1])
-        state.pyr = list(torch.ops.raft_stir.corr_volume(f1, f2, state.levels, state.scale))
+        bf16 = state.pyr_bf16 and f1.dtype == torch.bfloat16
+        state.pyr = list(torch.ops.raft_stir.corr_volume(f1, f2, state.levels, state.scale, bf16))
         state.shape = (f1.shape, f2.shape)
         ctx.state = state
         ctx.save_for_backward(f1, f2)
@@ -101,7 +107,7 @@ class _CorrLookup(torch.autograd.Function):
         state: CorrState = ctx.state
         (coords,) = ctx.saved_tensors
         if state.gpyr is None:
-            state.gpyr = [torch.zeros_like(p) for p in state.pyr]
+            state.gpyr = state.zero_grads()
         torch.ops.raft_stir.corr_lookup_backward(state.gpyr, coords, state.radius,
                                                  dout.contiguous())
         return coords.new_zeros(()), None, None, None
@@ -115,7 +121,7 @@ class AllPairsCorr:
     view in ``out_dtype``.
     """
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, out_dtype=torch.float32, pyr_dtype=torch.float32):
         self.num_levels = num_levels
         self.radius = radius
         self.out_dtype = out_dtype
@@ -126,7 +132,8 @@ class AllPairsCorr:
             f2 = to_nhwc(fmap2.to(f1.dtype))
             if f1.dtype not in (torch.float32, torch.bfloat16):
                 f1, f2 = f1.float(), f2.float()
-            self.state = CorrState(num_levels, radius)
+            # bf16 pyramid storage needs bf16 feature maps (autocast); fp32 otherwise
+            self.state = CorrState(num_levels, radius, pyr_bf16=pyr_dtype == torch.bfloat16)
             self.token = _CorrVolume.apply(f1.view(B, H * W, C), f2, self.state)
         else:
             self.pyramid = ref.corr_pyramid(fmap1, fmap2, num_levels)

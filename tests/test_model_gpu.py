@@ -51,6 +51,28 @@ def test_bf16_inference_close_to_fp32(cuda):
     assert err < 2.0 * err_ref + 1e-2, (err, err_ref)
 
 
+def test_bf16_pyramid_epe_drift(cuda):
+    """EPE-drift gate for bf16 pyramid storage (RAFTConfig.corr_dtype,
+    SURVEY 7.3-1): at 12 iterations the bf16-pyramid engine must stay as close
+    to the fp32 model as the fp32-pyramid bf16 engine does (+ a small margin)."""
+    from raft_stir_amd.data.synthetic import make_batch
+    torch.manual_seed(0)
+    m32 = RAFT(make_args()).to(cuda).to(memory_format=torch.channels_last).eval()
+    mix = copy.deepcopy(m32)
+    mix.cfg = mix.cfg.__class__(**{**mix.cfg.to_dict(), "mixed_precision": True})
+    mbp = copy.deepcopy(mix)
+    mbp.cfg = mbp.cfg.__class__(**{**mbp.cfg.to_dict(), "corr_dtype": "bfloat16"})
+    i1, i2, _, _ = make_batch(1, 192, 256, seed=11, device=cuda)
+    with torch.no_grad():
+        _, a = m32(i1, i2, iters=12, test_mode=True)
+        _, b = mix(i1, i2, iters=12, test_mode=True)
+        _, c = mbp(i1, i2, iters=12, test_mode=True)
+    e_mix = (a - b).norm(dim=1).mean().item()
+    e_bp = (a - c).norm(dim=1).mean().item()
+    print(f"EPE vs fp32: bf16 engine {e_mix:.4f}, + bf16 pyramid {e_bp:.4f}")
+    assert e_bp <= 1.25 * e_mix + 0.02, (e_bp, e_mix)
+
+
 @pytest.mark.parametrize("small", [False, True])
 def test_training_grads_match_cpu(cuda, small):
     torch.manual_seed(0)
