@@ -133,6 +133,25 @@ class _Encoder(nn.Module):
                 if m.bias is not None:
                     nn.init.constant_(m.bias, 0)
 
+    def stage_fns(self):
+        """The forward as a list of callables: stem, each residual block, head.
+        RAFT.forward runs two encoders stage-by-stage in lockstep on two HIP
+        streams, so the HOST issues both chains interleaved -- and, because
+        autograd replays nodes by creation order, so does the backward (a
+        whole encoder issued first left the other stream idle for its ~2 ms
+        of host issue time, profiles/r2/train_streams.md)."""
+        fns = [lambda x: conv_norm_act(self.conv1, self.norm1, x)]
+        for layer in (self.layer1, self.layer2, self.layer3):
+            fns.extend(layer)
+
+        def head(x):
+            x = conv_module(self.conv2, x)
+            if self.training and self.dropout is not None:
+                x = self.dropout(x)
+            return x
+        fns.append(head)
+        return fns
+
     def forward(self, x):
         pair = isinstance(x, (list, tuple))
         if pair:

@@ -25,6 +25,8 @@ Engine differences (outputs unchanged):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -107,7 +109,10 @@ class RAFT(nn.Module):
         """slot 0: context encoder / flow branch; slot 1: deferred weight gradients."""
         st = _SIDE_STREAMS.get((dev.index, slot))
         if st is None:
-            st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev)
+            # RS_SIDE_PRIO: priority of the context-encoder / flow-branch stream
+            # (lower = more urgent; the deferred weight-gradient stream keeps the default)
+            prio = int(os.environ.get("RS_SIDE_PRIO", "0")) if slot == 0 else 0
+            st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev, priority=prio)
         return st
 
     def freeze_bn(self):
@@ -165,10 +170,21 @@ class RAFT(nn.Module):
             side.wait_stream(main)
         with self._autocast(dev):
             if side is not None:
-                with torch.cuda.stream(side):
-                    cnet = self.cnet(image1)
+                # fnet (main) and cnet (side) stage by stage, interleaved on the host
+                xf = torch.cat([image1, image2], dim=0)
+                xc = image1
+                ff, fc = self.fnet.stage_fns(), self.cnet.stage_fns()
+                for k in range(max(len(ff), len(fc))):
+                    if k < len(ff):
+                        xf = ff[k](xf)
+                    if k < len(fc):
+                        with torch.cuda.stream(side):
+                            xc = fc[k](xc)
+                cnet = xc
                 image1.record_stream(side)  # main-stream block read on side (kept by cnet's backward)
-            fmap1, fmap2 = self.fnet([image1, image2])
+                fmap1, fmap2 = torch.split(xf, [image1.shape[0], image2.shape[0]], dim=0)
+            else:
+                fmap1, fmap2 = self.fnet([image1, image2])
             # The reference casts the features to fp32 (core/raft.py:102-103).
             # Under bf16 autocast they are exactly representable in bf16, so the
             # MFMA volume kernel consumes them in bf16 with fp32 accumulation

@@ -73,3 +73,64 @@ class GraphCache:
             self.pool = g.graph.pool()
             self.graphs[key] = g
         return g(image1, image2, flow_init)
+
+
+class GraphedTrainStep:
+    """hipGraph capture of a WHOLE training step (reference train.py:162-183):
+    forward (encoders, correlation volume, the 12-iteration fused loop on
+    its HIP streams), sequence loss, backward, gradient clipping and the
+    AdamW update, replayed with one host call.
+
+    The eager step costs ~12 ms of host time (Python + ~950 kernel launches)
+    against ~20 ms of GPU work, so the host -- not the GPU -- bounds the step
+    as soon as the kernels get faster (scripts/host_overhead.py).  The
+    standard whole-network capture recipe is used: warm up on a side stream,
+    capture with the gradients set to None (the captured backward then
+    WRITES, not accumulates, the .grad tensors on every replay), static
+    input buffers, and an optimizer built with ``capturable=True`` and a
+    device learning-rate tensor that the (uncaptured) LR scheduler updates
+    in place between replays.
+
+    ``step(batch)`` copies the batch into the static buffers, replays and
+    returns the static loss tensor (valid until the next replay).
+    """
+
+    def __init__(self, model, optimizer, loss_fn, sample_batch, clip=1.0, warmup=3, iters=12):
+        self.model = model
+        self.optimizer = optimizer
+        self.loss_fn = loss_fn
+        self.clip = clip
+        self.iters = iters
+        for g in optimizer.param_groups:
+            if not isinstance(g["lr"], torch.Tensor) or not g.get("capturable", False):
+                raise ValueError("GraphedTrainStep needs an optimizer with capturable=True and a tensor lr")
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.static = [t.clone() for t in sample_batch]
+        dev = self.static[0].device
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                optimizer.zero_grad(set_to_none=True)
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        optimizer.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = self._body()
+
+    def _body(self):
+        i1, i2, flow, valid = self.static
+        preds = self.model(i1, i2, iters=self.iters)
+        loss = self.loss_fn(preds, flow, valid)
+        loss.backward()
+        if self.clip and self.clip > 0:
+            torch.nn.utils.clip_grad_norm_(self.params, self.clip)
+        self.optimizer.step()
+        return loss.detach()
+
+    def step(self, batch):
+        for dst, src in zip(self.static, batch):
+            dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.loss

@@ -11,11 +11,16 @@ import torch
 import torch.optim as optim
 
 
-def fetch_optimizer(args, model, fused=None):
+def fetch_optimizer(args, model, fused=None, capturable=False):
+    """``capturable``: the learning rate lives in a device tensor (updated in
+    place by the scheduler) and the update reads no host state, so the whole
+    step can be replayed from a hipGraph (runtime/graph.py GraphedTrainStep)."""
     params = [p for p in model.parameters() if p.requires_grad]
     if fused is None:
         fused = bool(params) and params[0].is_cuda
     kw = dict(lr=args.lr, weight_decay=args.wdecay, eps=args.epsilon)
+    if capturable:
+        kw.update(lr=torch.tensor(float(args.lr), device=params[0].device), capturable=True)
     try:
         optimizer = optim.AdamW(params, fused=fused, **kw)
     except (RuntimeError, TypeError):

@@ -1,0 +1,60 @@
+#!/usr/bin/env python
+"""Stream-level summary of one training step from a rocprofv3 kernel trace:
+per-queue busy time, GPU-idle time, and the main-queue gaps (what the other
+queues run while the main stream waits).
+
+    python scripts/trace_streams.py gpurun_out/trace/train_kernel_trace.csv.gz
+"""
+import collections
+import csv
+import gzip
+import sys
+
+
+def main(path):
+    op = gzip.open if path.endswith(".gz") else open
+    rows = list(csv.DictReader(op(path, "rt")))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"]]
+    groups = []
+    for i in idx:
+        if groups and i - groups[-1][-1] <= 2:
+            groups[-1].append(i)
+        else:
+            groups.append([i])
+    s0, s1 = groups[-2][-1] + 1, groups[-1][-1] + 1
+    step = rows[s0:s1]
+    T = lambda r: (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+    t0 = min(T(r)[0] for r in step)
+    t1 = max(T(r)[1] for r in step)
+    byq, cnt = collections.defaultdict(float), collections.Counter()
+    for r in step:
+        s, e = T(r)
+        byq[r["Queue_Id"]] += (e - s) / 1e6
+        cnt[r["Queue_Id"]] += 1
+    iv = sorted(T(r) for r in step)
+    busy, (cs, ce) = 0, iv[0]
+    for s, e in iv[1:]:
+        if s > ce:
+            busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    busy += ce - cs
+    print(f"step {(t1 - t0) / 1e6:.3f} ms, {len(step)} kernels, GPU busy {busy / 1e6:.3f} ms, idle {(t1 - t0 - busy) / 1e6:.3f} ms")
+    for q in sorted(byq):
+        print(f"  queue {q}: {cnt[q]} kernels, {byq[q]:.3f} ms busy")
+    main = max(byq, key=byq.get)
+    mq = [r for r in step if r["Queue_Id"] == main]
+    gaps = []
+    for a, b in zip(mq, mq[1:]):
+        g = T(b)[0] - T(a)[1]
+        if g > 100000:
+            gaps.append(((T(a)[1] - t0) / 1e6, g / 1e6, b["Kernel_Name"][:60]))
+    print(f"main-queue gaps > 100 us: {len(gaps)}, {sum(g[1] for g in gaps):.3f} ms")
+    for g in gaps:
+        print(f"  at {g[0]:7.3f} ms: {g[1]:6.3f} ms idle, then {g[2]}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
