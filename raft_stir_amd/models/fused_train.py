@@ -278,15 +278,27 @@ class FusedTrainEngine:
     @staticmethod
     def config_capable(cfg) -> bool:
         """The configuration half of ``eligible`` (no tensors needed)."""
-        return (bool(cfg.mixed_precision) and cfg.fused_gru and not cfg.small and not cfg.alternate_corr
+        return (bool(cfg.mixed_precision) and cfg.fused_gru and not cfg.small
                 and getattr(cfg, "fused_train", True))
 
     @staticmethod
     def eligible(model, image, corr_fn) -> bool:
+        corr_ok = getattr(corr_fn, "state", None) is not None or (  # all-pairs pyramid, or on-the-fly
+            getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == 4
+            and corr_fn.f1.dtype == torch.bfloat16)
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
                 and FusedTrainEngine.config_capable(model.cfg)
-                and getattr(corr_fn, "hip", False) and getattr(corr_fn, "state", None) is not None
+                and getattr(corr_fn, "hip", False) and corr_ok
                 and _ext.use_hip(image))
+
+    @staticmethod
+    def corr_inputs(corr_fn):
+        """(corr_state, token, otf tensors) for FusedTrainLoop.apply: the all-pairs
+        pyramid state + its volume token, or the on-the-fly correlation's f1 and
+        pooled f2 levels (their gradients are returned by the loop itself)."""
+        if getattr(corr_fn, "state", None) is not None:
+            return corr_fn.state, corr_fn.token, ()
+        return None, None, (corr_fn.f1, *corr_fn.f2s)
 
     def buffers(self, B, H, W, iters, dev):
         key = (B, H, W, iters, dev)
@@ -333,8 +345,15 @@ class DeferGrads(torch.autograd.Function):
 
 
 class FusedTrainLoop(torch.autograd.Function):
+    """``otf``: None (all-pairs pyramid in corr_state) or (radius, scale, n_levels):
+    the first n_levels + 1 of ``tensors`` are the on-the-fly correlation's f1 and
+    pooled f2 levels (reference AlternateCorrBlock, core/corr.py:63-91, here also
+    differentiable: SURVEY B1); the rest are the update-block parameters."""
+
     @staticmethod
-    def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, defer, *params):
+    def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, defer, otf, *tensors):
+        nt = 0 if otf is None else otf[2] + 1
+        otf_t, params = tensors[:nt], tensors[nt:]
         B, _, H, W = coords1.shape
         dev = coords1.device
         eng.pack(dev)
@@ -347,6 +366,8 @@ class FusedTrainLoop(torch.autograd.Function):
         sl(C, 0).copy_(coords1.detach())
         c0 = coords0.detach().float().contiguous()
         inpb = S["inp"]
+        if otf is not None:
+            S["corr"][..., otf[2] * 81:].zero_()  # K padding of the correlation slot (lookup_into zeroes its own)
         # flow branch (flow encoder + convf2) on the second HIP stream, parallel
         # to lookup + convc1 + convc2; disjoint channels of `mot`, joined before
         # the conv that reads it
@@ -359,7 +380,11 @@ class FusedTrainLoop(torch.autograd.Function):
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 R.flow_encode(coords, f1w, f1b, sl(S["f1"], i), 0, hx, 254)
                 conv_fused([(sl(S["f1"], i), 0, 128)], eng.f2.w, eng.f2.b, 3, 3, 64, EPI_RELU, sl(S["mot"], i), 192)
-            R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+            if otf is None:
+                R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+            else:
+                cf = R.corr_otf(otf_t[0], list(otf_t[1:]), coords, otf[0], otf[1], True)
+                sl(S["corr"], i)[..., :cf.shape[-1]].copy_(cf)
             conv_fused([(sl(S["corr"], i), 0, CORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, 256, EPI_RELU, sl(S["c1"], i))
             conv_fused([(sl(S["c1"], i), 0, 256)], eng.c2.w, eng.c2.b, 3, 3, 192, EPI_RELU, sl(S["mot"], i), 0)
             if side is not None:
@@ -386,6 +411,9 @@ class FusedTrainLoop(torch.autograd.Function):
         flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
         up = R.convex_upsample(flows, S["mask"])
         ctx.eng, ctx.state, ctx.S, ctx.iters = eng, corr_state, S, iters
+        ctx.otf = otf
+        if otf is not None:
+            ctx.save_for_backward(*otf_t)
         ctx.defer = bool(defer) and eng.side_stream(dev) is not None
         ctx.c0 = c0
         ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
@@ -404,8 +432,13 @@ class FusedTrainLoop(torch.autograd.Function):
         # (joined by DeferGrads.backward); else convf2 dgrad on the side stream
         side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
         lside = eng.side_stream(dev, 0) if ctx.defer else None
-        if st.gpyr is None:
-            st.gpyr = st.zero_grads()
+        otf = ctx.otf
+        if otf is None:
+            if st.gpyr is None:
+                st.gpyr = st.zero_grads()
+        else:
+            otf_t = ctx.saved_tensors
+            d_otf = None  # fp32 sums over the iterations: [df1, df2_0 .. df2_{L-1}]
         G = S["G"]
         G.zero_()
         inpb = S["inp"]
@@ -449,9 +482,22 @@ class FusedTrainLoop(torch.autograd.Function):
             if lside is not None:
                 lside.wait_stream(main)
             with torch.cuda.stream(lside) if lside is not None else contextlib.nullcontext():
-                R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+                if otf is None:
+                    R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+                else:
+                    ch = otf[2] * 81
+                    gi = R.corr_otf_backward(otf_t[0], list(otf_t[1:]), sl(C, i), otf[0], otf[1],
+                                             dcorr[..., :ch].contiguous())
+                    if d_otf is None:
+                        d_otf = list(gi)
+                    else:
+                        for acc, g in zip(d_otf, gi):
+                            acc.add_(g)
         if lside is not None:
             main.wait_stream(lside)
+            if otf is not None:
+                for g in d_otf:
+                    g.record_stream(main)
         d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
         d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
@@ -474,8 +520,12 @@ class FusedTrainLoop(torch.autograd.Function):
         if ctx.defer:
             for gr in grads:
                 gr.record_stream(main)
-        token_grad = torch.zeros((), device=dev)
-        return (None, None, token_grad, d_net, d_inp, None, None, None, None, *grads)
+        if otf is None:
+            token_grad, otf_grads = torch.zeros((), device=dev), ()
+        else:
+            token_grad = None
+            otf_grads = tuple(g.to(t.dtype) for g, t in zip(d_otf, otf_t))
+        return (None, None, token_grad, d_net, d_inp, None, None, None, None, None, *otf_grads, *grads)
 
     @staticmethod
     def _wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):

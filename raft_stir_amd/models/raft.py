@@ -212,8 +212,10 @@ class RAFT(nn.Module):
 
             if not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn):
                 eng = self._train_engine()
-                up = FusedTrainLoop.apply(eng, corr_fn.state, corr_fn.token, net, inp, coords0, coords1,
-                                          iters, dparams is not None,
+                cstate, ctoken, otf_t = FusedTrainEngine.corr_inputs(corr_fn)
+                otf = None if not otf_t else (corr_fn.radius, corr_fn.scale, len(otf_t) - 1)
+                up = FusedTrainLoop.apply(eng, cstate, ctoken, net, inp, coords0, coords1,
+                                          iters, dparams is not None, otf, *otf_t,
                                           *(dparams if dparams is not None else eng.params))
                 # consecutive views of one tensor: the fused loss reads it whole
                 return list(up.view(iters, *coords1.shape[:1], *up.shape[1:]).unbind(0))

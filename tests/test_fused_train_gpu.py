@@ -128,6 +128,42 @@ def test_fused_training_matches_module_graph(cuda):
     assert not bad, bad
 
 
+def test_fused_training_onthefly_corr_matches_module_graph(cuda):
+    """--alternate_corr training through the fused engine (on-the-fly
+    correlation forward + atomic backward per iteration, gradients returned to
+    f1 / the pooled f2 levels) vs the module graph with the same correlation."""
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.models.fused_train import FusedTrainEngine
+    from raft_stir_amd.train.loss import sequence_loss
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True, alternate_corr=True)).to(cuda).to(memory_format=torch.channels_last)
+    m.train()
+    ref = copy.deepcopy(m)
+    ref.cfg = ref.cfg.__class__(**{**ref.cfg.to_dict(), "fused_train": False})
+    i1, i2, flow, valid = make_batch(2, 192, 256, seed=4, device=cuda)
+    res = {}
+    calls = []
+    orig = FusedTrainEngine.eligible
+    FusedTrainEngine.eligible = staticmethod(lambda *a: calls.append(orig(*a)) or calls[-1])
+    try:
+        for name, net in (("fused", m), ("ref", ref)):
+            preds = net(i1, i2, iters=6)
+            loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+            loss.backward()
+            res[name] = (loss.item(), _grads(net))
+    finally:
+        FusedTrainEngine.eligible = staticmethod(orig)
+    assert calls[0] and not calls[-1], calls  # fused engine used for m only
+    (lf, gf), (lr, gr) = res["fused"], res["ref"]
+    assert abs(lf - lr) < 2e-2 * abs(lr) + 1e-2, (lf, lr)
+    a = torch.cat([gf[k].flatten() for k in gr])
+    b = torch.cat([gr[k].flatten() for k in gr])
+    rel = ((a - b).norm() / b.norm()).item()
+    assert rel < 0.05, rel
+    # the correlation gradient reaches fnet
+    assert gf["fnet.conv1.weight"].norm() > 0
+
+
 def test_stream_overlap_matches_serial(cuda):
     """Context encoder / flow branch on the second HIP stream and the deferred
     update-block weight gradients (DeferGrads, third stream) give the same
