@@ -139,7 +139,7 @@ class _Encoder(nn.Module):
         streams, so the HOST issues both chains interleaved -- and, because
         autograd replays nodes by creation order, so does the backward (a
         whole encoder issued first left the other stream idle for its ~2 ms
-        of host issue time, profiles/r2/train_streams.md)."""
+        of host issue time, profiles/r2/train_streams.txt)."""
         fns = [lambda x: conv_norm_act(self.conv1, self.norm1, x)]
         for layer in (self.layer1, self.layer2, self.layer3):
             fns.extend(layer)
