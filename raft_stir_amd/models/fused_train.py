@@ -57,25 +57,32 @@ R = torch.ops.raft_stir
 HD = 128          # hidden dim (full RAFT)
 CORR_C = 324
 CORR_PAD = 384
+SHD = 96          # RAFT-small: hidden dim, 4 levels x 7 x 7 correlation taps (radius 3)
+SCORR_C = 196
+SCORR_PAD = 256
 
 
 class _PConv:
     """A conv of the update block: forward packing, dgrad packing, grad unpacking."""
 
-    def __init__(self, convs, segs, scale=1.0):
+    def __init__(self, convs, segs, scale=1.0, wsegs=None):
         self.convs = convs if isinstance(convs, (list, tuple)) else [convs]
         self.segs = segs          # [(C, [(w0, n, s0), ...]), ...] as in pack_weight
+        # segment layout of the weight-gradient GEMM (its K segments must be
+        # multiples of 64: RAFT-small reads wider, zero-weighted windows there)
+        self.wsegs = wsegs if wsegs is not None else segs
         self.scale = scale        # output scale folded into the epilogue (mask x 0.25)
         w0 = self.convs[0].weight
         self.kh, self.kw = w0.shape[2], w0.shape[3]
         self.cout = sum(c.weight.shape[0] for c in self.convs)
         self.cin = w0.shape[1]
         self.ktot = sum(c for c, _ in segs)
+        self.wktot = sum(c for c, _ in self.wsegs)
 
     def index_maps(self, pidx, fill):
         """Index maps (into the flat parameter vector) of the packed forward
         weight [Cout_pad128][taps][Ktot], the bias, and the dgrad weight
-        Wd[k][tap'][co] = W[co][taps-1-tap'][k] ([pad128(Ktot)][taps][pad64(Cout)])."""
+        Wd[k][tap'][co] = W[co][taps-1-tap'][k] ([pad128(Ktot)][taps][pad32(Cout)])."""
         weight = torch.cat([pidx[id(c.weight)] for c in self.convs], 0)
         bias = torch.cat([pidx[id(c.bias)] for c in self.convs], 0)
         cout, cin, kh, kw = weight.shape
@@ -87,7 +94,7 @@ class _PConv:
             for w0, n, s0 in pieces:
                 w[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
             kb += c
-        cy = pad_to(cout, 64)
+        cy = pad_to(cout, 32)  # the dgrad's K = the gradient slot width (32-channel granules)
         wd = torch.full((pad_to(self.ktot, 128), taps, cy), fill, dtype=torch.long)
         wd[:self.ktot] = w[:cy].flip(1).permute(2, 1, 0)
         self.cy = cy
@@ -100,7 +107,7 @@ class _PConv:
         taps = self.kh * self.kw
         gw = torch.empty(self.cout, taps, self.cin, dtype=torch.long)
         kb = 0
-        for c, pieces in self.segs:
+        for c, pieces in self.wsegs:
             for w0, n, s0 in pieces:
                 gw[:, :, w0:w0 + n] = dwi[:self.cout, :, kb + s0:kb + s0 + n]
             kb += c
@@ -119,18 +126,40 @@ class FusedTrainEngine:
         ub = model.update_block
         enc, g = ub.encoder, ub.gru
         full = lambda c: [(c, [(0, c, 0)])]
-        gru_segs = [(HD, [(0, HD, 0)]), (128, [(HD, 128, 0)]), (128, [(HD + 128, 128, 0)])]
-        self.c1 = _PConv(enc.convc1, [(CORR_PAD, [(0, CORR_C, 0)])])
-        self.c2 = _PConv(enc.convc2, full(256))
-        self.f2 = _PConv(enc.convf2, full(128))
-        self.cv = _PConv(enc.conv, full(256))
-        self.zr = [_PConv([g.convz1, g.convr1], gru_segs), _PConv([g.convz2, g.convr2], gru_segs)]
-        self.q = [_PConv(g.convq1, gru_segs), _PConv(g.convq2, gru_segs)]
-        self.head = _PConv([ub.flow_head.conv1, ub.mask[0]], full(HD))
-        self.flow = _PConv(ub.flow_head.conv2, full(256))
-        self.mask2 = _PConv(ub.mask[2], full(256), scale=0.25)
-        self.convs = [self.c1, self.c2, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow, self.mask2]
+        self.small = bool(model.cfg.small)
+        if self.small:
+            # RAFT-small (reference core/update.py SmallMotionEncoder / ConvGRU /
+            # FlowHead(96, 128)): hx slot = [h 96 | inp 64 | motion 80 | flow 2 | 0 14]
+            # = cat[h, x] of the ConvGRU in ONE 256-channel window
+            self.hd, self.hx_c, self.corr_c, self.corr_pad = SHD, 256, SCORR_C, SCORR_PAD
+            self.c1 = _PConv(enc.convc1, [(SCORR_PAD, [(0, SCORR_C, 0)])])
+            self.f2 = _PConv(enc.convf2, full(64))
+            self.cv = _PConv(enc.conv, full(128))
+            self.zr = [_PConv([g.convz, g.convr], [(256, [(0, SHD + 146, 0)])])]
+            # q reads [r*h | x]; its weight gradient reads 64-aligned windows
+            # (r*h slot zero-padded to 128, x from hx[64:256] with zero weights on h[64:96])
+            self.q = [_PConv(g.convq, [(SHD, [(0, SHD, 0)]), (160, [(SHD, 146, 0)])],
+                             wsegs=[(128, [(0, SHD, 0)]), (192, [(SHD, 146, 32)])])]
+            self.head = _PConv(ub.flow_head.conv1, full(SHD), wsegs=[(128, [(0, SHD, 0)])])
+            self.flow = _PConv(ub.flow_head.conv2, full(128))
+            self.mask2 = None
+            self.c2 = None
+            self.convs = [self.c1, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow]
+        else:
+            self.hd, self.hx_c, self.corr_c, self.corr_pad = HD, 256, CORR_C, CORR_PAD
+            gru_segs = [(HD, [(0, HD, 0)]), (128, [(HD, 128, 0)]), (128, [(HD + 128, 128, 0)])]
+            self.c1 = _PConv(enc.convc1, [(CORR_PAD, [(0, CORR_C, 0)])])
+            self.c2 = _PConv(enc.convc2, full(256))
+            self.f2 = _PConv(enc.convf2, full(128))
+            self.cv = _PConv(enc.conv, full(256))
+            self.zr = [_PConv([g.convz1, g.convr1], gru_segs), _PConv([g.convz2, g.convr2], gru_segs)]
+            self.q = [_PConv(g.convq1, gru_segs), _PConv(g.convq2, gru_segs)]
+            self.head = _PConv([ub.flow_head.conv1, ub.mask[0]], full(HD))
+            self.flow = _PConv(ub.flow_head.conv2, full(256))
+            self.mask2 = _PConv(ub.mask[2], full(256), scale=0.25)
+            self.convs = [self.c1, self.c2, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow, self.mask2]
         self.f1 = enc.convf1
+        self.f1c = self.f1.weight.shape[0]
         # parameter order handed to autograd (grads are returned in this order)
         self.params = []
         for pc in self.convs:
@@ -183,7 +212,7 @@ class FusedTrainEngine:
             layout.append((pc, w.shape, wd.shape, b.shape))
             bf_maps += [w.reshape(-1), wd.reshape(-1)]
             f32_maps.append(b.reshape(-1))
-        f1w = pidx[id(self.f1.weight)].permute(2, 3, 1, 0).contiguous()  # [7][7][2][128]
+        f1w = pidx[id(self.f1.weight)].permute(2, 3, 1, 0).contiguous()  # [7][7][2][f1c]
         f32_maps += [f1w.reshape(-1), pidx[id(self.f1.bias)].reshape(-1)]
         nbf = sum(m.numel() for m in bf_maps)
         gather = torch.cat(bf_maps + f32_maps)
@@ -197,12 +226,13 @@ class FusedTrainEngine:
         # gradient buffer: per conv dW [Cout_pad128][taps][Ktot] + db [Cout], then flow-conv dW, db
         glayout, go = [], 0
         for pc in self.convs:
-            dws = (pad_to(pc.cout, 128), pc.kh * pc.kw, pc.ktot)
+            dws = (pad_to(pc.cout, 128), pc.kh * pc.kw, pc.wktot)
             n = dws[0] * dws[1] * dws[2]
             glayout.append((go, dws, go + n, pc.cout))
             go += n + pc.cout
-        gf1 = (go, go + 49 * 2 * 128)
-        gtotal = gf1[1] + 128
+        fc = self.f1c
+        gf1 = (go, go + 49 * 2 * fc)
+        gtotal = gf1[1] + fc
         gids = torch.arange(gtotal)
         gmaps, gscaled, o = [], [], 0
         for pc, (dwo, dws, dbo, nb) in zip(self.convs, glayout):
@@ -214,8 +244,8 @@ class FusedTrainEngine:
                     scaled_range = (o, o + gw.numel() + gb.numel(), pc.scale)
                     gscaled.append(scaled_range)
                 o += gw.numel() + gb.numel()
-        f1g = gids[gf1[0]:gf1[1]].view(7, 7, 2, 128).permute(3, 2, 0, 1).contiguous()
-        gmaps += [f1g.reshape(-1), gids[gf1[1]:gf1[1] + 128]]
+        f1g = gids[gf1[0]:gf1[1]].view(7, 7, 2, fc).permute(3, 2, 0, 1).contiguous()
+        gmaps += [f1g.reshape(-1), gids[gf1[1]:gf1[1] + fc]]
         self._maps = dict(dev=dev, gather=gather.to(dev), nbf=nbf, layout=layout, scaled=scaled,
                           glayout=glayout, gf1=gf1, gtotal=gtotal, ggather=torch.cat(gmaps).to(dev),
                           gscaled=gscaled, zero=torch.zeros(1, device=dev))
@@ -244,9 +274,10 @@ class FusedTrainEngine:
             of += bs.numel()
         fc = self.model.update_block.flow_head.conv2  # 2-channel output conv: csrc/flowhead.hip
         self.flow_w32 = fc.weight.detach().float().permute(0, 2, 3, 1).contiguous()  # [2][3][3][256]
-        self.f1w = vals[of:of + 49 * 2 * 128].view(7, 7, 2, 128)
-        of += 49 * 2 * 128
-        self.f1b = vals[of:of + 128]
+        fc = self.f1c
+        self.f1w = vals[of:of + 49 * 2 * fc].view(7, 7, 2, fc)
+        of += 49 * 2 * fc
+        self.f1b = vals[of:of + fc]
 
     def side_stream(self, dev, slot: int = 0, flow: bool = False):
         from .raft import OVERLAP
@@ -262,7 +293,7 @@ class FusedTrainEngine:
             pc.dw = g[dwo:dwo + dws[0] * dws[1] * dws[2]].view(dws)
             pc.db = g[dbo:dbo + nb]
         a, b = M["gf1"]
-        return g, g[a:b].view(49, 2, 128), g[b:b + 128]
+        return g, g[a:b].view(49, 2, self.f1c), g[b:b + self.f1c]
 
     def unpack_grads(self, g):
         M = self._maps
@@ -278,13 +309,14 @@ class FusedTrainEngine:
     @staticmethod
     def config_capable(cfg) -> bool:
         """The configuration half of ``eligible`` (no tensors needed)."""
-        return (bool(cfg.mixed_precision) and cfg.fused_gru and not cfg.small
+        return (bool(cfg.mixed_precision) and cfg.fused_gru
+                and not (cfg.small and cfg.alternate_corr)  # on-the-fly correlation: radius-4 kernels only
                 and getattr(cfg, "fused_train", True))
 
     @staticmethod
     def eligible(model, image, corr_fn) -> bool:
         corr_ok = getattr(corr_fn, "state", None) is not None or (  # all-pairs pyramid, or on-the-fly
-            getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == 4
+            getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == 4 and not model.cfg.small
             and corr_fn.f1.dtype == torch.bfloat16)
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
                 and FusedTrainEngine.config_capable(model.cfg)
@@ -303,7 +335,24 @@ class FusedTrainEngine:
     def buffers(self, B, H, W, iters, dev):
         key = (B, H, W, iters, dev)
         S = self._bufs.get(key)
-        if S is None:
+        if S is None and self.small:
+            n = iters * B
+            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=torch.bfloat16)
+            z = lambda b, c: torch.zeros(b, H, W, c, device=dev, dtype=torch.bfloat16)
+            S = dict(
+                corr=e(n, SCORR_PAD), f1=e(n, 64), mot=e(n, 128),
+                hx=z(n + B, 256),                 # channels 242:256 stay zero
+                z=[e(n, SHD)], r=[e(n, SHD)], q=[e(n, SHD)],
+                rh=[z(n, 128)],                   # channels 96:128 stay zero (weight-gradient window)
+                head=e(n, 128), inp=e(B, 64),
+                C=torch.empty(n + B, 2, H, W, device=dev),
+                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
+                d_head=e(n, 128), d_zr=[e(n, 2 * SHD)], d_q=[e(n, SHD)], d_conv=e(n, 96), d_mot=e(n, 128),
+                d_f1=e(n, 64), d_corr=e(n, SCORR_PAD),
+                G=torch.empty(B, H, W, 256, device=dev),
+            )
+            self._bufs = {key: S}
+        elif S is None:
             n = iters * B
             e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=torch.bfloat16)
             S = dict(
@@ -352,6 +401,8 @@ class FusedTrainLoop(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, defer, otf, *tensors):
+        if eng.small:
+            return _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer)
         nt = 0 if otf is None else otf[2] + 1
         otf_t, params = tensors[:nt], tensors[nt:]
         B, _, H, W = coords1.shape
@@ -421,6 +472,8 @@ class FusedTrainLoop(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_up):
+        if ctx.eng.small:
+            return _small_backward(ctx, g_up)
         eng, st, S, iters = ctx.eng, ctx.state, ctx.S, ctx.iters
         c0 = ctx.c0
         B, H, W = S["inp"].shape[:3]
@@ -501,8 +554,21 @@ class FusedTrainLoop(torch.autograd.Function):
         d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
         d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
-        # ---------------- weight / bias gradients, batched over all iterations
-        gbuf, dwf, dbf = eng.grad_buffers(dev)
+        grads = FusedTrainLoop._param_grads(ctx, FusedTrainLoop._wgrads, S, C, B, H, W, n, main, side)
+        if otf is None:
+            token_grad, otf_grads = torch.zeros((), device=dev), ()
+        else:
+            token_grad = None
+            otf_grads = tuple(g.to(t.dtype) for g, t in zip(d_otf, otf_t))
+        return (None, None, token_grad, d_net, d_inp, None, None, None, None, None, *otf_grads, *grads)
+
+    @staticmethod
+    def _param_grads(ctx, wgrads, S, C, B, H, W, n, main, side):
+        """Weight / bias gradients batched over all iterations (``wgrads``), the
+        data-parallel all-reduce of the packed buffer and the unpacking --
+        deferred onto the weight-gradient stream when ``ctx.defer``."""
+        eng = ctx.eng
+        gbuf, dwf, dbf = eng.grad_buffers(main.device)
         if ctx.defer:  # on the weight-gradient stream, joined by DeferGrads.backward
             side.wait_stream(main)
             gbuf.record_stream(side)
@@ -512,7 +578,7 @@ class FusedTrainLoop(torch.autograd.Function):
                 main.wait_stream(side)
             wstream = contextlib.nullcontext()
         with wstream:
-            FusedTrainLoop._wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
+            wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
             if eng.grad_group is not None:  # data parallel: one RCCL all-reduce of the packed buffer
                 eng.reduce_packed(gbuf)
             grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype)
@@ -520,12 +586,7 @@ class FusedTrainLoop(torch.autograd.Function):
         if ctx.defer:
             for gr in grads:
                 gr.record_stream(main)
-        if otf is None:
-            token_grad, otf_grads = torch.zeros((), device=dev), ()
-        else:
-            token_grad = None
-            otf_grads = tuple(g.to(t.dtype) for g, t in zip(d_otf, otf_t))
-        return (None, None, token_grad, d_net, d_inp, None, None, None, None, None, *otf_grads, *grads)
+        return grads
 
     @staticmethod
     def _wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):
@@ -553,3 +614,132 @@ class FusedTrainLoop(torch.autograd.Function):
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
         R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
+
+
+# ------------------------------------------------------------------ RAFT-small
+# The same engine for the small model (reference core/update.py:
+# SmallMotionEncoder, ConvGRU 3x3 hidden 96, FlowHead(96, 128), no mask:
+# bilinear x8 upsampling, core/raft.py:134-137).  Per iteration:
+#   flow branch (side stream): flow_encode -> f1 (64), convf2 3x3 -> mot[96:128]
+#   lookup (radius 3, 196 taps) -> corr, convc1 1x1 -> mot[0:96]
+#   conv 3x3 mot -> hx[160:240]           hx = [h | inp | motion | flow | 0]
+#   z|r 3x3 over hx[0:256] (gate epilogue), q 3x3 over [r*h | hx[96:256]] -> h'
+#   head 3x3 h' -> 128 (ReLU), flow head -> coords_{i+1}
+# All iterations' x8 upsamplings are one interpolation after the loop.
+
+def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer):
+    B, _, H, W = coords1.shape
+    dev = coords1.device
+    hd = SHD
+    eng.pack(dev)
+    S = eng.buffers(B, H, W, iters, dev)
+    sl = lambda t, i: t[i * B:(i + 1) * B]
+    hv = S["hx"].view(iters + 1, B, H, W, 256)
+    hv[0, ..., :hd].copy_(net.permute(0, 2, 3, 1))
+    hv[..., hd:hd + 64].copy_(inp.permute(0, 2, 3, 1))  # the context features of every slot
+    C = S["C"]
+    sl(C, 0).copy_(coords1.detach())
+    c0 = coords0.detach().float().contiguous()
+    main, side = torch.cuda.current_stream(dev), eng.side_stream(dev, flow=True)
+    zr, q = eng.zr[0], eng.q[0]
+    for i in range(iters):
+        hx, hx1 = sl(S["hx"], i), sl(S["hx"], i + 1)
+        coords = sl(C, i)
+        mot = sl(S["mot"], i)
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            R.flow_encode(coords, eng.f1w, eng.f1b, sl(S["f1"], i), 0, hx, 240)
+            conv_fused([(sl(S["f1"], i), 0, 64)], eng.f2.w, eng.f2.b, 3, 3, 32, EPI_RELU, mot, 96)
+        R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+        conv_fused([(sl(S["corr"], i), 0, SCORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, hd, EPI_RELU, mot, 0)
+        if side is not None:
+            main.wait_stream(side)
+        conv_fused([(mot, 0, 128)], eng.cv.w, eng.cv.b, 3, 3, 80, EPI_RELU, hx, 160)
+        z, r, qq, rh = (sl(S[k][0], i) for k in ("z", "r", "q", "rh"))
+        conv_fused([(hx, 0, 256)], zr.w, zr.b, 3, 3, 2 * hd, EPI_GRU_ZR, z, 0, hd=hd, out2=rh, out3=r,
+                   aux1=hx, a1off=0)
+        conv_fused([(rh, 0, hd), (hx, hd, 160)], q.w, q.b, 3, 3, hd, EPI_GRU_Q, hx1, 0, out2=qq, aux1=hx,
+                   a1off=0, aux2=z)
+        head = sl(S["head"], i)
+        conv_fused([(hx1, 0, hd)], eng.head.w, eng.head.b, 3, 3, 128, EPI_RELU, head, 0)
+        R.flow_head(head, 0, 128, eng.flow_w32, eng.flow.b, sl(C, i + 1), coords)
+    n = iters * B
+    flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
+    up = 8 * torch.nn.functional.interpolate(flows, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)
+    ctx.eng, ctx.state, ctx.S, ctx.iters, ctx.otf = eng, corr_state, S, iters, None
+    ctx.defer = bool(defer) and eng.side_stream(dev) is not None
+    ctx.c0 = c0
+    ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
+    return up
+
+
+def _small_backward(ctx, g_up):
+    eng, st, S, iters = ctx.eng, ctx.state, ctx.S, ctx.iters
+    hd = SHD
+    B, H, W = S["inp"].shape[:3]
+    dev = ctx.c0.device
+    n = iters * B
+    sl = lambda t, i: t[i * B:(i + 1) * B]
+    main = torch.cuda.current_stream(dev)
+    side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
+    lside = eng.side_stream(dev, 0) if ctx.defer else None
+    if st.gpyr is None:
+        st.gpyr = st.zero_grads()
+    G = S["G"]  # fp32 [dh 96 | d inp 64 | d motion 80 | d flow 2 | 0]
+    G.zero_()
+    C = S["C"]
+    if g_up is None:
+        g_up = torch.zeros(n, 2, 8 * H, 8 * W, device=dev)
+    # adjoint of the x8 bilinear upsampling (align_corners) of every iteration
+    dflow = 8 * torch.ops.aten.upsample_bilinear2d_backward(g_up.float().contiguous(), [8 * H, 8 * W],
+                                                             [n, 2, H, W], True)
+    S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
+    zr, q = eng.zr[0], eng.q[0]
+    for i in reversed(range(iters)):
+        hx, head, dh = sl(S["hx"], i), sl(S["head"], i), sl(S["d_head"], i)
+        R.flow_head_dgrad(sl(dflow, i), eng.flow_w32, 128, head, 0, dh, 0)
+        conv_fused([(dh, 0, 128)], eng.head.wd, None, 3, 3, hd, EPI_ACC_F32, G, 0)
+        z, r, qq = sl(S["z"][0], i), sl(S["r"][0], i), sl(S["q"][0], i)
+        dq, dzr = sl(S["d_q"][0], i), sl(S["d_zr"][0], i)
+        R.gru_gate_bwd(G, z, qq, hx, 0, dq, dzr)
+        conv_fused([(dq, 0, hd)], q.wd, None, 3, 3, 256, EPI_GRU_QBWD, G, 0, hd=hd, out2=dzr, o2off=hd,
+                   aux1=hx, a1off=0, aux2=r)
+        conv_fused([(dzr, 0, 2 * hd)], zr.wd, None, 3, 3, 256, EPI_ACC_F32, G, 0)
+        dcv, dmot = sl(S["d_conv"], i), sl(S["d_mot"], i)
+        R.relu_take(G, 160, 80, 96, hx, 160, dcv)  # consumes d motion, drops d flow (coords detached)
+        conv_fused([(dcv, 0, 96)], eng.cv.wd, None, 3, 3, 128, EPI_RELU_BWD, dmot, 0, aux1=sl(S["mot"], i))
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            conv_fused([(dmot, 96, 32)], eng.f2.wd, None, 3, 3, 64, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
+                       aux1=sl(S["f1"], i))
+        dcorr = sl(S["d_corr"], i)
+        conv_fused([(dmot, 0, hd)], eng.c1.wd, None, 1, 1, SCORR_PAD, EPI_BIAS, dcorr, 0)
+        if lside is not None:
+            lside.wait_stream(main)
+        with torch.cuda.stream(lside) if lside is not None else contextlib.nullcontext():
+            R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+    if lside is not None:
+        main.wait_stream(lside)
+    d_net = G[..., :hd].permute(0, 3, 1, 2).to(ctx.net_dtype)
+    d_inp = G[..., hd:hd + 64].permute(0, 3, 1, 2).to(ctx.inp_dtype)
+    grads = FusedTrainLoop._param_grads(ctx, _small_wgrads, S, C, B, H, W, n, main, side)
+    return (None, None, torch.zeros((), device=dev), d_net, d_inp, None, None, None, None, None, *grads)
+
+
+def _small_wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):
+    hxs = S["hx"][:n]
+
+    def wg(pc, dy, yoff, segs, bn128=0):
+        R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
+                     [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db, bn128)
+
+    wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 128)])
+    wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, 128)])
+    wg(eng.zr[0], S["d_zr"][0], 0, [(hxs, 0, 256)])
+    wg(eng.q[0], S["d_q"][0], 0, [(S["rh"][0], 0, 128), (hxs, 64, 192)])
+    wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 128)])
+    wg(eng.f2, S["d_mot"], 96, [(S["f1"], 0, 64)])
+    wg(eng.c1, S["d_mot"], 0, [(S["corr"], 0, SCORR_PAD)])
+    R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)

@@ -18,7 +18,7 @@ Engine differences (outputs unchanged):
   * GPU inference (no autograd, bf16) runs the refinement loop through the
     fused engine of models/fused_update.py: ~12 hand-written HIP launches per
     iteration over persistent NHWC buffers instead of the module graph.
-  * GPU training (full RAFT, bf16) runs it as ONE autograd node
+  * GPU training (full RAFT and RAFT-small, bf16) runs it as ONE autograd node
     (models/fused_train.py): fused forward kernels saving activations, a
     hand-written backward (dgrad convs with gradient epilogues, gate
     backward kernels) and weight gradients batched over all iterations.
@@ -161,7 +161,7 @@ class RAFT(nn.Module):
         side = None
         dparams = None
         if (gpu and self.cfg.overlap_encoders and OVERLAP["defer"] and self.training and torch.is_grad_enabled() and mixed
-                and self.cfg.fused_train and not self.cfg.small and not test_mode):
+                and self.cfg.fused_train and not test_mode):
             # update-block weight gradients overlap the encoder backward (see DeferGrads)
             dparams = DeferGrads.apply(self._side_stream(dev, 1), *self._train_engine().params)
         if gpu and self.cfg.overlap_encoders and OVERLAP["cnet"]:

@@ -91,21 +91,30 @@ def _grads(model):
     return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
 
 
-def test_fused_training_matches_module_graph(cuda):
+@pytest.mark.parametrize("small", [False, True], ids=["raft", "raft_small"])
+def test_fused_training_matches_module_graph(cuda, small):
     from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.models.fused_train import FusedTrainEngine
     from raft_stir_amd.train.loss import sequence_loss
     torch.manual_seed(0)
-    m = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).train()
+    m = RAFT(make_args(mixed_precision=True, small=small)).to(cuda).to(memory_format=torch.channels_last).train()
     ref = copy.deepcopy(m)
     ref.cfg = ref.cfg.__class__(**{**ref.cfg.to_dict(), "fused_train": False})
     i1, i2, flow, valid = make_batch(2, 192, 256, seed=2, device=cuda)
     res = {}
-    for name, net in (("fused", m), ("ref", ref)):
-        preds = net(i1, i2, iters=6)
-        assert len(preds) == 6
-        loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
-        loss.backward()
-        res[name] = (loss.item(), [p.detach() for p in preds], _grads(net))
+    calls = []
+    orig = FusedTrainEngine.eligible
+    FusedTrainEngine.eligible = staticmethod(lambda *a: calls.append(orig(*a)) or calls[-1])
+    try:
+        for name, net in (("fused", m), ("ref", ref)):
+            preds = net(i1, i2, iters=6)
+            assert len(preds) == 6
+            loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+            loss.backward()
+            res[name] = (loss.item(), [p.detach() for p in preds], _grads(net))
+    finally:
+        FusedTrainEngine.eligible = staticmethod(orig)
+    assert calls[0] and not calls[-1], calls  # fused engine used for m only
     lf, pf, gf = res["fused"]
     lr, pr, gr = res["ref"]
     assert abs(lf - lr) < 2e-2 * abs(lr) + 1e-2, (lf, lr)
