@@ -33,6 +33,8 @@ class RAFTConfig:
     # "bfloat16" (half the volume bytes; needs bf16 autocast features), or "auto"
     # (bf16 storage exactly when mixed_precision)
     corr_dtype: str = "float32"
+    # bitwise-reproducible GPU training steps (runtime/determinism.py)
+    deterministic: bool = False
 
     @property
     def pyr_dtype(self):
@@ -80,6 +82,7 @@ def resolve_config(args=None, **overrides) -> RAFTConfig:
         fused_train=bool(_get(args, "fused_train", True)),
         overlap_encoders=bool(_get(args, "overlap_encoders", os.environ.get("RS_OVERLAP_ENCODERS", "1") != "0")),
         corr_dtype=str(_get(args, "corr_dtype", os.environ.get("RS_CORR_DTYPE", "float32"))),
+        deterministic=bool(_get(args, "deterministic", False)),
         **dims,
     )
     cfg.update(overrides)

@@ -26,6 +26,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace rs {
 namespace wgrad {
 
@@ -44,6 +46,10 @@ struct Args {
   int Ktot, taps;
   float* dw;
   int kchunk;
+  // deterministic mode: per-K-split partial tiles (plain stores) reduced in a
+  // fixed order by det_reduce_kernel instead of fp32 atomics into dw / db
+  float* part;    // [ksplit][Cout][taps][Ktot]
+  float* dbpart;  // [ksplit][Cout]
   unsigned dy_bytes, seg_bytes[3];
 };
 
@@ -229,7 +235,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int co = m0 + acg * 8 + j;
-      if (co < a.Cout) atomicAdd(db + co, bsum[j]);
+      if (co < a.Cout) {
+        if (a.dbpart)
+          a.dbpart[(size_t)(lid / (ntiles * mtiles)) * a.Cout + co] = bsum[j];
+        else
+          atomicAdd(db + co, bsum[j]);
+      }
     }
   }
   // C[co][k]: row = 4*(lane>>4) + j (co), col = lane & 15 (k)
@@ -241,7 +252,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
       for (int j = 0; j < 4; ++j) {
         const int co = m0 + wm * (BM / 2) + mt * 16 + (lane >> 4) * 4 + j;
         const int k = kb + wn * (BN / 2) + nt * 16 + (lane & 15);
-        if (co < a.Cout) atomicAdd(a.dw + ((size_t)co * a.taps + tap) * a.Ktot + k, acc[mt][nt][j]);
+        if (co < a.Cout) {
+          const size_t o = ((size_t)co * a.taps + tap) * a.Ktot + k;
+          if (a.part)
+            a.part[(size_t)(lid / (ntiles * mtiles)) * a.Cout * a.taps * a.Ktot + o] = acc[mt][nt][j];
+          else
+            atomicAdd(a.dw + o, acc[mt][nt][j]);
+        }
       }
 }
 
@@ -456,7 +473,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
         float s = 0.f;
         for (int u = t; u < NT; u += CA) s += red[u * 8 + j];
         const int co = m0 + t * 8 + j;
-        if (co < a.Cout) atomicAdd(db + co, s);
+        if (co < a.Cout) {
+          if (a.dbpart)
+            a.dbpart[(size_t)(lid / (ntiles * mtiles)) * a.Cout + co] = s;
+          else
+            atomicAdd(db + co, s);
+        }
       }
     }
   }
@@ -468,19 +490,29 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
       for (int j = 0; j < 4; ++j) {
         const int co = m0 + wm * (BM / WGM) + mt * 16 + (lane >> 4) * 4 + j;
         const int k = kb + wn * (BN / WGN) + nt * 16 + (lane & 15);
-        if (co < a.Cout) atomicAdd(a.dw + ((size_t)co * a.taps + tap) * a.Ktot + k, acc[mt][nt][j]);
+        if (co < a.Cout) {
+          const size_t o = ((size_t)co * a.taps + tap) * a.Ktot + k;
+          if (a.part)
+            a.part[(size_t)(lid / (ntiles * mtiles)) * a.Cout * a.taps * a.Ktot + o] = acc[mt][nt][j];
+          else
+            atomicAdd(a.dw + o, acc[mt][nt][j]);
+        }
       }
 }
 
 // db[c] += sum_p dY[p][yoff + c]; block = 256 pixels, threads over channels.
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ dy, int ystr, int yoff,
-                                                     int C, int P, float* __restrict__ db) {
+                                                     int C, int P, float* __restrict__ db,
+                                                     float* __restrict__ part) {
   const int p0 = blockIdx.x * 256;
   const int p1 = min(P, p0 + 256);
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
     for (int p = p0; p < p1; ++p) s += bf2f(dy[(size_t)p * ystr + yoff + c]);
-    atomicAdd(db + c, s);
+    if (part)
+      part[(size_t)blockIdx.x * C + c] = s;
+    else
+      atomicAdd(db + c, s);
   }
 }
 
@@ -494,7 +526,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 constexpr int FROWS = 8;
 __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict__ coords, int Bp, int H, int W,
                                                          const bf16_t* __restrict__ df, int fstr, int Cout,
-                                                         float* __restrict__ dw, float* __restrict__ db) {
+                                                         float* __restrict__ dw, float* __restrict__ db,
+                                                         float* __restrict__ part) {
   extern __shared__ float fl[];  // [2][FROWS + 6][W + 6]
   const int HW = H * W, WP = W + 6, RP = FROWS + 6;
   const int rblocks = cdiv(H, FROWS);
@@ -540,9 +573,27 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
           for (int kx = 0; kx < 6; ++kx) win[ky][kx] = win[ky][kx + 1];
       }
     }
+    if (part) {  // deterministic mode: this block's [98 * Cout | Cout] partial, reduced in order later
+      float* pb = part + (size_t)blockIdx.x * 99 * Cout;
 #pragma unroll
-    for (int i = 0; i < 49; ++i) atomicAdd(dw + ((size_t)i * 2 + ci) * Cout + co, acc[i]);
-    if (ci == 0) atomicAdd(db + co, bsum);
+      for (int i = 0; i < 49; ++i) pb[(i * 2 + ci) * Cout + co] = acc[i];
+      if (ci == 0) pb[98 * Cout + co] = bsum;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 49; ++i) atomicAdd(dw + ((size_t)i * 2 + ci) * Cout + co, acc[i]);
+      if (ci == 0) atomicAdd(db + co, bsum);
+    }
+  }
+}
+
+// out[i] += sum_{s < nsplit} part[s * sstride + i], summed in split order
+// (deterministic mode's replacement for the fp32 atomics above)
+__global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict__ part, int nsplit, long sstride,
+                                                         long n, float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += part[(size_t)k * sstride + i];
+    out[i] += s;
   }
 }
 
@@ -560,7 +611,53 @@ struct WgradLaunch {
   int bn128;  // allow 128-wide N tiles
   unsigned dy_bytes, seg_bytes[3];  // buffer range checks
   int dma;  // 1: buffer-DMA kernel
+  float* part;    // deterministic mode: >= wgrad_splits(L) * (Cout*taps*Ktot + Cout) floats, else null
 };
+
+namespace {
+struct WgradPlan {
+  int var, bm, bn, nthr, ntiles, mtiles, ksplit, kchunk;
+};
+
+// Tile variant and split-K of one weight-gradient GEMM.  ``det``: the
+// deterministic mode's partial-tile buffers scale with the split count, so it
+// is capped at 32 there.
+WgradPlan wgrad_plan(const WgradLaunch& L, bool det) {
+  WgradPlan pl{};
+  // tile variant (L.bn128): 0 = 128x64 (64x64 for Cout <= 64), 1 = 128x128,
+  // 8-wave DMA tiles: 2 = 128x128, 3 = 256x128, 4 = 256x64, 5 = 64x128 (4 waves)
+  bool seg128 = true;  // a 128-wide N tile must stay inside one segment
+  for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
+  int var = L.bn128;
+  if (var < 0 || var > 5 || (!L.dma && var > 1)) var = 0;
+  if ((var == 1 || var == 2 || var == 3 || var == 5) && !seg128) var = 0;
+  if (var == 1 && L.Cout <= 64) var = 0;
+  pl.var = var;
+  pl.bm = var == 3 || var == 4 ? 256 : (var == 5 ? 64 : (var == 0 && L.Cout <= 64 ? 64 : 128));
+  pl.bn = var == 0 || var == 4 ? 64 : 128;
+  pl.nthr = var >= 2 && var <= 4 ? 512 : 256;
+  const int taps = L.KH * L.KW, P = L.Bp * L.H * L.W;
+  pl.ntiles = taps * (L.Ktot / pl.bn);
+  pl.mtiles = cdiv(L.Cout, pl.bm);
+  // split-K over the pixels: more blocks hide latency, but every split adds a
+  // full dW tile of fp32 atomics (~1.3 TB/s chip-wide, MI355X_MICROARCH.md)
+  static const int target_blocks = [] {
+    const char* e = getenv("RS_WGRAD_BLOCKS");
+    return e ? atoi(e) : 2048;
+  }();
+  int ksplit = cdiv(target_blocks, pl.ntiles * pl.mtiles);
+  ksplit = max(1, min(ksplit, cdiv(P, wgrad::BK * 8)));
+  if (det) ksplit = min(ksplit, 32);
+  pl.kchunk = round_up(cdiv(P, ksplit), wgrad::BK);
+  pl.ksplit = cdiv(P, pl.kchunk);  // every split is non-empty (each writes its whole partial tile)
+  return pl;
+}
+}  // namespace
+
+int wgrad_splits(const WgradLaunch& L) { return wgrad_plan(L, true).ksplit; }
+
+static void wgrad_kernels(const WgradLaunch& L, const wgrad::Args& a, int var, int bm, int bn, int nthr, dim3 grid,
+                          hipStream_t stream);
 
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   wgrad::Args a{};
@@ -579,30 +676,32 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   a.dw = L.dw;
   a.dy_bytes = L.dy_bytes;
   for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
-  // tile variant (L.bn128): 0 = 128x64 (64x64 for Cout <= 64), 1 = 128x128,
-  // 8-wave DMA tiles: 2 = 128x128, 3 = 256x128, 4 = 256x64, 5 = 64x128 (4 waves)
-  bool seg128 = true;  // a 128-wide N tile must stay inside one segment
-  for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
-  int var = L.bn128;
-  if (var < 0 || var > 5 || (!L.dma && var > 1)) var = 0;
-  if ((var == 1 || var == 2 || var == 3 || var == 5) && !seg128) var = 0;
-  if (var == 1 && a.Cout <= 64) var = 0;
-  const int bm = var == 3 || var == 4 ? 256 : (var == 5 ? 64 : (var == 0 && a.Cout <= 64 ? 64 : 128));
-  const int bn = var == 0 || var == 4 ? 64 : 128;
-  const int nthr = var >= 2 && var <= 4 ? 512 : 256;
-  const int ntiles = a.taps * (a.Ktot / bn);
-  const int mtiles = cdiv(a.Cout, bm);
-  // split-K over the pixels: more blocks hide latency, but every split adds a
-  // full dW tile of fp32 atomics (~1.3 TB/s chip-wide, MI355X_MICROARCH.md)
-  static const int target_blocks = [] {
-    const char* e = getenv("RS_WGRAD_BLOCKS");
-    return e ? atoi(e) : 2048;
-  }();
-  int ksplit = cdiv(target_blocks, ntiles * mtiles);
-  ksplit = max(1, min(ksplit, cdiv(a.P, wgrad::BK * 8)));
-  a.kchunk = round_up(cdiv(a.P, ksplit), wgrad::BK);
-  ksplit = cdiv(a.P, a.kchunk);
-  dim3 grid(ntiles * mtiles * ksplit);
+  const bool det = L.part != nullptr;
+  const WgradPlan pl = wgrad_plan(L, det);
+  const int var = pl.var, bm = pl.bm, bn = pl.bn, nthr = pl.nthr;
+  const int ksplit = pl.ksplit;
+  a.kchunk = pl.kchunk;
+  const long pstride = (long)a.Cout * a.taps * a.Ktot;
+  if (det) {
+    a.part = L.part;
+    a.dbpart = L.db ? L.part + (size_t)ksplit * pstride : nullptr;
+  }
+  dim3 grid(pl.ntiles * pl.mtiles * ksplit);
+  if (det) {
+    wgrad_kernels(L, a, var, bm, bn, nthr, grid, stream);
+    const int rb = (int)std::min<long>(4096, cdiv(pstride, 256));
+    hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(rb), dim3(256), 0, stream, a.part, ksplit, pstride, pstride,
+                       a.dw);
+    if (L.db)
+      hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(cdiv(a.Cout, 256)), dim3(256), 0, stream, a.dbpart, ksplit,
+                         (long)a.Cout, (long)a.Cout, L.db);
+    return;
+  }
+  wgrad_kernels(L, a, var, bm, bn, nthr, grid, stream);
+}
+
+static void wgrad_kernels(const WgradLaunch& L, const wgrad::Args& a, int var, int bm, int bn, int nthr, dim3 grid,
+                          hipStream_t stream) {
   if (L.dma) {
     switch (var) {
       case 1: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
@@ -626,17 +725,32 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
     hipLaunchKernelGGL((wgrad::wgrad_kernel<64, 64>), grid, dim3(256), 0, stream, a, L.db);
 }
 
-void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream) {
-  hipLaunchKernelGGL(wgrad::colsum_kernel, dim3(cdiv(P, 256)), dim3(256), 0, stream,
-                     static_cast<const bf16_t*>(dy), ystr, yoff, C, P, db);
+int colsum_blocks(int P) { return cdiv(P, 256); }
+
+void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, float* part, hipStream_t stream) {
+  const int blocks = colsum_blocks(P);
+  hipLaunchKernelGGL(wgrad::colsum_kernel, dim3(blocks), dim3(256), 0, stream,
+                     static_cast<const bf16_t*>(dy), ystr, yoff, C, P, db, part);
+  if (part)
+    hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(cdiv(C, 256)), dim3(256), 0, stream, part, blocks, (long)C,
+                       (long)C, db);
 }
 
+int flow_wgrad_blocks(int Bp, int H) { return Bp * cdiv(H, wgrad::FROWS); }
+
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
-                       float* db, hipStream_t stream) {
-  const int blocks = Bp * cdiv(H, wgrad::FROWS);
+                       float* db, float* part, hipStream_t stream) {
+  const int blocks = flow_wgrad_blocks(Bp, H);
   const size_t lds = sizeof(float) * 2 * (wgrad::FROWS + 6) * (W + 6);
   hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(blocks), dim3(256), lds, stream, coords, Bp, H, W,
-                     static_cast<const bf16_t*>(df), fstr, Cout, dw, db);
+                     static_cast<const bf16_t*>(df), fstr, Cout, dw, db, part);
+  if (part) {  // [blocks][98 * Cout | Cout] partials -> dw, db in block order
+    const long st = 99L * Cout;
+    hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(cdiv(98 * Cout, 256)), dim3(256), 0, stream, part, blocks, st,
+                       98L * Cout, dw);
+    hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(cdiv(Cout, 256)), dim3(256), 0, stream, part + 98 * Cout,
+                       blocks, st, (long)Cout, db);
+  }
 }
 
 }  // namespace rs

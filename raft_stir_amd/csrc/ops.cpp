@@ -6,6 +6,7 @@
 // shape must never reach a kernel) and launches on PyTorch's current HIP
 // stream, so the ops compose with torch streams and hipGraph capture.
 
+#include <atomic>
 #include <ATen/ATen.h>
 #include "host_common.h"
 #include <c10/core/DeviceGuard.h>
@@ -17,6 +18,13 @@
 #include <hip/hip_runtime.h>
 
 namespace rs {
+// Deterministic mode (torch.ops.raft_stir.set_deterministic): the kernels that
+// accumulate with fp32 atomics (weight / bias gradients, flow-encoder weight
+// gradient) write per-split partials reduced in a fixed order instead, and the
+// ops that have no such variant refuse to run.
+static std::atomic<bool> g_deterministic{false};
+bool deterministic() { return g_deterministic.load(std::memory_order_relaxed); }
+
 void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1, int H2, int W2,
                         int C, int levels, void* const* out, const int* Hs, const int* Ws, const int* Ss,
                         bool out_bf16, void* ws, float scale, hipStream_t stream);
@@ -295,6 +303,9 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
   const c10::DeviceGuard guard(f1.device());
   const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
   const int levels = f2.size(), D = 2 * radius + 1;
+  TORCH_CHECK(!rs::deterministic(),
+              "corr_otf_backward: the on-the-fly correlation backward scatters with fp32 atomics and has no "
+              "deterministic variant; train with the all-pairs correlation (no --alternate_corr) in deterministic mode");
   check_gpu(dout, "dout");
   TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
                   dout.size(3) == levels * D * D,
@@ -467,9 +478,14 @@ std::vector<Tensor> gru_bwd_fin(const Tensor& dhd, const Tensor& drhx, const Ten
   return {dh, dx};
 }
 
+void set_deterministic(bool on) { rs::g_deterministic.store(on); }
+bool is_deterministic() { return rs::deterministic(); }
+
 }  // namespace
 
 TORCH_LIBRARY(raft_stir, m) {
+  m.def("set_deterministic(bool on) -> ()", &set_deterministic);
+  m.def("is_deterministic() -> bool", &is_deterministic);
   m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale, bool out_bf16=False) -> Tensor[]");
   m.def("corr_lookup(Tensor[] pyr, Tensor coords, int radius, bool out_bf16) -> Tensor");
   m.def("corr_lookup_into(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");

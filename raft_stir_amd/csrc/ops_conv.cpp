@@ -53,11 +53,16 @@ struct WgradLaunch {
   float* db;
   int bn128;  unsigned dy_bytes, seg_bytes[3];  // buffer range checks
   int dma;  // 1: buffer-DMA kernel
+  float* part;  // deterministic mode: split partials (see wgrad_splits), else null
 };
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream);
-void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, hipStream_t stream);
+int wgrad_splits(const WgradLaunch& L);
+int colsum_blocks(int P);
+void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, float* part, hipStream_t stream);
+int flow_wgrad_blocks(int Bp, int H);
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
-                       float* db, hipStream_t stream);
+                       float* db, float* part, hipStream_t stream);
+bool deterministic();
 }  // namespace rs
 
 namespace {
@@ -344,6 +349,14 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   L.dw = dw.data_ptr<float>();
   L.db = db ? db->data_ptr<float>() : nullptr;
   L.bn128 = bn128;
+  L.part = nullptr;
+  Tensor part;
+  if (rs::deterministic()) {
+    TORCH_CHECK(L.dma, "conv_wgrad: deterministic mode needs the buffer-DMA kernels (RS_WGRAD_DMA=1)");
+    const int64_t n = int64_t(rs::wgrad_splits(L)) * (int64_t(Cout) * KH * KW * Ktot + Cout);
+    part = at::empty({n}, dy.options().dtype(at::kFloat));
+    L.part = part.data_ptr<float>();
+  }
   rs::wgrad_launch(L, stream());
   RS_CHECK_LAUNCH();
 }
@@ -354,7 +367,10 @@ void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
   TORCH_CHECK(db.is_cuda() && db.scalar_type() == at::kFloat && db.numel() >= C, "colsum: fp32 db");
   const c10::DeviceGuard guard(dy.device());
   const int P = dy.numel() / dy.size(-1);
-  rs::colsum_launch(dy.data_ptr(), dy.size(-1), yoff, C, P, db.data_ptr<float>(), stream());
+  Tensor part;
+  if (rs::deterministic()) part = at::empty({int64_t(rs::colsum_blocks(P)) * C}, dy.options().dtype(at::kFloat));
+  rs::colsum_launch(dy.data_ptr(), dy.size(-1), yoff, C, P, db.data_ptr<float>(),
+                    part.defined() ? part.data_ptr<float>() : nullptr, stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -371,9 +387,13 @@ void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const 
                   db.scalar_type() == at::kFloat,
               "flow_wgrad: dw fp32 [49][2][Cout], db fp32 [Cout]");
   TORCH_CHECK(W <= 1024, "flow_wgrad: row width <= 1024 (LDS staging)");
+  TORCH_CHECK(dw.is_contiguous() && db.is_contiguous(), "flow_wgrad: dw, db contiguous");
   const c10::DeviceGuard guard(coords.device());
+  Tensor part;
+  if (rs::deterministic())
+    part = at::empty({int64_t(rs::flow_wgrad_blocks(Bp, H)) * 99 * Cout}, coords.options());
   rs::flow_wgrad_launch(coords.data_ptr<float>(), Bp, H, W, df.data_ptr(), df.size(3), Cout, dw.data_ptr<float>(),
-                        db.data_ptr<float>(), stream());
+                        db.data_ptr<float>(), part.defined() ? part.data_ptr<float>() : nullptr, stream());
   RS_CHECK_LAUNCH();
 }
 

@@ -627,6 +627,28 @@ class FusedTrainLoop(torch.autograd.Function):
 #   head 3x3 h' -> 128 (ReLU), flow head -> coords_{i+1}
 # All iterations' x8 upsamplings are one interpolation after the loop.
 
+_INTERP = {}
+
+
+def _interp_matrix(n_in: int, n_out: int, dev) -> torch.Tensor:
+    """[n_out, n_in] weights of 1-D linear interpolation with align_corners=True,
+    using upsample_bilinear2d's float32 source-index arithmetic."""
+    key = (n_in, n_out, str(dev))
+    m = _INTERP.get(key)
+    if m is None:
+        scale = torch.tensor(float(n_in - 1), dtype=torch.float32) / (n_out - 1) if n_out > 1 else torch.tensor(0.0)
+        src = scale * torch.arange(n_out, dtype=torch.float32)
+        i0 = src.long()
+        lam = src - i0.float()
+        i1 = torch.where(i0 < n_in - 1, i0 + 1, i0)
+        m = torch.zeros(n_out, n_in, dtype=torch.float32)
+        rows = torch.arange(n_out)
+        m[rows, i0] += 1 - lam
+        m[rows, i1] += lam
+        m = _INTERP[key] = m.to(dev)
+    return m
+
+
 def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer):
     B, _, H, W = coords1.shape
     dev = coords1.device
@@ -691,9 +713,11 @@ def _small_backward(ctx, g_up):
     C = S["C"]
     if g_up is None:
         g_up = torch.zeros(n, 2, 8 * H, 8 * W, device=dev)
-    # adjoint of the x8 bilinear upsampling (align_corners) of every iteration
-    dflow = 8 * torch.ops.aten.upsample_bilinear2d_backward(g_up.float().contiguous(), [8 * H, 8 * W],
-                                                             [n, 2, H, W], True)
+    # adjoint of the x8 bilinear upsampling (align_corners) of every iteration:
+    # separable, so two batched GEMMs (deterministic, unlike the atomic scatter
+    # of upsample_bilinear2d_backward)
+    ah, aw = _interp_matrix(H, 8 * H, dev), _interp_matrix(W, 8 * W, dev)
+    dflow = (8 * torch.matmul(torch.matmul(ah.t(), g_up.float()), aw)).contiguous()
     S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
     zr, q = eng.zr[0], eng.q[0]
     for i in reversed(range(iters)):

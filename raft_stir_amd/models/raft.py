@@ -83,6 +83,9 @@ class RAFT(nn.Module):
             self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch", dropout=cfg.dropout)
             self.update_block = BasicUpdateBlock(cfg, hidden_dim=hdim)
         self.set_fused_gru(cfg.fused_gru)
+        if cfg.deterministic:  # process-wide switch (runtime/determinism.py)
+            from ..runtime.determinism import set_deterministic
+            set_deterministic(True)
 
     # ------------------------------------------------------------------ utils
     def set_fused_gru(self, enabled: bool):

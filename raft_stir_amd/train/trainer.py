@@ -86,6 +86,9 @@ def build_parser():
     p.add_argument("--device", default=None, help="force cpu / cuda")
     p.add_argument("--synthetic_length", type=int, default=22232)
     p.add_argument("--bucket_mb", type=float, default=5.0, help="DDP gradient bucket size")
+    p.add_argument("--deterministic", action="store_true",
+                   help="bitwise-reproducible GPU steps: ordered reductions instead of fp32 atomics "
+                        "(runtime/determinism.py; not with --alternate_corr)")
     return p
 
 
@@ -113,8 +116,14 @@ def train(args):
     torch.manual_seed(args.seed + info.rank)
     np.random.seed(args.seed + info.rank)
 
+    if getattr(args, "deterministic", False):
+        if args.alternate_corr:
+            raise SystemExit("--deterministic: the on-the-fly correlation backward has no deterministic variant")
+        from ..runtime.determinism import set_deterministic
+        set_deterministic(True)
     margs = make_args(small=args.small, mixed_precision=args.mixed_precision,
-                      alternate_corr=args.alternate_corr, dropout=args.dropout)
+                      alternate_corr=args.alternate_corr, dropout=args.dropout,
+                      deterministic=getattr(args, "deterministic", False))
     model = RAFT(margs)
     if info.is_main:
         print("Parameter Count: %d" % count_parameters(model))

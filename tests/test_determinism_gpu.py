@@ -1,0 +1,97 @@
+"""Deterministic mode (runtime/determinism.py): two identical training steps
+give bitwise-identical gradients; the ordered-reduction kernels agree with
+the atomic ones to fp32 round-off."""
+import copy
+
+import pytest
+import torch
+
+from raft_stir_amd.config import make_args
+from raft_stir_amd.models import RAFT
+from raft_stir_amd.ops.conv import pad_to
+from raft_stir_amd.runtime.determinism import deterministic
+
+pytestmark = pytest.mark.gpu
+
+
+def _step_grads(model, batch, iters):
+    from raft_stir_amd.train.loss import sequence_loss
+    i1, i2, flow, valid = batch
+    model.zero_grad(set_to_none=True)
+    preds = model(i1, i2, iters=iters)
+    loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                   if p.grad is not None}
+
+
+@pytest.mark.parametrize("small", [False, True], ids=["raft", "raft_small"])
+def test_training_step_bitwise_reproducible(cuda, small):
+    from raft_stir_amd.data.synthetic import make_batch
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True, small=small)).to(cuda).to(memory_format=torch.channels_last).train()
+    batch = make_batch(2, 192, 256, seed=5, device=cuda)
+    with deterministic():
+        l0, g0 = _step_grads(m, batch, 4)
+        # a different allocation pattern in between must not matter
+        junk = torch.empty(123457, device=cuda)
+        l1, g1 = _step_grads(m, batch, 4)
+        del junk
+    assert torch.equal(l0, l1)
+    assert g0.keys() == g1.keys() and len(g0) > 0
+    bad = [k for k in g0 if not torch.equal(g0[k], g1[k])]
+    assert not bad, bad[:8]
+    # the deterministic step is the same step as the default one (round-off only)
+    l2, g2 = _step_grads(m, batch, 4)
+    assert torch.allclose(l0, l2, rtol=1e-3, atol=1e-3)
+    for k in g0:
+        a, b = g0[k].float().flatten(), g2[k].float().flatten()
+        if b.norm() < 1e-6:
+            continue
+        assert torch.nn.functional.cosine_similarity(a, b, dim=0) > 0.99, k
+
+
+def test_wgrad_deterministic_matches_atomic(cuda):
+    g = torch.Generator(device=cuda).manual_seed(1)
+    B, H, W, cin, cout = 6, 24, 40, 128, 192
+    x = torch.randn(B, H, W, cin, device=cuda, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, H, W, cout, device=cuda, generator=g).to(torch.bfloat16)
+    outs = []
+    for det in (False, True, True):
+        dw = torch.zeros(pad_to(cout, 128), 9, cin, device=cuda)
+        db = torch.zeros(cout, device=cuda)
+        with deterministic(det):
+            torch.ops.raft_stir.conv_wgrad(dy, 0, cout, [x], [0], [cin], [B * H * W], 3, 3, dw, db, 0)
+        outs.append((dw, db))
+    (a, ab), (d1, d1b), (d2, d2b) = outs
+    assert torch.equal(d1, d2) and torch.equal(d1b, d2b)
+    torch.testing.assert_close(d1, a, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(d1b, ab, rtol=1e-4, atol=1e-3)
+
+
+def test_flow_wgrad_deterministic(cuda):
+    g = torch.Generator(device=cuda).manual_seed(2)
+    Bp, H, W, C = 8, 20, 36, 128
+    coords = torch.rand(Bp, 2, H, W, device=cuda, generator=g) * 30
+    df = torch.randn(Bp, H, W, C, device=cuda, generator=g).to(torch.bfloat16)
+    res = []
+    for det in (False, True, True):
+        dw = torch.zeros(49, 2, C, device=cuda)
+        db = torch.zeros(C, device=cuda)
+        with deterministic(det):
+            torch.ops.raft_stir.flow_wgrad(coords, df, dw, db)
+        res.append((dw, db))
+    assert torch.equal(res[1][0], res[2][0]) and torch.equal(res[1][1], res[2][1])
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-4, atol=1e-2)
+
+
+def test_otf_backward_refused_in_deterministic_mode(cuda):
+    B, H, W, C = 1, 8, 8, 256
+    f1 = torch.randn(B, H, W, C, device=cuda)
+    f2 = [torch.randn(B, H >> l, W >> l, C, device=cuda) for l in range(2)]
+    coords = torch.rand(B, 2, H, W, device=cuda) * 7
+    dout = torch.randn(B, H, W, 2 * 81, device=cuda)
+    with deterministic():
+        with pytest.raises(RuntimeError, match="deterministic"):
+            torch.ops.raft_stir.corr_otf_backward(f1, f2, coords, 4, 0.125, dout)

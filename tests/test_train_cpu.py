@@ -128,3 +128,28 @@ def test_nonfinite_step_skipped_on_cpu(tmp_path, monkeypatch):
     assert all(torch.isfinite(v).all() for v in sd.values() if v.is_floating_point())
     lines = open(tmp_path / "logs" / "metrics.jsonl").read()
     assert '"skipped": 1.0' in lines
+
+
+def test_bilinear_x8_adjoint_matrices():
+    """RAFT-small's fused engine differentiates the x8 align_corners upsampling
+    as two GEMMs (models/fused_train.py:_interp_matrix): same forward and
+    adjoint as upsample_bilinear2d."""
+    import torch.nn.functional as F
+    from raft_stir_amd.models.fused_train import _interp_matrix
+    H, W = 13, 21
+    x = torch.randn(3, 2, H, W, dtype=torch.float64).float().requires_grad_()
+    up = F.interpolate(x, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)
+    ah, aw = _interp_matrix(H, 8 * H, "cpu"), _interp_matrix(W, 8 * W, "cpu")
+    torch.testing.assert_close(ah @ x.detach() @ aw.t(), up.detach(), rtol=0, atol=2e-6)
+    g = torch.randn_like(up)
+    up.backward(g)
+    torch.testing.assert_close(ah.t() @ g @ aw, x.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_deterministic_flag_plumbing():
+    from raft_stir_amd.config import make_args, resolve_config
+    from raft_stir_amd.train.trainer import build_parser
+    assert resolve_config(make_args(deterministic=True)).deterministic
+    assert not resolve_config(make_args()).deterministic
+    a = build_parser().parse_args(["--deterministic"])
+    assert a.deterministic
