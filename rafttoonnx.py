@@ -20,21 +20,36 @@ import torch  # noqa: E402
 
 from raft_stir_amd.cli_common import add_model_args, load_image, load_model  # noqa: E402
 from raft_stir_amd.export.pointtrack import (NUMITERS, POINTCOUNT, RaftPointTrack, _FlowOnly,  # noqa: E402
-                                             export_onnx, export_pointtrack, export_torchscript,
-                                             onnx_available)
+                                             _reference_mode, export_onnx, export_pointtrack,
+                                             export_torchscript, onnx_available)
 from raft_stir_amd.utils.padder import InputPadder  # noqa: E402
 
 
 def testconvertmodel(args, device):
     """Bare model on padded demo frames -> raftsmall.onnx (reference :49-92)."""
-    model = load_model(args, device)
     images = sorted(glob.glob(os.path.join(args.path, "*.png")) + glob.glob(os.path.join(args.path, "*.jpg")))
-    if len(images) < 2 or not onnx_available():
-        return None
+    if len(images) < 2:
+        raise FileNotFoundError(f"testconvertmodel: need >= 2 frames in {args.path!r} "
+                                "(demo-frames/ ships with the repo: scripts/make_demo_frames.py)")
+    model = load_model(args, device)
     image1, image2 = load_image(images[0], device), load_image(images[1], device)
     image1, image2 = InputPadder(image1.shape).pad(image1, image2)
-    return export_onnx(_FlowOnly(model, NUMITERS), (image1, image2), os.path.join(args.out, "raftsmall.onnx"),
-                       ["image1", "image2"], ["flow_low", "flow_up"])
+    module = _FlowOnly(model, NUMITERS)
+    if onnx_available():
+        return export_onnx(module, (image1, image2), os.path.join(args.out, "raftsmall.onnx"),
+                           ["image1", "image2"], ["flow_low", "flow_up"])
+    # no onnx package: the same graph as TorchScript (raftsmall.pt), checked against eager
+    path = os.path.join(args.out, "raftsmall.pt")
+    module.eval()
+    with torch.no_grad(), _reference_mode():
+        traced = torch.jit.trace(module, (image1, image2), check_trace=False)
+        traced.save(path)
+        want, got = module(image1, image2), torch.jit.load(path, map_location=device)(image1, image2)
+    err = max((w - g).abs().max().item() for w, g in zip(want, got))
+    if err > 1e-3:
+        raise AssertionError(f"raftsmall.pt parity failed: max|diff|={err}")
+    print(f"onnx not installed: wrote {path} (TorchScript, max|diff| vs eager {err:.2e})")
+    return path
 
 
 def convertmodeldirect(args, device):

@@ -109,6 +109,8 @@ def test_cli_scripts(fake_root, tmp_path):
                          env=env, capture_output=True, text=True, timeout=900)
     assert res.returncode == 0, res.stderr[-2000:]
     assert os.path.exists(tmp_path / "exp" / "raft_pointtrackSTIR.pt")
+    # the demo-shape export of the bare model (ONNX, or TorchScript without onnx)
+    assert os.path.exists(tmp_path / "exp" / "raftsmall.pt") or os.path.exists(tmp_path / "exp" / "raftsmall.onnx")
     # without --random_init a missing checkpoint is an error (reference CLIs load strictly)
     res = subprocess.run([sys.executable, os.path.join(ROOT, "evaluate.py"), "--small", "--dataset", "kitti",
                           "--data_root", r, "--model", str(tmp_path / "typo.pth")], env=env,
@@ -131,3 +133,22 @@ def test_core_shim_imports():
         for k in ("raft", "utils.utils", "utils"):
             sys.modules.pop(k, None)
         sys.modules.update(saved)
+
+
+def test_shipped_demo_frames():
+    """demo-frames/ (scripts/make_demo_frames.py) is the default --path of
+    demo.py / rafttoonnx.py: procedural frames with a known motion."""
+    import importlib.util
+    import numpy as np
+    from raft_stir_amd.data import frame_utils
+    frames = sorted(glob.glob(os.path.join(ROOT, "demo-frames", "*.png")))
+    assert len(frames) >= 2
+    img = np.asarray(frame_utils.read_gen(frames[0]))
+    assert img.shape == (436, 1024, 3) and img.dtype == np.uint8
+    spec = importlib.util.spec_from_file_location("mdf", os.path.join(ROOT, "scripts", "make_demo_frames.py"))
+    mdf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mdf)
+    assert np.array_equal(mdf.frame(0), img)  # regenerates bit-identically
+    # the background moves by (3, 1) px: frame 1 == frame 0 shifted, away from the disk
+    f0, f1 = mdf.frame(0).astype(int), mdf.frame(1).astype(int)
+    assert np.abs(f1[11:100, 13:300] - f0[10:99, 10:297]).max() <= 1
