@@ -47,7 +47,9 @@ __device__ __forceinline__ int swz(int r, int c) {
   return CPR == 4 ? r * 4 + (c ^ ((r >> 2) & 3)) : r * 8 + (c ^ ((r >> 1) & 7));
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int BK>
+// GEO: strided input / remapped output pixels (Args geometry fields): the
+// encoder's stride-2 convolutions and the phase-split dgrads of them.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool GEO = false>
 __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
   static_assert(BK == 32 || BK == 64, "BK");
@@ -64,6 +66,8 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   const int H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW, Ktot = a.Ktot;
   const int taps = a.KH * KW;
   const int HW = H * W;
+  // input grid and stride (GEO), else the output grid at stride 1
+  const int Hi = GEO ? a.Hi : H, Wi = GEO ? a.Wi : W, SY = GEO ? a.SY : 1, SX = GEO ? a.SX : 1;
 
   // this thread's staging rows
   const bf16_t* arow[NA];
@@ -114,9 +118,9 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
     _Pragma("unroll") for (int i = 0; i < NA; ++i)                                              \
       ra[i] = ld16(arow[i] + (size_t)tap * Ktot + kseg + c0);                                   \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
-      const int yy = sy[i] + dy, xx = sx[i] + dx;                                               \
-      const bool ok = sb[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;                    \
-      rb[i] = ok ? ld16(sp + ((size_t)(sb[i] * H + yy) * W + xx) * sst + c0 + ((t + 256 * i) % CPR) * 8) \
+      const int yy = sy[i] * SY + dy, xx = sx[i] * SX + dx;                                     \
+      const bool ok = sb[i] >= 0 && yy >= 0 && yy < Hi && xx >= 0 && xx < Wi;                  \
+      rb[i] = ok ? ld16(sp + ((size_t)(sb[i] * Hi + yy) * Wi + xx) * sst + c0 + ((t + 256 * i) % CPR) * 8) \
                  : zero;                                                                        \
     }                                                                                           \
   } while (0)
@@ -181,7 +185,15 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
       py[nt] = px[nt] = 0;
     }
   }
-  epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+  if constexpr (GEO) {
+    int pp[WN];
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt)
+      pp[nt] = (pb[nt] * a.oH + py[nt] * a.OSY + a.OOY) * a.oW + px[nt] * a.OSX + a.OOX;
+    epilogue_pix<WM, WN>(a, acc, m0, lane, pp, pb, py, px);
+  } else {
+    epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
+  }
 }
 
 // ------------------------------------------------------------------ direct-to-LDS variant
@@ -926,6 +938,8 @@ struct ConvLaunch {
   int tile;  // kernel variant (ops/conv.py choose_tile)
   unsigned seg_bytes[3];  // bytes from seg_ptr to the end of its tensor (buffer range checks)
   unsigned w_bytes;
+  int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
+  int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
 };
 
 void conv_launch(const ConvLaunch& L, hipStream_t stream) {
@@ -954,6 +968,23 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     return e ? atoi(e) : 1;
   }();
   a.xcd_remap = xcd_env;
+  if (L.geo) {
+    a.Hi = L.Hi; a.Wi = L.Wi; a.SY = L.SY; a.SX = L.SX;
+    a.oH = L.oH; a.oW = L.oW; a.OSY = L.OSY; a.OSX = L.OSX; a.OOY = L.OOY; a.OOX = L.OOX;
+#define RS_GEO(BM_, BN_, WM_, WN_, BK_)                                                             \
+  hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, WM_, WN_, BK_, true>),                      \
+                     dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
+    switch (L.tile) {
+      case 2: RS_GEO(64, 128, 1, 4, 32); break;
+      case 3: RS_GEO(64, 64, 2, 2, 32); break;
+      case 6: RS_GEO(64, 64, 2, 2, 64); break;
+      case 7: RS_GEO(128, 64, 2, 2, 64); break;
+      case 8: RS_GEO(128, 128, 2, 2, 64); break;
+      default: RS_GEO(128, 64, 2, 2, 32); break;  // 4
+    }
+#undef RS_GEO
+    return;
+  }
   if (L.tile >= 24 && L.tile <= 26) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)
     const int TH = L.tile == 26 ? 4 : 8, BM = L.tile == 25 ? 64 : 128;
     const dim3 grid(cdiv(L.Cout, BM) * L.B * cdiv(L.H, TH) * cdiv(L.W, 16));

@@ -55,6 +55,12 @@ struct Args {
   int xcd_remap;  // conv_glds_kernel: remap block ids so each XCD walks contiguous tiles
   unsigned seg_bytes[3];
   unsigned w_bytes;
+  // strided / remapped geometry (conv_lds_kernel<..., GEO = true> only): the
+  // GEMM pixel grid is B x H x W; GEMM pixel (b, y, x) reads input pixel
+  // (b, y*SY + tap_dy, x*SX + tap_dx) of the Hi x Wi segment grid and writes
+  // output pixel ((b*oH + y*OSY + OOY)*oW + x*OSX + OOX)
+  int Hi, Wi, SY, SX;
+  int oH, oW, OSY, OSX, OOY, OOX;
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }

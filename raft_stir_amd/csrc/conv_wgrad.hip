@@ -42,6 +42,7 @@ struct Args {
   Seg seg[3];
   int nseg;
   int Bp, H, W, P;
+  int Hi, Wi, SY, SX;  // input grid / stride (wgrad_dma_kernel): X pixel = (y*SY + ky - PH, x*SX + kx - PW)
   int KH, KW, PH, PW;
   int Ktot, taps;
   float* dw;
@@ -299,6 +300,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
   if (nsteps == 0) return;
   const int H = a.H, W = a.W, HW = H * W;
+  const int Hi = a.Hi, Wi = a.Wi, SY = a.SY, SX = a.SX;  // X grid and stride
   const int dy_ = tap / a.KW - a.PH, dx_ = tap % a.KW - a.PW;
   const bool do_bias = db != nullptr && ntile == 0;
 
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
   const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);
   const int sper = si == 0 ? s0.period : (si == 1 ? s1.period : s2.period);
   const unsigned sbytes = si == 0 ? a.seg_bytes[0] : (si == 1 ? a.seg_bytes[1] : a.seg_bytes[2]);
-  const int nbs = sper / HW;
+  const int nbs = sper / (Hi * Wi);
   const int cbase = kb - (si == 0 ? 0 : (si == 1 ? c01 : c012));
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)sp, (short)0, sbytes, 0x00020000);
@@ -349,9 +351,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
           (S) * ystep, 0, 0);                                                                   \
     }                                                                                           \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
-      const int y = by[i] + dy_, x = bx[i] + dx_;                                               \
-      const bool ok = brow[i] < rem_ && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W; \
-      const int v = ok ? (((bb[i] * H + y) * W + x) * sst + bch[i]) * 2 : kFar;                 \
+      const int y = by[i] * SY + dy_, x = bx[i] * SX + dx_;                                     \
+      const bool ok = brow[i] < rem_ && (unsigned)y < (unsigned)Hi && (unsigned)x < (unsigned)Wi; \
+      const int v = ok ? (((bb[i] * Hi + y) * Wi + x) * sst + bch[i]) * 2 : kFar;               \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                 \
           rx, (__attribute__((address_space(3))) void*)(st_ + BK * RA + (wbase + NT * i) * 16), \
           16, v, 0, 0, 0);                                                                      \
@@ -612,6 +614,7 @@ struct WgradLaunch {
   unsigned dy_bytes, seg_bytes[3];  // buffer range checks
   int dma;  // 1: buffer-DMA kernel
   float* part;    // deterministic mode: >= wgrad_splits(L) * (Cout*taps*Ktot + Cout) floats, else null
+  int Hi, Wi, SY, SX;  // strided conv (DMA kernel): X grid and stride; 0 = dY's grid, stride 1
 };
 
 namespace {
@@ -671,6 +674,8 @@ void wgrad_launch(const WgradLaunch& L, hipStream_t stream) {
   }
   a.nseg = L.nseg;
   a.Bp = L.Bp; a.H = L.H; a.W = L.W; a.P = L.Bp * L.H * L.W;
+  a.Hi = L.Hi ? L.Hi : L.H; a.Wi = L.Wi ? L.Wi : L.W;
+  a.SY = L.SY ? L.SY : 1; a.SX = L.SX ? L.SX : 1;
   a.KH = L.KH; a.KW = L.KW; a.PH = L.KH / 2; a.PW = L.KW / 2;
   a.Ktot = L.Ktot; a.taps = L.KH * L.KW;
   a.dw = L.dw;

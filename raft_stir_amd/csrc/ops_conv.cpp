@@ -28,6 +28,8 @@ struct ConvLaunch {
   int tile;
   unsigned seg_bytes[3];  // bytes from seg_ptr to the end of its tensor (buffer range checks)
   unsigned w_bytes;
+  int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
+  int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
 };
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
@@ -54,6 +56,7 @@ struct WgradLaunch {
   int bn128;  unsigned dy_bytes, seg_bytes[3];  // buffer range checks
   int dma;  // 1: buffer-DMA kernel
   float* part;  // deterministic mode: split partials (see wgrad_splits), else null
+  int Hi, Wi, SY, SX;  // strided conv (DMA kernel): X grid and stride; 0 = dY's grid, stride 1
 };
 void wgrad_launch(const WgradLaunch& L, hipStream_t stream);
 int wgrad_splits(const WgradLaunch& L);
@@ -211,6 +214,73 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
 
 // convf1 of the motion encoder from coords1 (flow = coords1 - grid), ReLU, bf16
 // NHWC into out[..., ooff:ooff+Cout]; the flow itself (bf16) into fout[..., foff:foff+2].
+// Strided / remapped implicit-GEMM convolution: the encoder's stride-2 3x3 and
+// 1x1 convolutions and the phase-split input gradients of them
+// (ops/enc_conv.py; csrc/conv.hip conv_lds_kernel<..., GEO>).
+//   segs : NHWC bf16 [B, Hi, Wi, Cb], one grid;  GEMM pixel grid B x Ho x Wo
+//   GEMM pixel (b, y, x) reads input (b, y*SY + ky - PH, x*SX + kx - PW) (zero outside)
+//   and writes out[b, y*OSY + OOY, x*OSX + OOX, ooff : ooff + Cout]  (out: NHWC bf16)
+void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C, const Tensor& w,
+              const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t PH, int64_t PW, int64_t SY,
+              int64_t SX, int64_t Ho, int64_t Wo, int64_t Cout, const Tensor& out, int64_t ooff, int64_t OSY,
+              int64_t OSX, int64_t OOY, int64_t OOX, int64_t tile) {
+  TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size(),
+              "conv_geo: 1..3 input segments");
+  TORCH_CHECK(tile == 2 || tile == 3 || tile == 4 || tile == 6 || tile == 7 || tile == 8,
+              "conv_geo: tile must be one of the register-staged variants 2, 3, 4, 6, 7, 8");
+  const int bk = tile >= 6 ? 64 : 32;
+  const int tileM = (tile == 2 || tile == 3 || tile == 6) ? 64 : 128;
+  const int B = segs[0].size(0), Hi = segs[0].size(1), Wi = segs[0].size(2);
+  const c10::DeviceGuard guard(segs[0].device());
+  rs::ConvLaunch L{};
+  int Ktot = 0;
+  for (size_t s = 0; s < 3; ++s) {
+    if (s < segs.size()) {
+      check_nhwc(segs[s], B, Hi, Wi, "conv_geo segment");
+      const int C = seg_C[s], off = seg_off[s], Cb = segs[s].size(3);
+      TORCH_CHECK(C > 0 && C % bk == 0, "conv_geo: segment channels must be a multiple of ", bk, " for tile ", tile);
+      TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb, "conv_geo: segment window");
+      L.seg_ptr[s] = static_cast<const at::BFloat16*>(segs[s].data_ptr()) + off;
+      L.seg_C[s] = C;
+      L.seg_stride[s] = Cb;
+      Ktot += C;
+    } else {
+      L.seg_ptr[s] = L.seg_ptr[0];
+      L.seg_C[s] = bk;
+      L.seg_stride[s] = L.seg_stride[0];
+    }
+  }
+  L.nseg = segs.size();
+  TORCH_CHECK(KH >= 1 && KW >= 1 && SY >= 1 && SX >= 1 && Ho >= 1 && Wo >= 1 && Cout >= 1, "conv_geo: geometry");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3 &&
+                  w.size(1) == KH * KW && w.size(2) == Ktot && w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
+              "conv_geo: packed weight must be bf16 [>= round_up(Cout, ", tileM, ")][KH*KW][Ktot]");
+  if (bias)
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() >= Cout,
+                "conv_geo: bias fp32 (Cout,)");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.scalar_type() == at::kBFloat16 &&
+                  out.size(0) == B && ooff >= 0 && ooff + Cout <= out.size(3),
+              "conv_geo: out must be contiguous NHWC bf16 with room for the channel window");
+  const int oH = out.size(1), oW = out.size(2);
+  TORCH_CHECK(OSY >= 1 && OSX >= 1 && OOY >= 0 && OOX >= 0 && (Ho - 1) * OSY + OOY < oH &&
+                  (Wo - 1) * OSX + OOX < oW,
+              "conv_geo: output pixel map out of bounds");
+  TORCH_CHECK(int64_t(B) * Ho * Wo < (int64_t(1) << 31) && out.numel() < (int64_t(1) << 31), "conv_geo: size");
+  L.w = w.data_ptr();
+  L.bias = bias ? bias->data_ptr<float>() : nullptr;
+  L.B = B; L.H = Ho; L.W = Wo; L.KH = KH; L.KW = KW; L.PH = PH; L.PW = PW;
+  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;
+  L.epi = 0; L.scale = 1.f; L.hd = 0;
+  L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = ooff;
+  L.tile = tile;
+  L.geo = 1;
+  L.Hi = Hi; L.Wi = Wi; L.SY = SY; L.SX = SX;
+  L.oH = oH; L.oW = oW; L.OSY = OSY; L.OSX = OSX; L.OOY = OOY; L.OOX = OOX;
+  rs::conv_launch(L, stream());
+  RS_CHECK_LAUNCH();
+}
+
 void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, const Tensor& out, int64_t ooff,
                  const c10::optional<Tensor>& fout, int64_t foff) {
   TORCH_CHECK(coords.is_cuda() && coords.is_contiguous() && coords.scalar_type() == at::kFloat &&
@@ -287,12 +357,18 @@ void flow_head_dgrad(const Tensor& dflow, const Tensor& w, int64_t cin, const Te
 }
 
 // dW (fp32, [>=Cout][taps][Ktot], accumulated) += sum_p dY[p][yoff + co] X[p + tap][k]
-void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
-                at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH, int64_t KW,
-                const Tensor& dw, const c10::optional<Tensor>& db, int64_t bn128) {
+// SY, SX > 1: a strided conv; the segments are on the INPUT grid (any Hi x Wi,
+// X pixel = (y*SY + ky - KH/2, x*SX + kx - KW/2)), buffer-DMA kernel only.
+void conv_wgrad_impl(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
+                     at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH,
+                     int64_t KW, const Tensor& dw, const c10::optional<Tensor>& db, int64_t bn128, int64_t SY,
+                     int64_t SX) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 4 && dy.scalar_type() == at::kBFloat16,
               "conv_wgrad: dy must be contiguous bf16 NHWC");
   const int Bp = dy.size(0), H = dy.size(1), W = dy.size(2);
+  const bool strided = SY != 1 || SX != 1;
+  TORCH_CHECK(SY >= 1 && SX >= 1, "conv_wgrad: stride >= 1");
+  const int Hi = strided ? segs.at(0).size(1) : H, Wi = strided ? segs.at(0).size(2) : W;
   static const int dma_env = [] {
     const char* e = getenv("RS_WGRAD_DMA");
     return e ? atoi(e) : 1;
@@ -314,11 +390,12 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
     if (s < segs.size()) {
       const Tensor& t = segs[s];
       TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4 && t.scalar_type() == at::kBFloat16 &&
-                      t.size(1) == H && t.size(2) == W,
-                  "conv_wgrad: segment must be contiguous bf16 NHWC with dy's spatial size");
+                      t.size(1) == Hi && t.size(2) == Wi,
+                  "conv_wgrad: segment must be contiguous bf16 NHWC with dy's spatial size (the input grid "
+                  "when strided)");
       const int per = seg_period[s];
-      TORCH_CHECK(per == t.size(0) * H * W && (Bp * H * W) % per == 0,
-                  "conv_wgrad: segment period must be its pixel count and divide dy's");
+      TORCH_CHECK(per == t.size(0) * Hi * Wi && Bp % t.size(0) == 0,
+                  "conv_wgrad: segment period must be its pixel count and its images divide dy's");
       const int C = seg_C[s], off = seg_off[s];
       TORCH_CHECK(C % 64 == 0 && off % 8 == 0 && off + C <= t.size(3), "conv_wgrad: segment window (C % 64)");
       L.seg_ptr[s] = static_cast<const at::BFloat16*>(t.data_ptr()) + off;
@@ -344,6 +421,8 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   TORCH_CHECK(dy.numel() * 2 < (int64_t(1) << 31), "conv_wgrad: dY tensor must be < 2 GiB");
   L.dy_bytes = (unsigned)(dy.numel() * 2);
   L.dma = dma_env;
+  TORCH_CHECK(!strided || L.dma, "conv_wgrad: strided weight gradients need the buffer-DMA kernels");
+  L.Hi = Hi; L.Wi = Wi; L.SY = SY; L.SX = SX;
   L.nseg = segs.size();
   L.Bp = Bp; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.Ktot = Ktot;
   L.dw = dw.data_ptr<float>();
@@ -359,6 +438,20 @@ void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<
   }
   rs::wgrad_launch(L, stream());
   RS_CHECK_LAUNCH();
+}
+
+void conv_wgrad(const Tensor& dy, int64_t yoff, int64_t Cout, const std::vector<Tensor>& segs,
+                at::IntArrayRef seg_off, at::IntArrayRef seg_C, at::IntArrayRef seg_period, int64_t KH, int64_t KW,
+                const Tensor& dw, const c10::optional<Tensor>& db, int64_t bn128) {
+  conv_wgrad_impl(dy, yoff, Cout, segs, seg_off, seg_C, seg_period, KH, KW, dw, db, bn128, 1, 1);
+}
+
+void conv_wgrad_strided(const Tensor& dy, int64_t Cout, const std::vector<Tensor>& segs, at::IntArrayRef seg_off,
+                        at::IntArrayRef seg_C, int64_t KH, int64_t KW, int64_t SY, int64_t SX, const Tensor& dw,
+                        const c10::optional<Tensor>& db) {
+  std::vector<int64_t> per;
+  for (const auto& t : segs) per.push_back(t.size(0) * t.size(1) * t.size(2));
+  conv_wgrad_impl(dy, 0, Cout, segs, seg_off, seg_C, per, KH, KW, dw, db, 0, SY, SX);
 }
 
 void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
@@ -443,23 +536,30 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("flow_head_dgrad(Tensor dflow, Tensor w, int cin, Tensor act, int aoff, Tensor(a!) out, int ooff) -> ()");
   m.def("colsum(Tensor dy, int yoff, int C, Tensor(a!) db) -> ()");
   m.def("flow_wgrad(Tensor coords, Tensor df, Tensor(a!) dw, Tensor(b!) db) -> ()");
+  m.def("conv_wgrad_strided(Tensor dy, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int KH, int KW, "
+        "int SY, int SX, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("gru_gate_bwd(Tensor(a!) dh, Tensor z, Tensor q, Tensor h, int hoff, Tensor(b!) dq, Tensor(c!) dzr) -> ()");
   m.def("relu_take(Tensor(a!) G, int goff, int n, int nz, Tensor act, int aoff, Tensor(b!) out) -> ()");
   m.def("conv_fused(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, "
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile) -> ()");
+  m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
+        "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
+        "int OOX, int tile) -> ()");
   m.def("flow_encode(Tensor coords, Tensor w, Tensor bias, Tensor(a!) out, int ooff, Tensor(b!)? fout, "
         "int foff) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
+  m.impl("conv_geo", &conv_geo);
   m.impl("flow_encode", &flow_encode);
   m.impl("flow_head", &flow_head);
   m.impl("flow_head_dgrad", &flow_head_dgrad);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("colsum", &colsum);
   m.impl("flow_wgrad", &flow_wgrad);
+  m.impl("conv_wgrad_strided", &conv_wgrad_strided);
   m.impl("gru_gate_bwd", &gru_gate_bwd);
   m.impl("relu_take", &relu_take);
 }

@@ -13,8 +13,10 @@ Parameter/buffer names are kept identical so reference ``.pth`` files load
 unchanged (including the aliased ``normK`` / ``downsample.1`` pair that the
 reference creates by registering the same norm module twice).
 
-MI355X notes: the encoders run once per image pair; their convolutions go
-through MIOpen in channels_last (NHWC) bf16 under autocast, and every
+MI355X notes: the encoders run once per image pair; on the GPU bf16 path
+their 3x3 (stride 1 and 2) and 1x1 convolutions run on the hand-written
+implicit-GEMM kernels (ops/enc_conv.py; only the 7x7 stem with its 3 input
+channels, and RAFT-small's narrow bottleneck convs, stay on MIOpen), and every
 norm -> ReLU (-> residual add -> ReLU) chain is one fused NHWC pass of
 csrc/norm.hip (ops/norm.py) instead of PyTorch's instance_norm, which would
 copy each channels_last map to NCHW and back.  NHWC also keeps the 1x1
@@ -26,8 +28,9 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops import enc_conv
 from ..ops.fp32conv import conv_module
-from ..ops.norm import conv_norm_act
+from ..ops.norm import conv_norm_act, conv_pair_norm_act
 
 
 def make_norm(kind: str, channels: int, groups: int) -> nn.Module:
@@ -60,8 +63,10 @@ class ResidualBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm3)
 
     def forward(self, x):
-        y = conv_norm_act(self.conv1, self.norm1, x)
-        skip = x if self.downsample is None else conv_norm_act(self.downsample[0], self.norm3, x, relu=False)
+        if self.downsample is None:
+            y, skip = conv_norm_act(self.conv1, self.norm1, x), x
+        else:
+            y, skip = conv_pair_norm_act(self.conv1, self.norm1, self.downsample[0], self.norm3, x)
         # relu(skip + relu(norm2(conv2(y)))) as one fused pass on GPU
         return conv_norm_act(self.conv2, self.norm2, y, relu=True, residual=skip)
 
@@ -145,12 +150,18 @@ class _Encoder(nn.Module):
             fns.extend(layer)
 
         def head(x):
-            x = conv_module(self.conv2, x)
+            x = self._head_conv(x)
             if self.training and self.dropout is not None:
                 x = self.dropout(x)
             return x
         fns.append(head)
         return fns
+
+    def _head_conv(self, x):
+        """1x1 projection (with bias): HIP implicit GEMM on the GPU bf16 path."""
+        if enc_conv.eligible_geo(self.conv2, x):
+            return enc_conv.conv_geo(self.conv2, x)
+        return conv_module(self.conv2, x)
 
     def forward(self, x):
         pair = isinstance(x, (list, tuple))
@@ -159,7 +170,7 @@ class _Encoder(nn.Module):
             x = torch.cat(list(x), dim=0)
         x = conv_norm_act(self.conv1, self.norm1, x)
         x = self.layer3(self.layer2(self.layer1(x)))
-        x = conv_module(self.conv2, x)
+        x = self._head_conv(x)
         if self.training and self.dropout is not None:
             x = self.dropout(x)
         if pair:

@@ -75,7 +75,8 @@ class FusedUpdate:
 
     # ------------------------------------------------------------ weights
     def _version_key(self):
-        return tuple((p.data_ptr(), p._version) for p in self.model.update_block.parameters())
+        from ..runtime.weights import generation
+        return (generation(),) + tuple((p.data_ptr(), p._version) for p in self.model.update_block.parameters())
 
     @torch.no_grad()
     def _pack(self):
@@ -168,13 +169,18 @@ class FusedUpdate:
 
     # ------------------------------------------------------------ run
     @torch.no_grad()
-    def run(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+    def refresh(self):
+        """Re-pack after a weight update, into the existing storage."""
         k = self._version_key()
         if k != self.key:
             old = self.__dict__.copy()
             self._pack()
             self._reuse_storage(old)
             self.key = k
+
+    @torch.no_grad()
+    def run(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        self.refresh()
         B, _, H, W = coords1.shape
         bufs = self._buffers(B, H, W, coords1.device)
         hx = bufs["hx"]

@@ -33,6 +33,7 @@ import torch.nn as nn
 from ..config import RAFTConfig, resolve_config
 from ..ops import _ext
 from ..ops import gru as gru_ops
+from ..ops import wpack
 from ..ops import reference as ref
 from ..ops.upsample import convex_upsample, upflow8
 from .corr import CorrBlock, AlternateCorrBlock
@@ -153,6 +154,10 @@ class RAFT(nn.Module):
         # once per forward instead of once per iteration (and its gradient
         # accumulates over the 12 iterations before a single cast back).
         gru_ops.begin_forward()
+        if gpu:
+            # packed encoder-conv weights after an optimizer step: one batched
+            # repack on the main stream, before any stream forks (ops/wpack.py)
+            wpack.refresh()
         # The context encoder (batch B) and the feature encoder + correlation
         # volume (batch 2B) are independent until the update loop: run cnet on
         # a second HIP stream so its small kernels (norm finalize, bias, ReLU

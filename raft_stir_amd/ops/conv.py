@@ -27,7 +27,8 @@ def pad_to(n: int, m: int) -> int:
 
 
 @torch.no_grad()
-def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int) -> torch.Tensor:
+def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int,
+                dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     cout, cin, kh, kw = weight.shape
     taps = kh * kw
     wt = weight.detach().float().permute(0, 2, 3, 1).reshape(cout, taps, cin)
@@ -40,7 +41,7 @@ def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int) ->
             assert s0 + n <= c and w0 + n <= cin
             out[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
         kb += c
-    return out.to(torch.bfloat16).contiguous()
+    return out.to(dtype).contiguous()
 
 
 @torch.no_grad()

@@ -19,12 +19,11 @@ convolutions have none.
 from __future__ import annotations
 
 import os
-import weakref
 
 import torch
 import torch.nn as nn
 
-from . import _ext
+from . import _ext, wpack
 from .conv import EPI_BIAS, conv_fused, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
@@ -74,32 +73,18 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1)
 
 
-# Packed bf16 weights per (parameter, layout), repacked when the parameter
-# changes (optimizer step / load_state_dict bump its version).  A repack is
-# copied into the previous storage so a captured hipGraph keeps reading the
-# live tensor; no packing kernels run inside a graph replay.  Entries hold a
-# weak reference to their parameter and are dropped when it dies, so a new
-# parameter that reuses a dead one's id() never sees its packed copy.
-_PACKED = {}
+# Packed bf16 weights: every layout is a static index map into the source
+# parameters, all repacked together in three kernels after each optimizer
+# step (ops/wpack.py).
+_F32 = torch.float32
 
 
 def _packed(weight: torch.Tensor, dgrad: bool) -> torch.Tensor:
-    key = (id(weight), dgrad)
-    ver = (weight.data_ptr(), weight._version, weight.device, tuple(weight.shape))
-    ent = _PACKED.get(key)
-    if ent is not None and ent[0]() is weight and ent[1] == ver:
-        return ent[2]
     cout, cin = weight.shape[:2]
     if dgrad:
-        new = pack_weight(weight.transpose(0, 1).flip(2, 3), [(cout, [(0, cout, 0)])], pad_to(cin, 128))
-    else:
-        new = pack_weight(weight, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
-    if ent is not None and ent[0]() is weight and ent[2].shape == new.shape and ent[2].device == new.device:
-        ent[2].copy_(new)
-        new = ent[2]
-    ref = weakref.ref(weight, lambda _r, k=key: _PACKED.pop(k, None))
-    _PACKED[key] = (ref, ver, new)
-    return new
+        return wpack.packed(("s1_dgrad", id(weight)), [weight], lambda ws: pack_weight(
+            ws[0].transpose(0, 1).flip(2, 3), [(cout, [(0, cout, 0)])], pad_to(cin, 128), _F32))
+    return _fwd_weight(weight)
 
 
 class _Conv3x3(torch.autograd.Function):
@@ -153,3 +138,245 @@ class _Conv3x3(torch.autograd.Function):
 def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """conv(x) without its bias (see :func:`eligible`)."""
     return _Conv3x3.apply(x, conv.weight)
+
+
+# ----------------------------------------------------------------- strided / 1x1
+# The rest of the encoder convolutions (reference core/extractor.py:10, 44, 65,
+# 103, 144): the stride-2 3x3 first conv of stages 2 and 3, the stride-2 1x1
+# downsample shortcut beside it, and the 1x1 projection head.  All on
+# csrc/conv.hip's register-staged implicit GEMM in its strided geometry
+# (torch.ops.raft_stir.conv_geo) and csrc/conv_wgrad.hip's strided weight
+# gradient (conv_wgrad_strided):
+#
+#   forward : GEMM pixel (y, x) reads input (y*S + ky - P, x*S + kx - P)
+#   dgrad   : split by the PARITY of the input pixel (phase r = i mod S): only
+#             taps k = (r + P) mod S contribute, each from dY at offset
+#             d = (r + P - k) / S, so every phase is a dense stride-1 conv of
+#             dY with a 1x1 / 1x2 / 2x1 / 2x2 sub-kernel whose outputs land on
+#             every S-th input pixel (no zero-tap MACs, no col2im, no atomics);
+#             the 1x1 shortcut only has the (0, 0) phase and is fused into the
+#             3x3's (0, 0) phase as a second K segment (conv_pair)
+#   wgrad   : split-K MFMA over dY pixels with strided X rows
+_GEO = os.environ.get("RS_ENC_GEO", "1") != "0"
+
+
+def _geo_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (_ENABLED and _GEO) or x.dtype != torch.bfloat16 or x.dim() != 4 or not _ext.use_hip(x):
+        return False
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros" or isinstance(p, str):
+        return False
+    shape_ok = (k == (3, 3) and s == (2, 2) and p == (1, 1)) or (k == (1, 1) and p == (0, 0) and s in ((1, 1), (2, 2)))
+    cin, cout = conv.in_channels, conv.out_channels
+    return (shape_ok and cin % 32 == 0 and cin >= 64 and cout % 32 == 0 and x.is_contiguous(memory_format=_CL)
+            and x.numel() * 2 < (1 << 31))
+
+
+def eligible_geo(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Strided 3x3 / strided or plain 1x1 encoder conv on the HIP kernels."""
+    return _geo_ok(conv, x)
+
+
+def _phase_taps(k: int, s: int, p: int, r: int):
+    """Taps k' (ascending dY offset d) feeding input phase r: [(d, k'), ...]."""
+    return sorted(((r + p - kk) // s, kk) for kk in range(k) if (r + p - kk) % s == 0)
+
+
+def _fwd_weight(weight):
+    cout, cin = weight.shape[:2]
+    return wpack.packed(("fwd", id(weight)), [weight],
+                        lambda ws: pack_weight(ws[0], [(cin, [(0, cin, 0)])], pad_to(cout, 128), _F32))
+
+
+def _phase_weight(weights, ry, rx, strides, pads):
+    """Packed dgrad weight of phase (ry, rx) of one strided conv:
+    [pad128(Cin)][kh' * kw'][Cout]."""
+    assert len(weights) == 1, "several convs share a phase weight through _pair_phase_weight"
+    w0 = weights[0]
+    cout, cin, kh, kw = w0.shape
+    ty = _phase_taps(kh, strides[0], pads[0], ry)
+    tx = _phase_taps(kw, strides[1], pads[1], rx)
+
+    def layout(ws):
+        sub = ws[0][:, :, [k for _, k in ty]][:, :, :, [k for _, k in tx]]  # [cout, cin, kh', kw']
+        return pack_weight(sub.transpose(0, 1), [(cout, [(0, cout, 0)])], pad_to(cin, 128), _F32)
+    return wpack.packed(("phase", id(w0), ry, rx, tuple(strides), tuple(pads)), [w0], layout)
+
+
+def _geo_tile(cout: int, chans) -> int:
+    k64 = all(c % 64 == 0 for c in chans)
+    if cout > 64:
+        return 7 if k64 else 4
+    return 6 if k64 else 3
+
+
+def _conv_geo_fwd(x, weight, bias, stride, pad):
+    xn = _nhwc(x)
+    N, Hi, Wi, cin = xn.shape
+    cout, _, kh, kw = weight.shape
+    Ho = (Hi + 2 * pad[0] - kh) // stride[0] + 1
+    Wo = (Wi + 2 * pad[1] - kw) // stride[1] + 1
+    out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.bfloat16)
+    b = None if bias is None else bias.detach().float().contiguous()
+    torch.ops.raft_stir.conv_geo([xn], [0], [cin], _fwd_weight(weight), b, kh, kw, pad[0], pad[1], stride[0],
+                                 stride[1], Ho, Wo, cout, out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]))
+    return out
+
+
+def _conv_geo_dgrad(dys, weights, x_shape, stride, pad):
+    """dX (NHWC bf16) of convs sharing the input: sum over ``weights`` of
+    their input gradients from ``dys`` (NHWC bf16 output gradients)."""
+    N, cin, Hi, Wi = x_shape
+    kh, kw = weights[0].shape[2:]
+    Ho, Wo = dys[0].shape[1:3]
+    sy, sx = stride
+    phases = []
+    for ry in range(sy):
+        for rx in range(sx):
+            use = [i for i, w in enumerate(weights)
+                   if _phase_taps(w.shape[2], sy, pad[0], ry) and _phase_taps(w.shape[3], sx, pad[1], rx)]
+            phases.append((ry, rx, use))
+    full = all(len(u) > 0 for _, _, u in phases)
+    dx = (torch.empty if full else torch.zeros)(N, Hi, Wi, cin, device=dys[0].device, dtype=torch.bfloat16)
+    for ry, rx, use in phases:
+        if not use:
+            continue
+        mh, mw = -(-(Hi - ry) // sy), -(-(Wi - rx) // sx)
+        if mh <= 0 or mw <= 0:
+            continue
+        ws = [weights[i] for i in use]
+        ty = _phase_taps(ws[0].shape[2], sy, pad[0], ry)
+        tx = _phase_taps(ws[0].shape[3], sx, pad[1], rx)
+        for w in ws[1:]:  # fused K segments must share the sub-kernel
+            assert _phase_taps(w.shape[2], sy, pad[0], ry) == ty and _phase_taps(w.shape[3], sx, pad[1], rx) == tx
+        wp = _phase_weight(ws, ry, rx, stride, pad)
+        chans = [weights[i].shape[0] for i in use]
+        torch.ops.raft_stir.conv_geo([dys[i] for i in use], [0] * len(use), chans, wp, None, len(ty), len(tx),
+                                     -ty[0][0], -tx[0][0], 1, 1, mh, mw, cin, dx, 0, sy, sx, ry, rx,
+                                     _geo_tile(cin, chans))
+    return dx
+
+
+def _conv_geo_wgrad(dy, x, weight, stride, want_bias):
+    """(dW, db) of a strided / 1x1 conv: split-K MFMA over dY pixels."""
+    xn = _nhwc(x)
+    cin = xn.shape[3]
+    cout, _, kh, kw = weight.shape
+    segs = [(0, cin)] if cin % 64 == 0 else [(0, cin - 32), (cin - 64, 64)]
+    ktot = sum(c for _, c in segs)
+    acc = torch.zeros(pad_to(cout, 128), kh * kw, ktot, device=x.device, dtype=torch.float32)
+    db = torch.zeros(cout, device=x.device, dtype=torch.float32) if want_bias else None
+    torch.ops.raft_stir.conv_wgrad_strided(dy, cout, [xn] * len(segs), [o for o, _ in segs], [c for _, c in segs],
+                                           kh, kw, stride[0], stride[1], acc, db)
+    acc = acc[:cout]
+    if len(segs) > 1:
+        acc = torch.cat([acc[..., :cin - 32], acc[..., cin:cin + 32]], -1)
+    dw = acc.view(cout, kh, kw, cin).permute(0, 3, 1, 2).to(weight.dtype)
+    return dw, (db.to(weight.dtype) if db is not None else None)
+
+
+class _ConvGeo(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad):
+        out = _conv_geo_fwd(x, weight, bias, stride, pad)
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dyn = _nhwc(dy.to(torch.bfloat16))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_geo_dgrad([dyn], [weight], x.shape, ctx.stride, ctx.pad).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = _conv_geo_wgrad(dyn, x, weight, ctx.stride, ctx.has_bias and ctx.needs_input_grad[2])
+        return dx, dw, db, None, None
+
+
+def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
+    """conv(x) on the HIP kernels (see :func:`eligible_geo`); ``bias=False``
+    drops the conv's bias (folded into a following normalisation)."""
+    b = conv.bias if bias else None
+    return _ConvGeo.apply(x, conv.weight, b, tuple(conv.stride), tuple(conv.padding))
+
+
+class _ConvPair(torch.autograd.Function):
+    """The stride-2 3x3 conv and the stride-2 1x1 shortcut of a residual
+    block's first conv (both read the block input, no biases): one input
+    gradient, with the shortcut's term fused into the 3x3's (0, 0) phase."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, stride):
+        y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1))
+        yd = _conv_geo_fwd(x, wd, None, stride, (0, 0))
+        ctx.save_for_backward(x, w1, wd)
+        ctx.stride = stride
+        return y1.permute(0, 3, 1, 2), yd.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy1, dyd):
+        x, w1, wd = ctx.saved_tensors
+        s = ctx.stride
+        d1 = _nhwc(dy1.to(torch.bfloat16))
+        dd = _nhwc(dyd.to(torch.bfloat16))
+        dx = dw1 = dwd = None
+        if ctx.needs_input_grad[0]:
+            dx = _pair_dgrad(d1, dd, w1, wd, x.shape, s).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dw1, _ = _conv_geo_wgrad(d1, x, w1, s, False)
+        if ctx.needs_input_grad[2]:
+            dwd, _ = _conv_geo_wgrad(dd, x, wd, s, False)
+        return dx, dw1, dwd, None
+
+
+def _pair_dgrad(d1, dd, w1, wd, x_shape, stride):
+    N, cin, Hi, Wi = x_shape
+    dx = torch.empty(N, Hi, Wi, cin, device=d1.device, dtype=torch.bfloat16)
+    sy, sx = stride
+    for ry in range(sy):
+        for rx in range(sx):
+            mh, mw = -(-(Hi - ry) // sy), -(-(Wi - rx) // sx)
+            ty = _phase_taps(3, sy, 1, ry)
+            tx = _phase_taps(3, sx, 1, rx)
+            shortcut = bool(_phase_taps(1, sy, 0, ry) and _phase_taps(1, sx, 0, rx))
+            if shortcut:  # (0, 0): the centre tap of the 3x3 and the 1x1, as two K segments
+                assert len(ty) == 1 and len(tx) == 1 and ty[0][0] == 0 and tx[0][0] == 0
+                ws, dys = [w1, wd], [d1, dd]
+            else:
+                ws, dys = [w1], [d1]
+            wp = _pair_phase_weight(ws, ry, rx, stride)
+            chans = [w.shape[0] for w in ws]
+            torch.ops.raft_stir.conv_geo(dys, [0] * len(ws), chans, wp, None, len(ty), len(tx), -ty[0][0],
+                                         -tx[0][0], 1, 1, mh, mw, cin, dx, 0, sy, sx, ry, rx, _geo_tile(cin, chans))
+    return dx
+
+
+def _pair_phase_weight(ws, ry, rx, stride):
+    """Phase (ry, rx) dgrad weight of the 3x3/s2 conv, with the 1x1/s2
+    shortcut appended as a second K segment on the (0, 0) phase."""
+    cout, cin = ws[0].shape[:2]
+    ty = _phase_taps(3, stride[0], 1, ry)
+    tx = _phase_taps(3, stride[1], 1, rx)
+
+    def layout(ts):
+        blocks = [ts[0][:, :, [k for _, k in ty]][:, :, :, [k for _, k in tx]].transpose(0, 1)]
+        if len(ts) > 1:  # the 1x1 shortcut: the same 1x1 sub-kernel (centre tap)
+            blocks.append(ts[1].transpose(0, 1))
+        segs, o = [], 0
+        for t in ts:
+            segs.append((t.shape[0], [(o, t.shape[0], 0)]))
+            o += t.shape[0]
+        return pack_weight(torch.cat(blocks, 1), segs, pad_to(cin, 128), _F32)
+    return wpack.packed(("pair", id(ws[0]), ry, rx, len(ws)), list(ws), layout)
+
+
+def pair_eligible(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor) -> bool:
+    return (_geo_ok(conv1, x) and _geo_ok(down, x) and conv1.kernel_size == (3, 3) and conv1.stride == (2, 2)
+            and down.kernel_size == (1, 1) and down.stride == (2, 2) and down.out_channels == conv1.out_channels)
+
+
+def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor):
+    """(conv1(x), down(x)) without biases (both folded into their norms)."""
+    return _ConvPair.apply(x, conv1.weight, down.weight, tuple(conv1.stride))

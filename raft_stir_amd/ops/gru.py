@@ -80,7 +80,8 @@ def _weights(convz, convr, convq, dt):
     # used outside RAFT.forward (no begin_forward) or a new module reusing a
     # freed one's id must never see stale weights
     ps = (convz.weight, convz.bias, convr.weight, convr.bias, convq.weight, convq.bias)
-    key = (id(convz), dt) + tuple((p.data_ptr(), p._version) for p in ps)
+    from ..runtime.weights import generation
+    key = (id(convz), dt, generation()) + tuple((p.data_ptr(), p._version) for p in ps)
     w = _WCACHE.get(key)
     if w is None:
         if len(_WCACHE) > 32:

@@ -154,5 +154,22 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
         return norm_act(norm, conv(x), relu, residual)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
         return norm_act(norm, enc_conv.conv3x3(conv, x), relu, residual, bias=conv.bias)
+    if enc_conv.eligible_geo(conv, x):  # stride-2 3x3 / 1x1 (strided geometry of the same kernels)
+        return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False), relu, residual, bias=conv.bias)
     y = fp32conv.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return norm_act(norm, y, relu, residual, bias=conv.bias)
+
+
+def conv_pair_norm_act(conv1: nn.Conv2d, norm1: nn.Module, down: nn.Conv2d, norm_d: nn.Module, x: torch.Tensor):
+    """(norm_act(norm1, conv1(x)), norm_act(norm_d, down(x), relu=False)) for a
+    residual block's stride-2 first conv and its stride-2 1x1 shortcut: on the
+    GPU path both convs are one autograd node (ops/enc_conv.py conv_pair) whose
+    backward produces ONE input gradient (the shortcut's term fused into the
+    3x3's (0, 0) phase) instead of two dgrads and an add."""
+    fold = (conv1.bias is not None and down.bias is not None and _FOLD_BIAS and _ext.use_hip(x)
+            and _norm_kind_ok(norm1) and _norm_kind_ok(norm_d))
+    if fold and enc_conv.pair_eligible(conv1, down, x):
+        y1, yd = enc_conv.conv_pair(conv1, down, x)
+        return (norm_act(norm1, y1, True, None, bias=conv1.bias),
+                norm_act(norm_d, yd, False, None, bias=down.bias))
+    return conv_norm_act(conv1, norm1, x), conv_norm_act(down, norm_d, x, relu=False)

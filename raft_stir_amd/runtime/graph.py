@@ -15,6 +15,8 @@ from typing import Dict, Tuple
 
 import torch
 
+from .weights import refresh_all, repack_in_graph, weights_key
+
 
 class GraphedInference:
     def __init__(self, model, shape, iters=12, warm_start=False, warmup=2, pool=None):
@@ -35,6 +37,7 @@ class GraphedInference:
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph, pool=pool):
             self.out = self._run()
+        self._wkey = weights_key(model)
 
     def _run(self):
         return self.model(self.i1, self.i2, iters=self.iters, flow_init=self.flow_init,
@@ -49,6 +52,10 @@ class GraphedInference:
                 self.flow_init.zero_()
             else:
                 self.flow_init.copy_(flow_init)
+        key = weights_key(self.model)
+        if key != self._wkey:  # weights moved since capture: re-pack into the captured storage
+            refresh_all(self.model)
+            self._wkey = key
         self.graph.replay()
         return self.out
 
@@ -116,10 +123,14 @@ class GraphedTrainStep:
         torch.cuda.current_stream(dev).wait_stream(s)
         optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # the step's own optimizer update moves the weights: record the
+        # weight-packing kernels too, so every replay packs the current weights
+        with torch.cuda.graph(self.graph), repack_in_graph():
             self.loss = self._body()
 
     def _body(self):
+        from ..ops import wpack
+        wpack.repack()  # recorded: every replay packs the weights its own optimizer step wrote
         i1, i2, flow, valid = self.static
         preds = self.model(i1, i2, iters=self.iters)
         loss = self.loss_fn(preds, flow, valid)

@@ -153,3 +153,37 @@ def test_deterministic_flag_plumbing():
     assert not resolve_config(make_args()).deterministic
     a = build_parser().parse_args(["--deterministic"])
     assert a.deterministic
+
+
+def test_fused_adamw_does_not_bump_version_but_generation_moves():
+    """Why the packed-weight caches key on runtime.weights.generation(): an
+    optimizer step may update parameters without bumping ``_version``
+    (fused / foreach kernels); the global post-step hook always fires."""
+    from raft_stir_amd.runtime import weights as wg
+    p = torch.nn.Parameter(torch.randn(4))
+    opt = torch.optim.SGD([p], lr=0.1, foreach=True)
+    p.grad = torch.ones(4)
+    g0 = wg.generation()
+    opt.step()
+    assert wg.generation() == g0 + 1
+
+
+def test_wpack_batched_layouts_follow_updates():
+    """ops/wpack.py: layouts registered as index maps into the parameters,
+    all views of one flat buffer, repacked together after an optimizer step
+    (which need not bump _version) and equal to the direct layout."""
+    from raft_stir_amd.ops import wpack
+    from raft_stir_amd.ops.conv import pack_weight, pad_to
+    torch.manual_seed(0)
+    w1 = torch.nn.Parameter(torch.randn(96, 64, 3, 3))
+    w2 = torch.nn.Parameter(torch.randn(96, 64, 1, 1))
+    lay1 = lambda ws: pack_weight(ws[0], [(64, [(0, 64, 0)])], 128, torch.float32)
+    lay2 = lambda ws: pack_weight(torch.cat([ws[0][:, :, 1:2, 1:2], ws[1]], 0).transpose(0, 1),
+                                  [(192, [(0, 192, 0)])], 128, torch.float32)
+    for step in range(3):
+        a = wpack.packed(("t1", id(w1)), [w1], lay1)
+        b = wpack.packed(("t2", id(w1), id(w2)), [w1, w2], lay2)
+        assert torch.equal(a, lay1([w1.detach()]).to(torch.bfloat16))
+        assert torch.equal(b, lay2([w1.detach(), w2.detach()]).to(torch.bfloat16))
+        w1.grad, w2.grad = torch.randn_like(w1), torch.randn_like(w2)
+        torch.optim.SGD([w1, w2], lr=0.5, foreach=True).step()
