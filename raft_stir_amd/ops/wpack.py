@@ -110,6 +110,7 @@ class _Registry:
     @torch.no_grad()
     def repack(self):
         """Every registered layout from the current parameter values (3 kernels)."""
+        STATS["repacks"] += 1
         live = {k: e for k, e in self.entries.items() if all(r() is not None for r in e.refs)}
         if len(live) != len(self.entries):
             self.entries, self.dirty = live, True
@@ -156,6 +157,7 @@ class _Registry:
 
 
 _REGS: Dict[torch.device, _Registry] = {}  # one per device
+STATS = {"repacks": 0}  # tests / scripts: how often everything was repacked
 
 
 def packed(key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
