@@ -76,17 +76,30 @@ __global__ __launch_bounds__(256) void flowhead_fwd_kernel(const bf16_t* __restr
   float acc[PX * 2];
 #pragma unroll
   for (int i = 0; i < PX * 2; ++i) acc[i] = 0.f;
+  // all 3 x (PX + 2) neighbourhood loads are unconditional (clamped address,
+  // 0/1 factor outside the image), so they are issued back to back and the
+  // wave waits for memory once instead of once per load
+  float v3[3][PX + 2][CPL];
 #pragma unroll
   for (int ty = 0; ty < 3; ++ty) {
     const int yy = y + ty - 1;
-    if (yy < 0 || yy >= H) continue;  // wave-uniform
-    const bf16_t* row = x + ((size_t)(b * H + yy) * W) * xstr + xoff + lane * CPL;
+    const bool iny = yy >= 0 && yy < H;
+    const bf16_t* row = x + ((size_t)(b * H + (iny ? yy : y)) * W) * xstr + xoff + lane * CPL;
 #pragma unroll
     for (int c = 0; c < PX + 2; ++c) {
       const int xx = x0 + c - 1;
-      if (xx < 0 || xx >= W) continue;  // wave-uniform
-      float v[CPL];
-      ldc<CPL>(row + (size_t)xx * xstr, v);
+      const bool in = iny && xx >= 0 && xx < W;
+      ldc<CPL>(row + (size_t)(in ? xx : x0) * xstr, v3[ty][c]);
+      const float m = in ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) v3[ty][c][j] *= m;
+    }
+  }
+#pragma unroll
+  for (int ty = 0; ty < 3; ++ty) {
+#pragma unroll
+    for (int c = 0; c < PX + 2; ++c) {
+      const float (&v)[CPL] = v3[ty][c];
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx) {
         const int px = c - tx;  // output pixel x0 + px uses input column x0 + px + tx - 1
@@ -168,6 +181,13 @@ __global__ __launch_bounds__(256) void flowhead_dgrad_kernel(const float* __rest
       g[r][c][1] = in ? dflow[o + plane] : 0.f;
     }
   }
+  // the hidden activations of the PX pixels (ReLU mask), loaded up front
+  float av[PX][CPL];
+#pragma unroll
+  for (int px = 0; px < PX; ++px) {
+    const int xc = x0 + px < W ? x0 + px : W - 1;
+    ldc<CPL>(act + ((size_t)(b * H + y) * W + xc) * astr + aoff + lane * CPL, av[px]);
+  }
 #pragma unroll
   for (int px = 0; px < PX; ++px) {
     if (x0 + px >= W) break;
@@ -185,10 +205,8 @@ __global__ __launch_bounds__(256) void flowhead_dgrad_kernel(const float* __rest
           acc[j] = fmaf(g0, wr[0][ty * 3 + tx][j], fmaf(g1, wr[1][ty * 3 + tx][j], acc[j]));
       }
     const size_t p = (size_t)(b * H + y) * W + x0 + px;
-    float a[CPL];
-    ldc<CPL>(act + p * astr + aoff + lane * CPL, a);
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) acc[j] = a[j] > 0.f ? acc[j] : 0.f;
+    for (int j = 0; j < CPL; ++j) acc[j] = av[px][j] > 0.f ? acc[j] : 0.f;
     stc<CPL>(out + p * ostr + ooff + lane * CPL, acc);
   }
 }
