@@ -814,97 +814,6 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(Args a) {
   }
 }
 
-// ------------------------------------------------------------------ flow encoder
-// convf1 of the motion encoder (reference core/update.py:67,84): a 7x7 conv
-// of the 2-channel flow (= coords1 - coords0, computed here from coords1)
-// with ReLU, written as bf16 NHWC.  K = 98 per output: a VALU kernel in fp32
-// (the flow can be ~100 px at 1/8 resolution; bf16 operands would quantise
-// it to 0.5 px).  It also writes the flow itself (bf16) into its slot of the
-// GRU input buffer (reference: cat([out, flow]) in the motion encoder).
-//
-// Block = an 8 x 8 pixel tile x 64 output channels (4 waves x 16).  The block
-// stages the 14 x 14 x 2 flow patch and its 64-channel slice of the weights
-// ([49][2][64] fp32, 25 KB) in LDS once; lane = pixel, and per tap each wave
-// reads its 2 x 16 weights as broadcast 16-B LDS reads and does 16 packed
-// 2-wide FMAs (v_pk_fma_f32).  The previous version read the weights as
-// per-tap scalar loads and stalled on them 49 times per wave (~29 us at
-// 1088x440 vs a few us of FMA work).
-constexpr int FE_T = 8;                 // tile edge (pixels)
-constexpr int FE_P = FE_T + 6;          // patch edge
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__ coords, int B, int H,
-                                                       int W, const float* __restrict__ w,  // [49][2][Cout]
-                                                       const float* __restrict__ bias, int Cout,
-                                                       bf16_t* __restrict__ out, int ostr, int ooff,
-                                                       bf16_t* __restrict__ fout, int fstr, int foff) {
-  __shared__ __attribute__((aligned(16))) float wl[49 * 2 * 64];
-  __shared__ float fl[2][FE_P * FE_P];
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int tx_n = cdiv(W, FE_T), ty_n = cdiv(H, FE_T);
-  const int tile = blockIdx.x;
-  const int b = tile / (tx_n * ty_n), rem = tile - b * tx_n * ty_n;
-  const int y0 = (rem / tx_n) * FE_T, x0 = (rem % tx_n) * FE_T;
-  const int cb = blockIdx.y * 64;          // block's first output channel
-  const int ncb = min(64, Cout - cb);      // multiple of 16
-  const int HW = H * W;
-  const float* cx = coords + (size_t)b * 2 * HW;
-  const float* cy = cx + HW;
-  // weights: rows (tap, ci) of ncb floats
-  for (int i = t; i < 98 * 16; i += 256) {
-    const int r = i >> 4, c4 = (i & 15) * 4;
-    if (c4 < ncb)
-      *reinterpret_cast<float4*>(wl + r * 64 + c4) = *reinterpret_cast<const float4*>(w + (size_t)r * Cout + cb + c4);
-  }
-  for (int i = t; i < FE_P * FE_P; i += 256) {
-    const int yy = y0 + i / FE_P - 3, xx = x0 + i % FE_P - 3;
-    const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    const int o = in ? yy * W + xx : 0;
-    fl[0][i] = in ? cx[o] - (float)xx : 0.f;
-    fl[1][i] = in ? cy[o] - (float)yy : 0.f;
-  }
-  __syncthreads();
-  const int c0 = wave * 16;
-  if (c0 >= ncb) return;
-  const int ly = lane >> 3, lx = lane & 7;
-  f32x2_t acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = f32x2_t{bias[cb + c0 + 2 * j], bias[cb + c0 + 2 * j + 1]};
-#pragma unroll 7
-  for (int tp = 0; tp < 49; ++tp) {
-    const int ky = tp / 7, kx = tp - ky * 7;
-    const int pi = (ly + ky) * FE_P + lx + kx;
-    const float fu = fl[0][pi], fv = fl[1][pi];
-    const f32x2_t u2 = f32x2_t{fu, fu}, v2 = f32x2_t{fv, fv};
-    const float4* wu = reinterpret_cast<const float4*>(wl + (tp * 2) * 64 + c0);
-    const float4* wv = reinterpret_cast<const float4*>(wl + (tp * 2 + 1) * 64 + c0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a = wu[q], c = wv[q];
-      acc[2 * q] = __builtin_elementwise_fma(u2, f32x2_t{a.x, a.y}, acc[2 * q]);
-      acc[2 * q + 1] = __builtin_elementwise_fma(u2, f32x2_t{a.z, a.w}, acc[2 * q + 1]);
-      acc[2 * q] = __builtin_elementwise_fma(v2, f32x2_t{c.x, c.y}, acc[2 * q]);
-      acc[2 * q + 1] = __builtin_elementwise_fma(v2, f32x2_t{c.z, c.w}, acc[2 * q + 1]);
-    }
-  }
-  const int y = y0 + ly, x = x0 + lx;
-  if (y >= H || x >= W) return;
-  const size_t p = (size_t)b * HW + (size_t)y * W + x;
-  uint32_t u[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    u[j] = uint32_t(f2bf(fmaxf(acc[j].x, 0.f))) | (uint32_t(f2bf(fmaxf(acc[j].y, 0.f))) << 16);
-  uint4* o = reinterpret_cast<uint4*>(out + p * ostr + ooff + cb + c0);
-  o[0] = make_uint4(u[0], u[1], u[2], u[3]);
-  o[1] = make_uint4(u[4], u[5], u[6], u[7]);
-  if (cb + c0 == 0 && fout) {
-    const int pi = (ly + 3) * FE_P + lx + 3;
-    fout[p * fstr + foff] = f2bf(fl[0][pi]);
-    fout[p * fstr + foff + 1] = f2bf(fl[1][pi]);
-  }
-}
-
 // ------------------------------------------------------------------ GRU gate backward
 // One ConvGRU pass h' = (1-z) h + z q~, q~ = tanh(q_pre), z = sigmoid(z_pre):
 //   dq_pre = dh' z (1 - q~^2)        -> dq (bf16, the q-conv dgrad/wgrad operand)
@@ -1123,12 +1032,5 @@ void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* a
                      static_cast<const bf16_t*>(act), astr, aoff, static_cast<bf16_t*>(out), ostr, P);
 }
 
-void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
-                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
-                     hipStream_t stream) {
-  const dim3 grid((unsigned)(B * cdiv(H, conv::FE_T) * cdiv(W, conv::FE_T)), (unsigned)cdiv(Cout, 64));
-  hipLaunchKernelGGL(conv::flow_enc_kernel, grid, dim3(256), 0, stream, coords, B, H, W, w, bias,
-                     Cout, static_cast<bf16_t*>(out), ostr, ooff, static_cast<bf16_t*>(fout), fstr, foff);
-}
 
 }  // namespace rs
