@@ -104,6 +104,7 @@ class _Encoder(nn.Module):
     block_cls = ResidualBlock
     stem_dim = 64
     stage_dims = (64, 96, 128)
+    hip_geo = True  # strided / 1x1 convs on the HIP kernels (ops/enc_conv.py geo_scope)
 
     def __init__(self, output_dim=128, norm_fn="batch", dropout=0.0):
         super().__init__()
@@ -148,14 +149,23 @@ class _Encoder(nn.Module):
         fns = [lambda x: conv_norm_act(self.conv1, self.norm1, x)]
         for layer in (self.layer1, self.layer2, self.layer3):
             fns.extend(layer)
+        if not self.hip_geo:
+            fns = [self._no_geo(f) for f in fns]
 
         def head(x):
             x = self._head_conv(x)
             if self.training and self.dropout is not None:
                 x = self.dropout(x)
             return x
-        fns.append(head)
+        fns.append(head if self.hip_geo else self._no_geo(head))
         return fns
+
+    @staticmethod
+    def _no_geo(fn):
+        def run(x):
+            with enc_conv.geo_scope(False):
+                return fn(x)
+        return run
 
     def _head_conv(self, x):
         """1x1 projection (with bias): HIP implicit GEMM on the GPU bf16 path."""
@@ -168,9 +178,10 @@ class _Encoder(nn.Module):
         if pair:
             n = x[0].shape[0]
             x = torch.cat(list(x), dim=0)
-        x = conv_norm_act(self.conv1, self.norm1, x)
-        x = self.layer3(self.layer2(self.layer1(x)))
-        x = self._head_conv(x)
+        with enc_conv.geo_scope(self.hip_geo):
+            x = conv_norm_act(self.conv1, self.norm1, x)
+            x = self.layer3(self.layer2(self.layer1(x)))
+            x = self._head_conv(x)
         if self.training and self.dropout is not None:
             x = self.dropout(x)
         if pair:
@@ -192,6 +203,7 @@ class SmallEncoder(_Encoder):
     block_cls = BottleneckBlock
     stem_dim = 32
     stage_dims = (32, 64, 96)
+    hip_geo = False
 
     def _build_head(self, in_dim, output_dim, dropout):
         self.dropout = nn.Dropout2d(p=dropout) if dropout > 0 else None

@@ -158,10 +158,27 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 #             3x3's (0, 0) phase as a second K segment (conv_pair)
 #   wgrad   : split-K MFMA over dY pixels with strided X rows
 _GEO = os.environ.get("RS_ENC_GEO", "1") != "0"
+_GEO_SCOPE = [True]  # per-encoder switch (geo_scope): RAFT-small's encoder keeps MIOpen
+
+
+class geo_scope:
+    """Enable / disable the strided-geometry path inside a block (set by the
+    encoder: RAFT-small's narrow bottleneck encoder measured faster on
+    MIOpen -- 657 vs 602 pairs/s -- while full RAFT's is neutral-to-faster)."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = _GEO_SCOPE[0]
+        _GEO_SCOPE[0] = self.on
+
+    def __exit__(self, *exc):
+        _GEO_SCOPE[0] = self.prev
 
 
 def _geo_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    if not (_ENABLED and _GEO) or x.dtype != torch.bfloat16 or x.dim() != 4 or not _ext.use_hip(x):
+    if not (_ENABLED and _GEO and _GEO_SCOPE[0]) or x.dtype != torch.bfloat16 or x.dim() != 4 or not _ext.use_hip(x):
         return False
     k, s, p = conv.kernel_size, conv.stride, conv.padding
     if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros" or isinstance(p, str):

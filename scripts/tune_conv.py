@@ -34,7 +34,7 @@ def record_calls(args):
     from raft_stir_amd.utils.padder import InputPadder
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = RAFT(make_args(mixed_precision=True)).to(dev).to(memory_format=torch.channels_last)
+    model = RAFT(make_args(mixed_precision=True, small=args.small)).to(dev).to(memory_format=torch.channels_last)
     calls = {}
 
     def grab(tag, fn):
@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--size", type=int, nargs=2, default=[368, 496])
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--small", action="store_true", help="tune RAFT-small's calls")
+    ap.add_argument("--merge", action="store_true", help="update the existing table instead of replacing it")
     args = ap.parse_args()
     os.environ["RS_CONV_TUNED"] = "0"  # record with the heuristic, compare against it
     from raft_stir_amd.ops import _ext
@@ -133,6 +135,12 @@ def main():
         report.append(dict(key=key, phase=tag, heuristic=heur, us_heuristic=round(res[heur], 2), best=best,
                            us_best=round(res[best], 2)))
         print(f"{tag:5s} {key:42s} heur t{heur} {res[heur]:7.1f}us  best t{best} {res[best]:7.1f}us", flush=True)
+    if args.merge and os.path.exists(args.out):
+        with open(args.out) as f:
+            old = json.load(f)
+        keys = set(table)
+        table = {**old.get("tiles", {}), **table}
+        report = [r for r in old.get("report", []) if r["key"] not in keys] + report
     with open(args.out, "w") as f:
         json.dump({"device": torch.cuda.get_device_name(0), "note": "scripts/tune_conv.py", "tiles": table,
                    "report": report}, f, indent=1)
