@@ -25,6 +25,7 @@ Engine differences (outputs unchanged):
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -32,6 +33,7 @@ import torch.nn as nn
 
 from ..config import RAFTConfig, resolve_config
 from ..ops import _ext
+from ..ops import enc_conv
 from ..ops import gru as gru_ops
 from ..ops import wpack
 from ..ops import reference as ref
@@ -64,7 +66,11 @@ class _StreamHandoff(torch.autograd.Function):
 
 _SIDE_STREAMS = {}  # (device index, slot) -> extra HIP stream
 # per-mechanism switches of the multi-stream schedule (all gated by cfg.overlap_encoders)
-OVERLAP = {"cnet": True, "flow": True, "defer": True}
+# defer_enc (encoder conv weight gradients on the deferred stream too) is off:
+# paired A/B on one box, 3 x 30 steps: 352 pairs/s on vs 366 off (the third
+# stream then ends the backward late and its GEMMs contend with the dgrads)
+OVERLAP = {"cnet": True, "flow": True, "defer": True,
+           "defer_enc": os.environ.get("RS_DEFER_ENC", "0") == "1"}
 
 
 class RAFT(nn.Module):
@@ -93,6 +99,20 @@ class RAFT(nn.Module):
         for m in self.modules():
             if hasattr(m, "fused") and m is not self:
                 m.fused = enabled
+
+    def _encoder_conv_params(self):
+        """Weights (and biases) of the encoder convolutions, in a fixed order."""
+        ps = self.__dict__.get("_enc_params")
+        if ps is None or ps[0] is not self.fnet.conv1.weight:
+            ps = []
+            for enc in (self.fnet, self.cnet):
+                for m in enc.modules():
+                    if isinstance(m, nn.Conv2d):
+                        ps.append(m.weight)
+                        if m.bias is not None:
+                            ps.append(m.bias)
+            self.__dict__["_enc_params"] = ps
+        return ps
 
     def _train_engine(self):
         eng = self.__dict__.get("_fused_train")
@@ -168,15 +188,23 @@ class RAFT(nn.Module):
         # branches of the inference graph.
         side = None
         dparams = None
+        enc_defer = contextlib.nullcontext()
         if (gpu and self.cfg.overlap_encoders and OVERLAP["defer"] and self.training and torch.is_grad_enabled() and mixed
                 and self.cfg.fused_train and not test_mode):
-            # update-block weight gradients overlap the encoder backward (see DeferGrads)
-            dparams = DeferGrads.apply(self._side_stream(dev, 1), *self._train_engine().params)
+            # update-block weight gradients overlap the encoder backward, and the
+            # encoder convs' weight gradients overlap their own dgrad chain
+            # (see DeferGrads; ops/enc_conv.py defer_weights)
+            uparams = self._train_engine().params
+            eparams = self._encoder_conv_params() if OVERLAP["defer_enc"] else []
+            views = DeferGrads.apply(self._side_stream(dev, 1), *uparams, *eparams)
+            dparams = views[:len(uparams)]
+            enc_defer = enc_conv.defer_weights(self._side_stream(dev, 1),
+                                               {id(p): v for p, v in zip(eparams, views[len(uparams):])})
         if gpu and self.cfg.overlap_encoders and OVERLAP["cnet"]:
             side = self._side_stream(dev)
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
-        with self._autocast(dev):
+        with self._autocast(dev), enc_defer:
             if side is not None:
                 # fnet (main) and cnet (side) stage by stage, interleaved on the host
                 xf = torch.cat([image1, image2], dim=0)

@@ -87,9 +87,68 @@ def _packed(weight: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return _fwd_weight(weight)
 
 
+# ----------------------------------------------------------- deferred wgrads
+# During a training forward RAFT.forward hands the encoder conv weights to the
+# convs as VIEWS produced by a DeferGrads node created before the encoders
+# (models/fused_train.py).  A conv fed such a view launches its weight
+# gradient on the deferred-gradient stream and returns at once, so the
+# encoder's dgrad chain (the critical path of the backward) does not wait for
+# the weight-gradient GEMMs; DeferGrads.backward, which autograd runs last,
+# joins that stream before the gradients reach AccumulateGrad / DDP.
+_DEFER = {"stream": None, "views": {}}
+
+
+class defer_weights:
+    """Route ``views`` ({id(param): view}) into the encoder convs, with their
+    weight gradients on ``stream``."""
+
+    def __init__(self, stream, views):
+        self.stream, self.views = stream, views
+
+    def __enter__(self):
+        self.prev = (_DEFER["stream"], _DEFER["views"])
+        _DEFER["stream"], _DEFER["views"] = self.stream, self.views
+
+    def __exit__(self, *exc):
+        _DEFER["stream"], _DEFER["views"] = self.prev
+
+
+class _Hold:
+    """A parameter passed to an autograd Function without an autograd edge
+    (its packed layouts are keyed on the parameter, not on the view)."""
+    __slots__ = ("p",)
+
+    def __init__(self, p):
+        self.p = p
+
+
+def _weight_in(param):
+    """(autograd input for the weight, deferred-gradient stream or None)."""
+    v = _DEFER["views"].get(id(param))
+    return (param, None) if v is None else (v, _DEFER["stream"])
+
+
+def _wgrad_on(stream, fn, inputs):
+    """Run ``fn()`` (-> tuple of gradients) on ``stream`` when deferred."""
+    if stream is None:
+        return fn()
+    cur = torch.cuda.current_stream(inputs[0].device)
+    stream.wait_stream(cur)
+    for t in inputs:
+        t.record_stream(stream)
+    with torch.cuda.stream(stream):
+        out = fn()
+    for g in out:
+        if g is not None:
+            g.record_stream(cur)
+    return out
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, hold, wstream):
+        weight = hold.p
+        ctx.param, ctx.wstream = weight, wstream
         xn = _nhwc(x)
         N, H, W, cin = xn.shape
         cout = weight.shape[0]
@@ -97,12 +156,13 @@ class _Conv3x3(torch.autograd.Function):
         wp = _packed(weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
         conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout))
-        ctx.save_for_backward(x, weight)
+        ctx.save_for_backward(x)
         return out.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        x, = ctx.saved_tensors
+        weight = ctx.param
         xn = _nhwc(x)
         N, H, W, cin = xn.shape
         cout = weight.shape[0]
@@ -115,29 +175,34 @@ class _Conv3x3(torch.autograd.Function):
             conv_fused([(dyn, 0, cout)], wd, None, 3, 3, cin, EPI_BIAS, dxn, 0, tile=choose_enc_tile(P, cout, cin))
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            if _wgrad_covers(cin, cout):
-                # the kernel tiles input channels in 64-wide segments: an odd
-                # multiple of 32 (96) is covered by two OVERLAPPING segments,
-                # [0, cin-32) and [cin-64, cin), whose dW columns are spliced
-                segs = [(0, cin)] if cin % 64 == 0 else [(0, cin - 32), (cin - 64, 64)]
-                ktot = sum(c for _, c in segs)
-                acc = torch.zeros(pad_to(cout, 128), 9, ktot, device=x.device, dtype=torch.float32)
-                torch.ops.raft_stir.conv_wgrad(dyn, 0, cout, [xn] * len(segs), [o for o, _ in segs],
-                                               [c for _, c in segs], [P] * len(segs), 3, 3, acc, None, 0)
-                acc = acc[:cout]
-                if len(segs) > 1:
-                    acc = torch.cat([acc[..., :cin - 32], acc[..., cin:cin + 32]], -1)
-                dw = acc.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(weight.dtype)
-            else:  # channel counts the wgrad kernel does not tile: MIOpen
-                dw = torch.ops.aten.convolution_backward(
-                    dyn.permute(0, 3, 1, 2), x, weight.to(torch.bfloat16), None, [1, 1], [1, 1], [1, 1], False,
-                    [0, 0], 1, [False, True, False])[1].to(weight.dtype)
-        return dx, dw
+            dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])
+        return dx, dw, None, None
+
+
+def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
+    if _wgrad_covers(cin, cout):
+        # the kernel tiles input channels in 64-wide segments: an odd
+        # multiple of 32 (96) is covered by two OVERLAPPING segments,
+        # [0, cin-32) and [cin-64, cin), whose dW columns are spliced
+        segs = [(0, cin)] if cin % 64 == 0 else [(0, cin - 32), (cin - 64, 64)]
+        ktot = sum(c for _, c in segs)
+        acc = torch.zeros(pad_to(cout, 128), 9, ktot, device=x.device, dtype=torch.float32)
+        torch.ops.raft_stir.conv_wgrad(dyn, 0, cout, [xn] * len(segs), [o for o, _ in segs],
+                                       [c for _, c in segs], [P] * len(segs), 3, 3, acc, None, 0)
+        acc = acc[:cout]
+        if len(segs) > 1:
+            acc = torch.cat([acc[..., :cin - 32], acc[..., cin:cin + 32]], -1)
+        return acc.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(weight.dtype)
+    # channel counts the wgrad kernel does not tile: MIOpen
+    return torch.ops.aten.convolution_backward(
+        dyn.permute(0, 3, 1, 2), x, weight.to(torch.bfloat16), None, [1, 1], [1, 1], [1, 1], False,
+        [0, 0], 1, [False, True, False])[1].to(weight.dtype)
 
 
 def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """conv(x) without its bias (see :func:`eligible`)."""
-    return _Conv3x3.apply(x, conv.weight)
+    w, st = _weight_in(conv.weight)
+    return _Conv3x3.apply(x, w, _Hold(conv.weight), st)
 
 
 # ----------------------------------------------------------------- strided / 1x1
@@ -294,29 +359,36 @@ def _conv_geo_wgrad(dy, x, weight, stride, want_bias):
 
 class _ConvGeo(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad):
+    def forward(ctx, x, weight, bias, stride, pad, hold, wstream):
+        weight = hold.p
         out = _conv_geo_fwd(x, weight, bias, stride, pad)
-        ctx.save_for_backward(x, weight)
+        ctx.save_for_backward(x)
+        ctx.param, ctx.wstream = weight, wstream
         ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
         return out.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        x, = ctx.saved_tensors
+        weight = ctx.param
         dyn = _nhwc(dy.to(torch.bfloat16))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _conv_geo_dgrad([dyn], [weight], x.shape, ctx.stride, ctx.pad).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = _conv_geo_wgrad(dyn, x, weight, ctx.stride, ctx.has_bias and ctx.needs_input_grad[2])
-        return dx, dw, db, None, None
+            want_b = ctx.has_bias and ctx.needs_input_grad[2]
+            dw, db = _wgrad_on(ctx.wstream, lambda: _conv_geo_wgrad(dyn, x, weight, ctx.stride, want_b), [dyn, x])
+        return dx, dw, db, None, None, None, None
 
 
 def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
     """conv(x) on the HIP kernels (see :func:`eligible_geo`); ``bias=False``
     drops the conv's bias (folded into a following normalisation)."""
     b = conv.bias if bias else None
-    return _ConvGeo.apply(x, conv.weight, b, tuple(conv.stride), tuple(conv.padding))
+    w, st = _weight_in(conv.weight)
+    if b is not None and st is not None:
+        b = _DEFER["views"].get(id(conv.bias), b)
+    return _ConvGeo.apply(x, w, b, tuple(conv.stride), tuple(conv.padding), _Hold(conv.weight), st)
 
 
 class _ConvPair(torch.autograd.Function):
@@ -325,27 +397,31 @@ class _ConvPair(torch.autograd.Function):
     gradient, with the shortcut's term fused into the 3x3's (0, 0) phase."""
 
     @staticmethod
-    def forward(ctx, x, w1, wd, stride):
+    def forward(ctx, x, w1, wd, stride, holds, wstream):
+        w1, wd = holds.p
         y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1))
         yd = _conv_geo_fwd(x, wd, None, stride, (0, 0))
-        ctx.save_for_backward(x, w1, wd)
+        ctx.save_for_backward(x)
+        ctx.params, ctx.wstream = (w1, wd), wstream
         ctx.stride = stride
         return y1.permute(0, 3, 1, 2), yd.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dy1, dyd):
-        x, w1, wd = ctx.saved_tensors
+        x, = ctx.saved_tensors
+        w1, wd = ctx.params
         s = ctx.stride
         d1 = _nhwc(dy1.to(torch.bfloat16))
         dd = _nhwc(dyd.to(torch.bfloat16))
         dx = dw1 = dwd = None
         if ctx.needs_input_grad[0]:
             dx = _pair_dgrad(d1, dd, w1, wd, x.shape, s).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            dw1, _ = _conv_geo_wgrad(d1, x, w1, s, False)
-        if ctx.needs_input_grad[2]:
-            dwd, _ = _conv_geo_wgrad(dd, x, wd, s, False)
-        return dx, dw1, dwd, None
+        n1, n2 = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        if n1 or n2:
+            dw1, dwd = _wgrad_on(ctx.wstream, lambda: (_conv_geo_wgrad(d1, x, w1, s, False)[0] if n1 else None,
+                                                       _conv_geo_wgrad(dd, x, wd, s, False)[0] if n2 else None),
+                                 [d1, dd, x])
+        return dx, dw1, dwd, None, None, None
 
 
 def _pair_dgrad(d1, dd, w1, wd, x_shape, stride):
@@ -396,4 +472,6 @@ def pair_eligible(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor) -> bool:
 
 def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor):
     """(conv1(x), down(x)) without biases (both folded into their norms)."""
-    return _ConvPair.apply(x, conv1.weight, down.weight, tuple(conv1.stride))
+    w1, st = _weight_in(conv1.weight)
+    wd, _ = _weight_in(down.weight)
+    return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st)

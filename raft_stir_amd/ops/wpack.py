@@ -111,7 +111,15 @@ class _Registry:
     def repack(self):
         """Every registered layout from the current parameter values (3 kernels)."""
         STATS["repacks"] += 1
-        live = {k: e for k, e in self.entries.items() if all(r() is not None for r in e.refs)}
+        # strong references for the whole repack: a cyclic GC pass triggered by
+        # an allocation below must not free a parameter between the liveness
+        # check and its use
+        hold, live = [], {}
+        for k, e in self.entries.items():
+            ws_ = [r() for r in e.refs]
+            if all(w is not None for w in ws_):
+                live[k] = e
+                hold.extend(ws_)
         if len(live) != len(self.entries):
             self.entries, self.dirty = live, True
         if not live:
