@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--infer-reps", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
+    ap.add_argument("--train-graph", action="store_true",
+                    help="one GPU: replay the whole training step (forward, loss, backward, clip, AdamW) "
+                         "from one hipGraph (runtime/graph.py GraphedTrainStep).  Measured equal to the "
+                         "eager step (22.30 vs 22.47 ms: the step is GPU-bound), so off by default")
     ap.add_argument("--corr-dtype", default="auto", choices=["auto", "float32", "bfloat16"],
                     help="all-pairs pyramid storage; auto = bf16 under bf16 autocast (EPE-drift gate: "
                          "tests/test_model_gpu.py::test_bf16_pyramid_epe_drift)")
@@ -117,22 +121,40 @@ def main():
     if not cpu:
         model = model.to(memory_format=torch.channels_last)
     model.train()
-    ddp = rdist.wrap_ddp(model, device=dev)
+    use_graph = a.train_graph and not cpu and not a.reference_ops
+    if use_graph and info.world_size > 1:
+        raise SystemExit("bench.py: --train-graph is one-GPU only (multi-GPU steps run eager under DDP)")
     targs = argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
-    optimizer, scheduler = fetch_optimizer(targs, model)
     H, W = a.size
     pool = DevicePool(4, a.batch, H, W, dev, seed=info.rank * 97)
 
-    def step():
-        i1, i2, flow, valid = pool.next()
-        optimizer.zero_grad(set_to_none=True)
-        preds = ddp(i1, i2, iters=a.iters)
-        loss, _ = sequence_loss(preds, flow, valid, gamma=0.8, sync_metrics=False)
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        optimizer.step()
-        scheduler.step()
-        return loss
+    if use_graph:
+        # the same step, replayed from one hipGraph: the AdamW learning rate lives in
+        # a device tensor that the (host-side) OneCycle scheduler updates between replays
+        from raft_stir_amd.runtime.graph import GraphedTrainStep
+        optimizer, scheduler = fetch_optimizer(targs, model, capturable=True)
+        gstep = GraphedTrainStep(
+            model, optimizer, lambda p, f, v: sequence_loss(p, f, v, gamma=0.8, sync_metrics=False)[0],
+            pool.next(), clip=1.0, warmup=3, iters=a.iters)
+
+        def step():
+            loss = gstep.step(pool.next())
+            scheduler.step()
+            return loss
+    else:
+        ddp = rdist.wrap_ddp(model, device=dev)
+        optimizer, scheduler = fetch_optimizer(targs, model)
+
+        def step():
+            i1, i2, flow, valid = pool.next()
+            optimizer.zero_grad(set_to_none=True)
+            preds = ddp(i1, i2, iters=a.iters)
+            loss, _ = sequence_loss(preds, flow, valid, gamma=0.8, sync_metrics=False)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            optimizer.step()
+            scheduler.step()
+            return loss
 
     sync = (lambda: None) if cpu else torch.cuda.synchronize
     for _ in range(a.warmup):
@@ -177,6 +199,7 @@ def main():
                 "parallelism": f"dp{info.world_size}",
                 "ops": "stock-pytorch (reference semantics)" if (a.reference_ops or cpu) else "hip-kernels",
                 "corr_pyramid": "fp32" if (a.reference_ops or cpu) else str(model_cfg_pyr(model)),
+                "train_step": "hipgraph" if use_graph else "eager",
                 "grad_allreduce": ("none" if info.world_size == 1 else
                                    "rccl: packed update-block buffer + DDP encoder buckets"
                                    if getattr(model.__dict__.get("_fused_train"), "grad_group", None)

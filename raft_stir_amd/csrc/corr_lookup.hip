@@ -25,6 +25,8 @@
 // applies the avg-pool backward (level l cell -> its 2^l x 2^l level-0 block,
 // weight 4^-l) and the 1/sqrt(C) scale once.
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace rs {
@@ -283,6 +285,74 @@ __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, lon
   }
 }
 
+// Same fold, 4 consecutive row elements per thread: grid (row chunks, rows),
+// 32-bit in-row index math only (the flat kernel above spends most of its time
+// in 64-bit div/mod per element: 469 us for the 477 MB of the training-shape
+// fold), one 16-B level-0 load, one 8-B bf16 store (or 16-B in-place store).
+// Needs S[0] % 4 == 0 (pyramid rows are padded to 128 B); the bf16 rows are
+// compact (pitch E = H0*W0), so 8-B stores need E % 4 == 0, else 2-B stores.
+template <bool BF16>
+__global__ __launch_bounds__(256) void pyr_fold4_kernel(PyrMut g, int levels, int rows, float scale,
+                                                        bf16_t* __restrict__ out_bf16) {
+  const int H0 = g.H[0], W0 = g.W[0], E = H0 * W0;
+  const int E4 = (E + 3) >> 2;
+  const bool vec_out = (E & 3) == 0;
+  for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+    float* r0 = g.p[0] + (size_t)row * g.S[0];
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < E4; q += gridDim.x * blockDim.x) {
+      const int e = q * 4;
+      const bool full = e + 4 <= E;
+      float v[4];
+      if (full) {
+        const float4 t = *reinterpret_cast<const float4*>(r0 + e);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = e + j < E ? r0[e + j] : 0.f;
+      }
+      int ys[4], xs[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ys[j] = (e + j) / W0;
+        xs[j] = e + j - ys[j] * W0;
+      }
+      float w = 1.f;
+#pragma unroll
+      for (int l = 1; l < 4; ++l) {
+        if (l >= levels) break;
+        w *= 0.25f;
+        const float* rl = g.p[l] + (size_t)row * g.S[l];
+        const int Hl = g.H[l], Wl = g.W[l];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int yl = ys[j] >> l, xl = xs[j] >> l;
+          if (e + j < E && yl < Hl && xl < Wl) v[j] += w * rl[yl * Wl + xl];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= scale;
+      if (BF16) {
+        bf16_t* o = out_bf16 + (size_t)row * E + e;
+        if (full && vec_out) {
+          const uint2 pk = make_uint2(uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                                      uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16));
+          *reinterpret_cast<uint2*>(o) = pk;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (e + j < E) o[j] = f2bf(v[j]);
+        }
+      } else if (full) {
+        *reinterpret_cast<float4*>(r0 + e) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (e + j < E) r0[e + j] = v[j];
+      }
+    }
+  }
+}
+
 inline int grid_for(long total) {
   long blocks = (total + 255) / 256;
   if (blocks > 65535L * 8) blocks = 65535L * 8;
@@ -375,6 +445,19 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, cons
   }
   const long total = rows * Hs[0] * Ws[0];
   if (total == 0) return;
+  const long E = (long)Hs[0] * Ws[0];
+  if (Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0 && rows < (1L << 31) &&
+      E < (1L << 30)) {
+    const int bx = (int)std::min<long>((E + 4 * 256 - 1) / (4 * 256), 64);
+    const dim3 grid(bx, (unsigned)std::min<long>(rows, 65535));
+    if (out_bf16)
+      hipLaunchKernelGGL(lookup::pyr_fold4_kernel<true>, grid, dim3(256), 0, stream, p, levels, (int)rows, scale,
+                         static_cast<bf16_t*>(out_bf16));
+    else
+      hipLaunchKernelGGL(lookup::pyr_fold4_kernel<false>, grid, dim3(256), 0, stream, p, levels, (int)rows, scale,
+                         nullptr);
+    return;
+  }
   hipLaunchKernelGGL(lookup::pyr_fold_kernel, dim3(lookup::grid_for(total)), dim3(256), 0, stream,
                      p, levels, rows, scale, static_cast<bf16_t*>(out_bf16));
 }

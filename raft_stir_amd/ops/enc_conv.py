@@ -36,7 +36,8 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
     if cin % 64 or cout % 64:
         return 4                   # 128x64 register-staged tile, 32-deep K steps
     if cout <= 64:
-        return 21                  # 64 co x 128 px buffer-DMA tile
+        return 17                  # 64 co x 64 px buffer-DMA tile (1/2-res 64->64: 125 vs 140 us for
+                                   # the 128-px tile 21, profiles/r2/enc_conv_tiles.txt)
     return 16 if P >= 40000 else 17
 
 

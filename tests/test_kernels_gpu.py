@@ -265,3 +265,31 @@ def test_allpairs_corr_autograd_bf16_pyramid(cuda):
     for got, want in ((b1.grad, a1.grad), (b2.grad, a2.grad)):
         rel = ((got.float().cpu() - want).norm() / want.norm()).item()
         assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("HW", [(46, 62), (11, 37), (12, 20)])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_pyr_grad_fold(cuda, HW, out_bf16):
+    """Pyramid-gradient fold (avg-pool adjoint of every level onto level 0, times
+    the 1/sqrt(C) scale) vs a PyTorch fp32 gather; (46, 62) and (12, 20) take the
+    4-wide kernel (H*W % 4 == 0), (11, 37) the per-element one."""
+    H, W = HW
+    B, N1, levels, scale = 2, 24, 4, 0.0625
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shapes = [(H >> l, W >> l) for l in range(levels)]
+    gpyr = [torch.randn(B, N1, h, w, generator=g).to(cuda) for h, w in shapes]
+    want = gpyr[0].clone()
+    for l in range(1, levels):
+        h, w = shapes[l]
+        ys, xs = torch.arange(H, device=cuda) >> l, torch.arange(W, device=cuda) >> l
+        m = (ys[:, None] < h) & (xs[None, :] < w)
+        up = gpyr[l][:, :, ys.clamp(max=h - 1)][:, :, :, xs.clamp(max=w - 1)]
+        want += 0.25 ** l * up * m
+    want *= scale
+    if out_bf16:
+        out = torch.empty(B, N1, H, W, device=cuda, dtype=torch.bfloat16)
+        torch.ops.raft_stir.pyr_grad_fold_bf16(gpyr, scale, out)
+        torch.testing.assert_close(out.float(), want, rtol=1e-2, atol=1e-2)
+    else:
+        torch.ops.raft_stir.pyr_grad_fold(gpyr, scale)
+        torch.testing.assert_close(gpyr[0], want, rtol=1e-5, atol=1e-5)
