@@ -66,6 +66,9 @@ int flow_wgrad_blocks(int Bp, int H);
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
                        float* db, float* part, hipStream_t stream);
 bool deterministic();
+bool enc_halo_launch(const uint16_t* x, int xstr, const uint16_t* w, int Ktot, uint16_t* y, int ystr, int B, int H,
+                     int W, int cin, int cout, int num_cus, hipStream_t stream);
+bool enc_halo_supported(int cin, int cout);
 }  // namespace rs
 
 namespace {
@@ -527,9 +530,45 @@ void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tenso
   RS_CHECK_LAUNCH();
 }
 
+int num_cus(int dev) {
+  static int n[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+// Stride-1 3x3 'same' conv on the halo-tile kernel (csrc/enc_halo.hip):
+// x NHWC (cin of its x.size(3) channels), w packed [Cout_pad][9][Ktot], y NHWC
+// (cout of its y.size(3) channels), no bias.
+void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin, int64_t cout) {
+  TORCH_CHECK(x.dim() == 4, "conv3x3_halo: x must be NHWC");
+  const int B = x.size(0), H = x.size(1), W = x.size(2);
+  check_nhwc(x, B, H, W, "conv3x3_halo: x");
+  check_nhwc(y, B, H, W, "conv3x3_halo: y");
+  TORCH_CHECK(rs::enc_halo_supported(cin, cout), "conv3x3_halo: unsupported channels ", cin, "->", cout);
+  TORCH_CHECK(cin <= x.size(3) && x.size(3) % 8 == 0, "conv3x3_halo: x channels");
+  TORCH_CHECK(cout <= y.size(3) && y.size(3) % 4 == 0, "conv3x3_halo: y channels");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3 &&
+                  w.size(0) >= cout && w.size(1) == 9 && w.size(2) >= cin && w.size(2) % 8 == 0,
+              "conv3x3_halo: w must be packed [Cout_pad>=cout][9][Ktot>=cin] bf16");
+  TORCH_CHECK(((uintptr_t)x.data_ptr() | (uintptr_t)w.data_ptr()) % 16 == 0 && (uintptr_t)y.data_ptr() % 8 == 0,
+              "conv3x3_halo: alignment");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31) && y.numel() < (int64_t(1) << 31), "conv3x3_halo: tensor too large");
+  const c10::DeviceGuard guard(x.device());
+  rs::enc_halo_launch(static_cast<const uint16_t*>(x.data_ptr()), x.size(3), static_cast<const uint16_t*>(w.data_ptr()),
+                      w.size(2), static_cast<uint16_t*>(y.data_ptr()), y.size(3), B, H, W, cin, cout,
+                      num_cus(x.get_device()), stream());
+  RS_CHECK_LAUNCH();
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout) -> ()");
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
         "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
   m.def("flow_head(Tensor x, int xoff, int cin, Tensor w, Tensor bias, Tensor(a!) crd, Tensor? src) -> ()");
@@ -552,6 +591,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
+  m.impl("conv3x3_halo", &conv3x3_halo);
   m.impl("conv_geo", &conv_geo);
   m.impl("flow_encode", &flow_encode);
   m.impl("flow_head", &flow_head);

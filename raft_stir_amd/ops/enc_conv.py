@@ -5,8 +5,10 @@ core/extractor.py:6-56, 118-192) spend most of the encoder FLOPs in stride-1
 3x3 convolutions at 1/2, 1/4 and 1/8 resolution (64, 96, 128 channels).  On
 the GPU bf16 path they run here instead of MIOpen:
 
-  forward : csrc/conv.hip implicit GEMM (NHWC, buffer-DMA tiles)
-  dgrad   : the same kernel on dY with the transposed, spatially flipped
+  forward : csrc/enc_halo.hip (halo tiles, the block's weights
+            resident in LDS) for 64 / 96 input channels, else the csrc/conv.hip
+            implicit GEMM (NHWC, buffer-DMA tiles)
+  dgrad   : the same kernels on dY with the transposed, spatially flipped
             weight (a stride-1 'same' conv's input gradient is a conv)
   wgrad   : csrc/conv_wgrad.hip (split-K over pixels, fp32 accumulation);
             96 input channels as two overlapping 64-channel segments
@@ -42,6 +44,21 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
 
 
 _WGRAD_DMA = os.environ.get("RS_WGRAD_DMA", "1") != "0"
+_HALO = os.environ.get("RS_ENC_HALO", "1") != "0"
+
+
+def _halo_ok(cin: int, cout: int) -> bool:
+    """csrc/enc_halo.hip (halo tiles, weights resident in LDS) has
+    this conv: 64 input channels with a multiple of 64 outputs, or 96 inputs
+    with a multiple of 32 (the encoders' layer1 / layer2 3x3 convs)."""
+    return _HALO and ((cin == 64 and cout % 64 == 0) or (cin == 96 and cout % 32 == 0))
+
+
+def _conv3x3_into(xn, wp, cin, cout, out, P):
+    if _halo_ok(cin, cout):
+        torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout)
+    else:
+        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout))
 
 
 def _wgrad_covers(cin: int, cout: int) -> bool:
@@ -156,7 +173,7 @@ class _Conv3x3(torch.autograd.Function):
         P = N * H * W
         wp = _packed(weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
-        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout))
+        _conv3x3_into(xn, wp, cin, cout, out, P)
         ctx.save_for_backward(x)
         return out.permute(0, 3, 1, 2)
 
@@ -173,7 +190,7 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wd = _packed(weight, True)
             dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
-            conv_fused([(dyn, 0, cout)], wd, None, 3, 3, cin, EPI_BIAS, dxn, 0, tile=choose_enc_tile(P, cout, cin))
+            _conv3x3_into(dyn, wd, cout, cin, dxn, P)
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])

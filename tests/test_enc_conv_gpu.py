@@ -55,3 +55,24 @@ def test_ineligible_shapes(cuda):
     assert not enc_conv.eligible(nn.Conv2d(64, 64, 1).to(cuda), x)
     assert not enc_conv.eligible(nn.Conv2d(64, 64, 3, padding=1).to(cuda), x.float())
     assert not enc_conv.eligible(nn.Conv2d(64, 24, 3, padding=1).to(cuda), x)
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (64, 128), (96, 32)])
+@pytest.mark.parametrize("shape", [(2, 37, 45), (1, 8, 32), (3, 13, 70)])
+def test_conv3x3_halo_kernel(cuda, cin, cout, shape):
+    """csrc/enc_halo.hip (persistent halo-tile 3x3 conv) vs the fp32 PyTorch conv:
+    partial tiles in both directions, zero padding at every border, channel
+    strides wider than the conv (x with 32 extra channels, y with 8)."""
+    from raft_stir_amd.ops.conv import pack_weight, pad_to
+    B, H, W = shape
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = (torch.randn(B, H, W, cin + 32, generator=g) * 0.5).to(cuda, torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(cuda)
+    wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
+    y = torch.full((B, H, W, cout + 8), 7.0, device=cuda, dtype=torch.bfloat16)
+    torch.ops.raft_stir.conv3x3_halo(x, wp, y, cin, cout)
+    want = F.conv2d(x[..., :cin].permute(0, 3, 1, 2).float(), w.to(torch.bfloat16).float(), padding=1)
+    got = y[..., :cout].permute(0, 3, 1, 2).float()
+    rel = ((got - want).norm() / want.norm()).item()
+    assert rel < 1e-2, rel
+    assert (y[..., cout:] == 7.0).all()  # channels past cout untouched
