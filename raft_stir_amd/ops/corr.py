@@ -58,6 +58,15 @@ def from_nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 3, 1, 2)
 
 
+def _side_stream(dev):
+    """The RAFT model's slot-0 side stream (models/raft.py), if its multi-stream
+    schedule created one on this device."""
+    if dev.type != "cuda":
+        return None
+    from ..models.raft import OVERLAP, _SIDE_STREAMS
+    return _SIDE_STREAMS.get((dev.index, 0)) if OVERLAP.get("cnet", False) else None
+
+
 class _CorrVolume(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f1, f2, state: CorrState):
@@ -83,8 +92,23 @@ class _CorrVolume(torch.autograd.Function):
             # gradient: ~5x faster than the fp32 GEMMs on MI355X
             G = torch.empty(B, N1, H2 * W2, device=f1.device, dtype=torch.bfloat16)
             torch.ops.raft_stir.pyr_grad_fold_bf16(state.gpyr, state.scale, G)
-            df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
-            df2 = torch.bmm(G.transpose(1, 2), f1)
+            side = _side_stream(f1.device)
+            if side is not None:
+                # the two GEMMs are independent and neither fills the GPU (~180
+                # workgroups each at the training shape): df2 on the side stream,
+                # which is idle between the loop backward and the encoder backward
+                main = torch.cuda.current_stream(f1.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    df2 = torch.bmm(G.transpose(1, 2), f1)
+                df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
+                main.wait_stream(side)
+                G.record_stream(side)
+                f1.record_stream(side)
+                df2.record_stream(main)
+            else:
+                df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
+                df2 = torch.bmm(G.transpose(1, 2), f1)
         else:
             torch.ops.raft_stir.pyr_grad_fold(state.gpyr, state.scale)
             G = state.gpyr[0].view(B, N1, H2 * W2)
