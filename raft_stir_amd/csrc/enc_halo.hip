@@ -9,7 +9,7 @@
 // and every pixel row 9 times (once per tap), ~1.7 GB of L2->CU traffic for
 // 186 MB of real HBM traffic.  Here
 //  * the block's weights (COB output channels x 9 taps x CIN) are staged ONCE
-//    in LDS and the block walks 2-8 consecutive tiles (~130 KB of LDS: one
+//    in LDS and the block walks 12 consecutive tiles (~130 KB of LDS: one
 //    block per CU at a time);
 //  * a tile is 8 output rows x 32 pixels of one image; its 10 x 34 input
 //    halo is loaded once (global -> registers, issued before the previous
@@ -25,6 +25,7 @@
 //    at any tap shift.
 // Zero padding: halo pixels outside the image are written as zeros.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -258,11 +259,19 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   if (a.ntiles == 0) return true;
   const int cob = cin == 64 ? 64 : 32;
   const int gy = cdiv(cout, cob);
-  // a few consecutive tiles per block (the LDS weights are loaded once per
-  // block), ~2 blocks per CU: NOT persistent -- the encoders run these convs
-  // on two HIP streams at once, and a CU-filling persistent grid of one
-  // stream would serialise behind the other's
-  a.tpb = std::max(2, std::min(8, a.ntiles * gy / std::max(1, 2 * num_cus)));
+  // 12 consecutive tiles per block (the LDS weights are loaded once per
+  // block).  In-situ A/B (scripts/ab_halo_tpb.sh, paired runs on one box):
+  // training 12 tiles 383 pairs/s, 16: 380, 24: 374, 48 (~persistent): 350,
+  // 2-8 or ~one block per CU: 368-379 -- the encoders run these convs on two
+  // HIP streams at once, and long-lived CU-filling blocks of one stream
+  // serialise behind the other's; eager 1088x436 inference 206 vs 194 FPS
+  // for one block per CU
+  a.tpb = 12;
+  static const int tpb_env = [] {  // RS_HALO_TPB: fixed tiles per block (tuning A/B)
+    const char* e = getenv("RS_HALO_TPB");
+    return e ? atoi(e) : 0;
+  }();
+  if (tpb_env > 0) a.tpb = tpb_env;
   const int gx = cdiv(a.ntiles, a.tpb);
   if (cin == 64)
     hipLaunchKernelGGL((ench::enc_halo_kernel<64, 64>), dim3(gx, gy), dim3(256), 0, stream, a);
