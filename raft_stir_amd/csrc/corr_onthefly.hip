@@ -21,10 +21,14 @@
 // (plain store once per pixel: every pixel owns its df1 row) and df2_l
 // receives g * f1 through float atomics (cells are shared between pixels).
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace rs {
 namespace otf {
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_v;
 
 constexpr int WAVES = 4;
 constexpr int MAXE2 = 100;  // (2r+2)^2 for r <= 4
@@ -67,10 +71,19 @@ __global__ __launch_bounds__(WAVES * 64) void otf_fwd_kernel(const T* __restrict
   const int slot = lane & 7, grp = lane >> 3;
   const int D = 2 * r + 1, K2 = D * D, E = D + 1, E2 = E * E, CH = levels * K2;
 
+  // bf16: f1 stays packed and each 4-channel piece is two v_dot2_f32_bf16
+  // (fp32 accumulation) instead of 4 unpacks + 4 FMAs
+  constexpr bool BF = std::is_same<T, bf16_t>::value;
   float4 a[CQ];
+  uint2 ab[CQ];
   const T* f1p = f1 + pixc * C;
 #pragma unroll
-  for (int q = 0; q < CQ; ++q) a[q] = ld4<T>(f1p + q * 32 + slot * 4);
+  for (int q = 0; q < CQ; ++q) {
+    if constexpr (BF)
+      ab[q] = *reinterpret_cast<const uint2*>(f1p + q * 32 + slot * 4);
+    else
+      a[q] = ld4<T>(f1p + q * 32 + slot * 4);
+  }
 
   const float cx0 = coords[((size_t)b * 2 + 0) * N1 + n];
   const float cy0 = coords[((size_t)b * 2 + 1) * N1 + n];
@@ -90,8 +103,16 @@ __global__ __launch_bounds__(WAVES * 64) void otf_fwd_kernel(const T* __restrict
         const T* row = f2b + ((size_t)Y * W + X) * C + slot * 4;
 #pragma unroll
         for (int q = 0; q < CQ; ++q) {
-          const float4 v = ld4<T>(row + q * 32);
-          s += a[q].x * v.x + a[q].y * v.y + a[q].z * v.z + a[q].w * v.w;
+          if constexpr (BF) {
+            const uint2 v = *reinterpret_cast<const uint2*>(row + q * 32);
+            s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_v, ab[q].x),
+                                                __builtin_bit_cast(bf16x2_v, v.x), s, false);
+            s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_v, ab[q].y),
+                                                __builtin_bit_cast(bf16x2_v, v.y), s, false);
+          } else {
+            const float4 v = ld4<T>(row + q * 32);
+            s += a[q].x * v.x + a[q].y * v.y + a[q].z * v.z + a[q].w * v.w;
+          }
         }
       }
       s += __shfl_xor(s, 1, 64);

@@ -200,7 +200,9 @@ class RAFT(nn.Module):
             dparams = views[:len(uparams)]
             enc_defer = enc_conv.defer_weights(self._side_stream(dev, 1),
                                                {id(p): v for p, v in zip(eparams, views[len(uparams):])})
-        if gpu and self.cfg.overlap_encoders and OVERLAP["cnet"]:
+        # (not while tracing for TorchScript export: a stream hand-off is a
+        # Python autograd Function the exported graph cannot hold)
+        if gpu and self.cfg.overlap_encoders and OVERLAP["cnet"] and not torch.jit.is_tracing():
             side = self._side_stream(dev)
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
