@@ -161,11 +161,25 @@ class RAFT(nn.Module):
     def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
         dev = image1.device
         gpu = dev.type == "cuda"
-        image1 = 2 * (image1 / 255.0) - 1.0
-        image2 = 2 * (image2 / 255.0) - 1.0
-        fmt = torch.channels_last if gpu else torch.contiguous_format
-        image1 = image1.contiguous(memory_format=fmt)
-        image2 = image2.contiguous(memory_format=fmt)
+        xin = None
+        if (gpu and image1.dtype == torch.float32 and image2.dtype == torch.float32
+                and image1.shape == image2.shape and not (image1.requires_grad or image2.requires_grad)):
+            # one kernel per image: x * 2/255 - 1 written straight into the two
+            # halves of ONE channels-last buffer -- the feature encoder's batched
+            # input (no separate scale / shift / layout-copy / cat kernels)
+            B = image1.shape[0]
+            xin = torch.empty((2 * B,) + tuple(image1.shape[1:]), device=dev,
+                              memory_format=torch.channels_last)
+            m1 = torch.tensor(-1.0)
+            torch.add(m1, image1, alpha=2.0 / 255.0, out=xin[:B])
+            torch.add(m1, image2, alpha=2.0 / 255.0, out=xin[B:])
+            image1, image2 = xin[:B], xin[B:]
+        else:
+            image1 = 2 * (image1 / 255.0) - 1.0
+            image2 = 2 * (image2 / 255.0) - 1.0
+            fmt = torch.channels_last if gpu else torch.contiguous_format
+            image1 = image1.contiguous(memory_format=fmt)
+            image2 = image2.contiguous(memory_format=fmt)
         hdim, cdim = self.hidden_dim, self.context_dim
         mixed = bool(self.cfg.mixed_precision) and gpu
 
@@ -174,9 +188,10 @@ class RAFT(nn.Module):
         # once per forward instead of once per iteration (and its gradient
         # accumulates over the 12 iterations before a single cast back).
         gru_ops.begin_forward()
-        if gpu:
+        if gpu and not torch.jit.is_tracing():
             # packed encoder-conv weights after an optimizer step: one batched
-            # repack on the main stream, before any stream forks (ops/wpack.py)
+            # repack on the main stream, before any stream forks (ops/wpack.py);
+            # not while tracing for export (stock ops only, nothing packed)
             wpack.refresh()
         # The context encoder (batch B) and the feature encoder + correlation
         # volume (batch 2B) are independent until the update loop: run cnet on
@@ -209,7 +224,7 @@ class RAFT(nn.Module):
         with self._autocast(dev), enc_defer:
             if side is not None:
                 # fnet (main) and cnet (side) stage by stage, interleaved on the host
-                xf = torch.cat([image1, image2], dim=0)
+                xf = xin if xin is not None else torch.cat([image1, image2], dim=0)
                 xc = image1
                 ff, fc = self.fnet.stage_fns(), self.cnet.stage_fns()
                 for k in range(max(len(ff), len(fc))):
