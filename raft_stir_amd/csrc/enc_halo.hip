@@ -259,14 +259,14 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   if (a.ntiles == 0) return true;
   const int cob = cin == 64 ? 64 : 32;
   const int gy = cdiv(cout, cob);
-  // 12 consecutive tiles per block (the LDS weights are loaded once per
-  // block).  In-situ A/B (scripts/ab_halo_tpb.sh, paired runs on one box):
-  // training 12 tiles 383 pairs/s, 16: 380, 24: 374, 48 (~persistent): 350,
-  // 2-8 or ~one block per CU: 368-379 -- the encoders run these convs on two
-  // HIP streams at once, and long-lived CU-filling blocks of one stream
-  // serialise behind the other's; eager 1088x436 inference 206 vs 194 FPS
-  // for one block per CU
-  a.tpb = 12;
+  // consecutive tiles per block (the LDS weights are loaded once per block),
+  // picked by in-situ A/B (scripts/ab_halo_tpb.sh, ab_halo_tpb_infer.sh; paired
+  // runs on one box): training (>= 1024 tile-blocks per conv) 12 tiles 383
+  // pairs/s, 16: 380, 24: 374, 48 (~persistent): 350, 2-8: 368-379 -- the
+  // encoders run these convs on two HIP streams at once and long-lived
+  // CU-filling blocks of one stream serialise behind the other's; graphed
+  // 1088x436 inference (< 1024) 4 tiles 286-289 FPS, 2: 278-281, 12: 266-268
+  a.tpb = a.ntiles * gy >= 1024 ? 12 : 4;
   static const int tpb_env = [] {  // RS_HALO_TPB: fixed tiles per block (tuning A/B)
     const char* e = getenv("RS_HALO_TPB");
     return e ? atoi(e) : 0;
