@@ -44,7 +44,7 @@ struct HArgs {
 
 template <int CIN, int COB>
 struct Cfg {
-  static constexpr int RPW = 2;                   // output rows per wave
+  static constexpr int RPW = CIN >= 128 ? 1 : 2;  // output rows per wave (LDS: 128-ch halo rows are 272 B)
   static constexpr int TH = 4 * RPW, TW = 32;     // output tile
   static constexpr int HR = TH + 2, HC = TW + 2;  // input halo
   static constexpr int RB = CIN * 2 + 16;         // LDS bytes per halo pixel / weight row
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void enc_halo_kernel(HArgs a) {
 
 // Supported (cin, cout-block) instantiations; false = caller falls back.
 bool enc_halo_supported(int cin, int cout) {
-  return (cin == 64 && cout % 64 == 0) || (cin == 96 && cout % 32 == 0);
+  return (cin == 64 && cout % 64 == 0) || ((cin == 96 || cin == 128) && cout % 32 == 0);
 }
 
 bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_t* y, int ystr, int B, int H, int W,
@@ -254,7 +254,7 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   a.xstr = xstr; a.ystr = ystr; a.Ktot = Ktot;
   a.B = B; a.H = H; a.W = W; a.Cout = cout;
   a.tiles_w = cdiv(W, 32);
-  a.tiles_img = cdiv(H, ench::Cfg<64, 64>::TH) * a.tiles_w;
+  a.tiles_img = cdiv(H, cin == 128 ? ench::Cfg<128, 32>::TH : ench::Cfg<64, 64>::TH) * a.tiles_w;
   a.ntiles = B * a.tiles_img;
   if (a.ntiles == 0) return true;
   const int cob = cin == 64 ? 64 : 32;
@@ -275,8 +275,10 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   const int gx = cdiv(a.ntiles, a.tpb);
   if (cin == 64)
     hipLaunchKernelGGL((ench::enc_halo_kernel<64, 64>), dim3(gx, gy), dim3(256), 0, stream, a);
-  else
+  else if (cin == 96)
     hipLaunchKernelGGL((ench::enc_halo_kernel<96, 32>), dim3(gx, gy), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((ench::enc_halo_kernel<128, 32>), dim3(gx, gy), dim3(256), 0, stream, a);
   return true;
 }
 

@@ -45,13 +45,20 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
 
 _WGRAD_DMA = os.environ.get("RS_WGRAD_DMA", "1") != "0"
 _HALO = os.environ.get("RS_ENC_HALO", "1") != "0"
+_HALO128 = os.environ.get("RS_ENC_HALO128", "0") == "1"  # layer3 (128 ch): opt-in, measured slower (profiles/r2/enc_halo_bench.txt)
 
 
 def _halo_ok(cin: int, cout: int) -> bool:
     """csrc/enc_halo.hip (halo tiles, weights resident in LDS) has
-    this conv: 64 input channels with a multiple of 64 outputs, or 96 inputs
-    with a multiple of 32 (the encoders' layer1 / layer2 3x3 convs)."""
-    return _HALO and ((cin == 64 and cout % 64 == 0) or (cin == 96 and cout % 32 == 0))
+    this conv: 64 input channels with a multiple of 64 outputs, or 96 / 128
+    inputs with a multiple of 32 (the encoders' layer1 / 2 / 3 3x3 convs)."""
+    if not _HALO:
+        return False
+    if cin == 64:
+        return cout % 64 == 0
+    if cin == 128 and not _HALO128:
+        return False
+    return cin in (96, 128) and cout % 32 == 0
 
 
 def _conv3x3_into(xn, wp, cin, cout, out, P):
