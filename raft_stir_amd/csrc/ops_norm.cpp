@@ -86,7 +86,8 @@ Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
   return y;
 }
 
-// returns dx, dres (empty if no residual), s1 (= dbeta per group), s2 (= dgamma per group).
+// returns dx, dres (empty if no residual), s1 (= dbeta per group), s2 (= dgamma per group),
+// and the (2, G, C) buffer s1 / s2 are views of.
 // batch_stats=false: the statistics were constants (BatchNorm in eval mode), so
 // dx = gamma * rstd * g without the mean/variance terms.
 std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const Tensor& mean,
@@ -107,7 +108,10 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
   const bool bf = x.scalar_type() == at::kBFloat16;
   auto fo = x.options().dtype(at::kFloat);
   Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
-  Tensor s1 = at::empty({G, C}, fo), s2 = at::empty({G, C}, fo);
+  // s1 / s2 are the two halves of one (2, G, C) buffer: the per-channel sums
+  // over groups (dbeta, dgamma) are then ONE reduction (ops/norm.py)
+  Tensor s12 = at::empty({2, G, C}, fo);
+  Tensor s1 = s12.select(0, 0), s2 = s12.select(0, 1);
   Tensor dx = at::empty_like(x);
   Tensor dres = res ? at::empty_like(x) : at::empty({0}, x.options());
   rs::norm_bwd_launch(bf, x.data_ptr(), dy.data_ptr(), res ? res->data_ptr() : nullptr,
@@ -115,7 +119,7 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
                       G, relu, batch_stats, ws.data_ptr<float>(), s1.data_ptr<float>(),
                       s2.data_ptr<float>(), dx.data_ptr(), res ? dres.data_ptr() : nullptr, stream());
   RS_CHECK_LAUNCH();
-  return {dx, dres, s1, s2};
+  return {dx, dres, s1, s2, s12};
 }
 
 }  // namespace

@@ -50,10 +50,16 @@ class _NormAct(torch.autograd.Function):
         x, gamma, beta, res, mean, rstd = ctx.saved_tensors
         dyn = _nhwc(dy.contiguous(memory_format=_CL)).to(x.dtype)
         rn = _nhwc(res) if res is not None else None
-        dx, dres, s1, s2 = torch.ops.raft_stir.norm_act_backward(
+        dx, dres, s1, s2, s12 = torch.ops.raft_stir.norm_act_backward(
             dyn, _nhwc(x), mean, rstd, gamma, beta, rn, ctx.relu, ctx.batch_stats)
-        dgamma = s2.sum(0) if gamma is not None and ctx.needs_input_grad[1] else None
-        dbeta = s1.sum(0) if beta is not None and ctx.needs_input_grad[2] else None
+        want_g = gamma is not None and ctx.needs_input_grad[1]
+        want_b = beta is not None and ctx.needs_input_grad[2]
+        if want_g and want_b:
+            d = s12.sum(1)  # (2, C): one reduction for dbeta and dgamma (s1 = s12[0], s2 = s12[1])
+            dbeta, dgamma = d[0], d[1]
+        else:
+            dgamma = s2.sum(0) if want_g else None
+            dbeta = s1.sum(0) if want_b else None
         dres_out = dres.permute(0, 3, 1, 2) if res is not None else None
         dbias = None
         if ctx.bias_meta is not None and ctx.needs_input_grad[8]:
