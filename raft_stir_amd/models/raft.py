@@ -65,6 +65,7 @@ class _StreamHandoff(torch.autograd.Function):
 
 
 _SIDE_STREAMS = {}  # (device index, slot) -> extra HIP stream
+_FUSED_PREP = os.environ.get("RS_FUSED_PREP", "1") != "0"  # one-kernel input normalisation into the fnet batch
 # per-mechanism switches of the multi-stream schedule (all gated by cfg.overlap_encoders)
 # defer_enc (encoder conv weight gradients on the deferred stream too) is off:
 # paired A/B on one box, 3 x 30 steps: 352 pairs/s on vs 366 off (the third
@@ -162,7 +163,7 @@ class RAFT(nn.Module):
         dev = image1.device
         gpu = dev.type == "cuda"
         xin = None
-        if (gpu and image1.dtype == torch.float32 and image2.dtype == torch.float32
+        if (gpu and _FUSED_PREP and image1.dtype == torch.float32 and image2.dtype == torch.float32
                 and image1.shape == image2.shape and not (image1.requires_grad or image2.requires_grad)):
             # one kernel per image: x * 2/255 - 1 written straight into the two
             # halves of ONE channels-last buffer -- the feature encoder's batched

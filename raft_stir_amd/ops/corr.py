@@ -22,6 +22,7 @@ zero-filled pyramid gradient each time) and then through
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -61,7 +62,7 @@ def from_nhwc(x: torch.Tensor) -> torch.Tensor:
 def _side_stream(dev):
     """The RAFT model's slot-0 side stream (models/raft.py), if its multi-stream
     schedule created one on this device."""
-    if dev.type != "cuda":
+    if dev.type != "cuda" or os.environ.get("RS_CORR_SIDE", "1") == "0":
         return None
     from ..models.raft import OVERLAP, _SIDE_STREAMS
     return _SIDE_STREAMS.get((dev.index, 0)) if OVERLAP.get("cnet", False) else None
