@@ -6,16 +6,23 @@ gradients).  ~50 such layouts exist for the two encoders.  Repacking each
 one with its own permute / zero / copy / cast kernels after every optimizer
 step is ~250 launches and ~2 ms of host time per training step; instead every
 layout is registered once as a static INDEX MAP into the concatenation of
-the source parameters (the layout function evaluated on an index tensor),
-and all layouts live as views of ONE flat bf16 buffer.  A repack of
-everything is then three kernels: cat(parameters) -> index_select -> cast
-into the flat buffer.
+its source parameters (the layout function evaluated on an index tensor).
+
+Layouts registered together live as views of one flat bf16 buffer (a
+CHUNK); a repack of a chunk is three kernels: cat(parameters) ->
+index_select -> cast into the flat buffer.  A chunk's storage never moves:
+layouts registered later (a second model, a deep copy, re-registration of a
+key) go into a NEW chunk, so a hipGraph captured against earlier views --
+``GraphedInference`` or the repack recorded by ``GraphedTrainStep`` -- keeps
+reading live, current storage (``snapshot()`` hands a captured graph strong
+references to every chunk it recorded).  A chunk is dropped once every
+parameter it was built from is gone.
 
 Staleness: runtime/weights.generation() (bumped by every optimizer step --
 fused AdamW does not bump ``_version``) plus the parameters' own version
 counters.  Under ``runtime.weights.repack_in_graph()`` (a captured training
 step) lookups never repack; the step body calls :func:`repack` itself so the
-three kernels are part of every replay.
+three kernels per chunk are part of every replay.
 """
 from __future__ import annotations
 
@@ -28,7 +35,7 @@ from ..runtime import weights as _wgen
 
 
 class _Entry:
-    __slots__ = ("refs", "layout", "local_map", "shape", "view", "vers")
+    __slots__ = ("refs", "layout", "local_map", "shape", "view", "vers", "chunk")
 
     def __init__(self, refs, layout, local_map, shape):
         self.refs = refs
@@ -37,56 +44,35 @@ class _Entry:
         self.shape = shape
         self.view = None
         self.vers = None
+        self.chunk = None
+
+    def alive(self) -> bool:
+        return all(r() is not None for r in self.refs)
 
 
-class _Registry:
-    def __init__(self, dev):
-        self.dev = dev
-        self.entries: Dict[tuple, _Entry] = {}
-        self.srcs: List[weakref.ref] = []      # distinct source parameters, registration order
-        self.src_ids: Dict[int, int] = {}
-        self.flat = None
-        self.gmap = None
-        self.dirty = True
-        self.gen = None
-        self._retired = []  # flat buffers of earlier layouts (registration phase only)
+class _Chunk:
+    """Entries packed together: one flat bf16 buffer, one gather map over
+    cat(the chunk's own distinct source parameters) + a trailing zero."""
 
-    # ---------------------------------------------------------------- layout
-    def _src_index(self, w):
-        i = self.src_ids.get(id(w))
-        if i is not None and self.srcs[i]() is w:
-            return i
-        self.srcs.append(weakref.ref(w))
-        self.src_ids[id(w)] = len(self.srcs) - 1
-        self.dirty = True
-        return len(self.srcs) - 1
-
-    def _rebuild(self, dev):
-        """Flat buffer + global gather map over every live entry."""
-        live = {k: e for k, e in self.entries.items() if all(r() is not None for r in e.refs)}
-        self.entries = live
-        # compact the source list to live parameters
-        srcs = []
-        ids = {}
-        for e in live.values():
+    def __init__(self, entries: List[_Entry], dev):
+        srcs, ids = [], {}
+        for e in entries:
             for r in e.refs:
                 w = r()
                 if id(w) not in ids:
                     ids[id(w)] = len(srcs)
                     srcs.append(r)
-        self.srcs, self.src_ids = srcs, ids
-        offs, o = [], 0
+        offs, o = {}, 0
         for r in srcs:
-            offs.append(o)
+            offs[id(r())] = o
             o += r().numel()
-        zero = o  # the appended zero
+        zero = o
         maps, n = [], 0
-        for e in live.values():
-            # local index space = cat(this entry's weights); translate to the global one
+        for e in entries:
             lo, trans = 0, []
             for r in e.refs:
                 w = r()
-                trans.append((lo, lo + w.numel(), offs[ids[id(w)]]))
+                trans.append((lo, lo + w.numel(), offs[id(w)]))
                 lo += w.numel()
             lm = e.local_map
             g = torch.full_like(lm, zero)
@@ -95,54 +81,77 @@ class _Registry:
                 g[sel] = lm[sel] - a + go
             maps.append(g)
             n += g.numel()
-        self.gmap = torch.cat(maps).to(dev) if maps else torch.zeros(0, dtype=torch.long, device=dev)
-        if self.flat is not None:  # earlier views may still be read by queued kernels on other streams
-            self._retired.append(self.flat)
+        self.srcs = srcs
+        self.numels = [r().numel() for r in srcs]
+        self.entries = list(entries)
+        self.gmap = torch.cat(maps).to(dev)
         self.flat = torch.empty(n, dtype=torch.bfloat16, device=dev)
         o = 0
-        for e in live.values():
+        for e in entries:
             k = e.local_map.numel()
             e.view = self.flat[o:o + k].view(e.shape)
+            e.chunk = self
             o += k
-        self.dirty = False
+
+    def alive(self) -> bool:
+        return any(e.alive() for e in self.entries)
+
+    @torch.no_grad()
+    def repack(self):
+        dev = self.flat.device
+        ws = [r() for r in self.srcs]
+        # a source that died (another model of the chunk was freed) packs as zeros:
+        # its layouts are unreachable, the live ones keep their offsets
+        parts = [w.detach().reshape(-1).float() if w is not None else torch.zeros(n, device=dev)
+                 for w, n in zip(ws, self.numels)]
+        src = torch.cat(parts + [torch.zeros(1, device=dev)])
+        self.flat.copy_(src.index_select(0, self.gmap))
+        for e in self.entries:
+            if e.alive():
+                e.vers = tuple((r().data_ptr(), r()._version) for r in e.refs)
+
+
+class _Registry:
+    def __init__(self, dev):
+        self.dev = dev
+        self.entries: Dict[tuple, _Entry] = {}   # key -> current entry
+        self.chunks: List[_Chunk] = []
+        self.pending: List[_Entry] = []          # registered, not yet in a chunk
+        self.gen = None
+
+    # ---------------------------------------------------------------- layout
+    def _flush(self):
+        """Build a chunk for the pending entries; drop chunks whose sources died."""
+        hold = []  # strong references across the allocations below (a GC pass must not free a source)
+        for e in self.pending:
+            hold.extend(r() for r in e.refs)
+        live = [e for e in self.pending if e.alive()]
+        self.pending = []
+        self.chunks = [c for c in self.chunks if c.alive()]
+        self.entries = {k: e for k, e in self.entries.items() if e.alive()}
+        if live:
+            self.chunks.append(_Chunk(live, self.dev))
+        del hold
 
     # ---------------------------------------------------------------- values
     @torch.no_grad()
     def repack(self):
-        """Every registered layout from the current parameter values (3 kernels)."""
+        """Every registered layout from the current parameter values (3 kernels per chunk)."""
         STATS["repacks"] += 1
-        # strong references for the whole repack: a cyclic GC pass triggered by
-        # an allocation below must not free a parameter between the liveness
-        # check and its use
-        hold, live = [], {}
-        for k, e in self.entries.items():
-            ws_ = [r() for r in e.refs]
-            if all(w is not None for w in ws_):
-                live[k] = e
-                hold.extend(ws_)
-        if len(live) != len(self.entries):
-            self.entries, self.dirty = live, True
-        if not live:
-            return
-        dev = self.dev
-        if self.dirty or self.flat is None:
-            self._rebuild(dev)
-        ws = [r() for r in self.srcs]
-        src = torch.cat([w.detach().reshape(-1).float() for w in ws] + [torch.zeros(1, device=dev)])
-        self.flat.copy_(src.index_select(0, self.gmap))
-        gen = _wgen.generation()
-        for e in self.entries.values():
-            e.vers = tuple((r().data_ptr(), r()._version) for r in e.refs)
-        self.gen = gen
+        if self.pending:
+            self._flush()
+        for c in self.chunks:
+            c.repack()
+        self.gen = _wgen.generation()
 
     def get(self, key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
         e = self.entries.get(key)
-        if e is None or any(r() is not w for r, w in zip(e.refs, weights)) or len(e.refs) != len(weights):
+        if e is None or len(e.refs) != len(weights) or any(r() is not w for r, w in zip(e.refs, weights)):
             e = self._register(key, weights, layout)
-        if _wgen.force_repack():  # captured training step: the body repacks explicitly
+        if _wgen.force_repack() and e.view is not None:  # captured training step: the body repacks explicitly
             return e.view
         vers = tuple((w.data_ptr(), w._version) for w in weights)
-        if self.dirty or e.view is None or self.gen != _wgen.generation() or e.vers != vers:
+        if e.view is None or self.gen != _wgen.generation() or e.vers != vers:
             self.repack()
         return e.view
 
@@ -158,10 +167,14 @@ class _Registry:
         lm = layout([t.float() for t in idx]).round().long() - 1
         e = _Entry(tuple(weakref.ref(w) for w in weights), layout, lm.reshape(-1).cpu(), tuple(lm.shape))
         self.entries[key] = e
-        for w in weights:
-            self._src_index(w)
-        self.dirty = True
+        self.pending.append(e)
         return e
+
+    def stale(self) -> bool:
+        if self.pending or self.gen != _wgen.generation():
+            return True
+        return any(e.vers != tuple((r().data_ptr(), r()._version) for r in e.refs)
+                   for e in self.entries.values() if e.alive())
 
 
 _REGS: Dict[torch.device, _Registry] = {}  # one per device
@@ -169,8 +182,8 @@ STATS = {"repacks": 0}  # tests / scripts: how often everything was repacked
 
 
 def packed(key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
-    """The bf16 packed tensor ``layout(weights)`` (a view of the flat buffer),
-    current with respect to every optimizer step / in-place write."""
+    """The bf16 packed tensor ``layout(weights)`` (a view of a chunk's flat
+    buffer), current with respect to every optimizer step / in-place write."""
     dev = weights[0].device
     reg = _REGS.get(dev)
     if reg is None:
@@ -183,10 +196,10 @@ def repack() -> None:
         reg.repack()
 
 
-def _stale(reg) -> bool:
-    return reg.dirty or reg.gen != _wgen.generation() or any(
-        e.vers != tuple((r().data_ptr(), r()._version) for r in e.refs)
-        for e in reg.entries.values() if all(r() is not None for r in e.refs))
+def snapshot() -> list:
+    """Strong references to every chunk's storage and gather map: a hipGraph
+    that recorded ``repack()`` keeps them for its whole life."""
+    return [(c.flat, c.gmap, list(c.srcs)) for reg in _REGS.values() for c in reg.chunks]
 
 
 def refresh() -> None:
@@ -195,7 +208,7 @@ def refresh() -> None:
     if _wgen.capturing() and not _wgen.force_repack():
         return
     for reg in _REGS.values():
-        if reg.entries and _stale(reg):
+        if (reg.entries or reg.pending) and reg.stale():
             reg.repack()
 
 

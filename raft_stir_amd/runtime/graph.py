@@ -15,7 +15,7 @@ from typing import Dict, Tuple
 
 import torch
 
-from .weights import refresh_all, repack_in_graph, weights_key
+from .weights import bump, refresh_all, repack_in_graph, weights_key
 
 
 class GraphedInference:
@@ -133,6 +133,11 @@ class GraphedTrainStep:
         # weight-packing kernels too, so every replay packs the current weights
         with torch.cuda.graph(self.graph), repack_in_graph():
             self.loss = self._body()
+        # the recorded repack reads these chunks' gather maps and writes their
+        # flat buffers on every replay: hold them for the graph's whole life
+        # (later registrations go to new chunks and never move these)
+        from ..ops import wpack
+        self._packed_storage = wpack.snapshot()
 
     def _body(self):
         from ..ops import wpack
@@ -150,4 +155,7 @@ class GraphedTrainStep:
         for dst, src in zip(self.static, batch):
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        # the replayed optimizer step moved the weights without touching
+        # _version / data_ptr: invalidate every packed-weight cache
+        bump()
         return self.loss

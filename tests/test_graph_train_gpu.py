@@ -48,7 +48,15 @@ def estep(b):
 for _ in range(3):
     estep(batches[0])
 le, lg = [], []
-for i in range(6):
+for i in range(8):
+    if i == 4:
+        # a model registered AFTER the capture (ADVICE r2: its packed layouts must
+        # not move or free the storage the captured repack reads)
+        m_x = copy.deepcopy(m_e)
+        with torch.no_grad():
+            m_x(batches[0][0], batches[0][1], iters=2)
+        import gc; gc.collect()
+        torch.cuda.empty_cache()
     b = batches[i % 4]
     le.append(float(estep(b)))
     lg.append(float(gs.step(b)))
@@ -56,6 +64,13 @@ torch.cuda.synchronize()
 w1 = torch.cat([p.detach().float().flatten() for p in m_g.parameters()])
 print("LOSSES", " ".join(f"{a:.5f},{b:.5f}" for a, b in zip(le, lg)))
 print("MOVED", float((w1 - w0).norm()))
+# eager inference after graphed steps sees the weights the replays wrote:
+# equal to a fresh model holding the same values (fresh packs)
+m_g.eval(); m_f = copy.deepcopy(m_g).eval()
+with torch.no_grad():
+    a = m_g(batches[1][0], batches[1][1], iters=4, test_mode=True)[1]
+    bb = m_f(batches[1][0], batches[1][1], iters=4, test_mode=True)[1]
+print("EVALDIFF", float((a - bb).abs().max()), float(bb.abs().max()))
 '''
 
 
@@ -67,8 +82,10 @@ def test_graphed_train_step_tracks_eager(cuda, tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("LOSSES")][-1]
     pairs = [tuple(map(float, t.split(","))) for t in line.split()[1:]]
-    assert len(pairs) == 6
+    assert len(pairs) == 8
     for e, g in pairs:
         assert abs(e - g) <= 0.05 * abs(e) + 1e-3, pairs
     moved = float([l for l in r.stdout.splitlines() if l.startswith("MOVED")][-1].split()[1])
     assert moved > 0
+    d, ref = map(float, [l for l in r.stdout.splitlines() if l.startswith("EVALDIFF")][-1].split()[1:])
+    assert d <= 1e-3 * max(ref, 1.0), (d, ref)

@@ -168,6 +168,37 @@ def test_fused_adamw_does_not_bump_version_but_generation_moves():
     assert wg.generation() == g0 + 1
 
 
+def test_wpack_views_never_move():
+    """layouts registered after a first pack (a second model) go to
+    a new chunk; the earlier views keep their storage (a captured graph reads
+    them) and stay current after an update; dead models' chunks are dropped."""
+    import gc
+    from raft_stir_amd.ops import wpack
+    from raft_stir_amd.ops.conv import pack_weight
+    lay = lambda ws: pack_weight(ws[0], [(32, [(0, 32, 0)])], 64, torch.float32)
+    w1 = torch.nn.Parameter(torch.randn(40, 32, 3, 3))
+    a = wpack.packed(("mv1", id(w1)), [w1], lay)
+    ptr = a.data_ptr()
+    reg = wpack._REGS[w1.device]
+    n_chunks = len(reg.chunks)
+    w2 = torch.nn.Parameter(torch.randn(40, 32, 3, 3))
+    b = wpack.packed(("mv2", id(w2)), [w2], lay)
+    assert len(reg.chunks) == n_chunks + 1
+    a2 = wpack.packed(("mv1", id(w1)), [w1], lay)
+    assert a2.data_ptr() == ptr
+    with torch.no_grad():
+        w1.add_(1.0)
+    wpack.refresh()
+    assert torch.equal(a, lay([w1.detach()]).to(torch.bfloat16))
+    assert torch.equal(b, lay([w2.detach()]).to(torch.bfloat16))
+    del w2, b
+    gc.collect()
+    w3 = torch.nn.Parameter(torch.randn(40, 32, 3, 3))
+    wpack.packed(("mv3", id(w3)), [w3], lay)
+    assert all(c.alive() for c in reg.chunks)
+    assert a.data_ptr() == ptr and torch.equal(a, lay([w1.detach()]).to(torch.bfloat16))
+
+
 def test_wpack_batched_layouts_follow_updates():
     """ops/wpack.py: layouts registered as index maps into the parameters,
     all views of one flat buffer, repacked together after an optimizer step
