@@ -1,0 +1,12 @@
+// conv_ws.h instantiations for the EK_RELUBWD epilogue class.
+#include "conv_ws.h"
+
+namespace rs {
+namespace conv {
+#ifdef RS_WS_LIST  // (kernel experiments: build a subset)
+RS_WS_DISPATCH(ws_relubwd, EK_RELUBWD, RS_WS_LIST)
+#else
+RS_WS_DISPATCH(ws_relubwd, EK_RELUBWD, RS_WS_1X1 RS_WS_3X3)
+#endif
+}  // namespace conv
+}  // namespace rs

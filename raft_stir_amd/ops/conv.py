@@ -107,17 +107,160 @@ def tuned_tiles() -> dict:
     return _TUNED
 
 
+# ---------------------------------------------------------------- weight-stationary kernel
+# csrc/conv_ws.hip: the weights of a wave's 32 output channels x (taps x Ktot /
+# ncs) input channels stay in VGPRs for the whole launch; the block walks a
+# 16-column strip down the image through an LDS ring of halo rows.
+WS_TILE = 48
+_G1, _G3, _GS = (4, 6, 8, 12, 16, 18, 24), (1, 2, 3, 4), (2, 4, 6)
+# instantiated (KH, KW) -> G per epilogue class (csrc/conv_ws_<class>.hip)
+WS_INST = {
+    "plain": {(1, 1): _G1, (3, 3): _G3},
+    "zr": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
+    "q": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
+    "relubwd": {(1, 1): _G1, (3, 3): _G3},
+    "acc": {(1, 1): _G1, (3, 3): _G3, (1, 5): _GS, (5, 1): _GS},
+    "qbwd": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
+}
+
+
+def ws_class(epi: int):
+    return {EPI_GRU_ZR: "zr", EPI_GRU_Q: "q", EPI_RELU_BWD: "relubwd", EPI_ACC_F32: "acc",
+            EPI_GRU_QBWD: "qbwd", EPI_FLOW: None}.get(epi, "plain")
+
+
+WS_G = {k: v for d in WS_INST.values() for k, v in d.items()}  # union (tests)
+_WS = os.environ.get("RS_CONV_WS", "1") != "0"
+_NUM_CUS = 256
+
+
+def frag_layout(w: torch.Tensor) -> torch.Tensor:
+    """[Cout_pad][taps][Ktot] packed weights (or index maps) -> the
+    weight-stationary kernel's fragment order, same shape: element
+    (cob, tap, kg, lane, j) = W[32 cob + lane % 32][tap][16 kg + 8 (lane // 32) + j],
+    i.e. one v_mfma_f32_32x32x16_bf16 A fragment = 1 KiB contiguous."""
+    cp, taps, k = w.shape
+    assert cp % 32 == 0 and k % 16 == 0, (cp, k)
+    return w.reshape(cp // 32, 32, taps, k // 16, 2, 8).permute(0, 2, 3, 4, 1, 5).reshape(cp, taps, k).contiguous()
+
+
+def ws_geometry(kh: int, kw: int, G: int, ncs: int, ncb: int, NB: int = 1):
+    """(ring-row slots, LDS slots, halo pieces per wave per tile) -- the checks of
+    ops_conv.cpp ws_setup; None if the configuration does not fit."""
+    TH, hwd, cs = 2 * NB, 16 + kw - 1, 2 * G + 1
+    rsp = (ncs * hwd * cs + 63) // 64 * 64
+    slots = (2 * TH + kh - 1) * rsp + ncs * ncb * NB * 256
+    ppw = -(-(TH * rsp // 64) // (ncs * ncb))
+    if slots > 10240 or ppw > 6 or ncs not in (4, 8) or ncs * ncb > 8 or kh * kw * G > 40:
+        return None
+    return rsp, slots, ppw
+
+
+def _ws_cost(B, H, W, cout, ktot, kh, kw, G, ncs, ncb):
+    """Rough cycle model of one launch (per-CU view): MFMA issue of the block's
+    tiles vs L2->CU bytes (weights once per block + halo rows), in rounds of
+    <= one block per CU.  Used only to rank candidates; measured tables win."""
+    geo = ws_geometry(kh, kw, G, ncs, ncb)
+    if geo is None:
+        return None
+    nw = ncs * ncb
+    ncob = -(-cout // 32)
+    ncog = -(-ncob // ncb)
+    nstrips = -(-W // 16)
+    base = ncog * B * nstrips
+    nrch = max(1, _NUM_CUS // base)
+    rpc = -(-H // nrch)
+    rpc += rpc & 1
+    nrch = -(-H // rpc)
+    blocks = base * nrch
+    rounds = -(-blocks // _NUM_CUS)
+    ntiles = -(-rpc // 2)
+    fr = kh * kw * G
+    tile_cyc = -(-nw // 4) * fr * 32 + 250 + (300 if ncs > 1 else 0)
+    wbytes = ncb * 32 * kh * kw * ktot * 2
+    hbytes = (rpc + kh - 1) * (16 + kw - 1) * ktot * 2
+    mem_cyc = (wbytes + hbytes) / 48.0
+    blk = max(1500 + wbytes / 64.0 + ntiles * tile_cyc, mem_cyc)
+    waste = ncog * ncb / ncob
+    return rounds * blk * (1.0 + 0.0 * waste), [G, 1, ncs, ncb, rpc]
+
+
+_WS_CFG: dict = {}
+
+
+def ws_config(B: int, H: int, W: int, cout: int, ktot: int, kh: int, kw: int, cout_pad: int, epi: int = EPI_BIAS):
+    """[G, NB, ncs, ncb, rows_per_chunk] for conv_ws, or None (no instantiated fit)."""
+    cls = ws_class(epi)
+    if cls is None:
+        return None
+    key = (B, H, W, cout, ktot, kh, kw, cout_pad, cls)
+    if key in _WS_CFG:
+        return _WS_CFG[key]
+    tuned = tuned_ws().get(f"{B}x{H}x{W}|{cout}|{ktot}|{kh}x{kw}")
+    best = None
+    if tuned is not None and tuned[0] in WS_INST[cls].get((kh, kw), ()):
+        best = (0.0, list(tuned))
+    else:
+        for G in WS_INST[cls].get((kh, kw), ()):
+            if ktot % (16 * G):
+                continue
+            ncs = ktot // (16 * G)
+            for ncb in (1, 2):
+                if ncs * ncb > 8 or ncs < 4:
+                    continue
+                ncob = -(-cout // 32)
+                if -(-ncob // ncb) * ncb * 32 > cout_pad:
+                    continue
+                c = _ws_cost(B, H, W, cout, ktot, kh, kw, G, ncs, ncb)
+                if c is not None and (best is None or c[0] < best[0]):
+                    best = c
+    cfg = best[1] if best is not None else None
+    _WS_CFG[key] = cfg
+    return cfg
+
+
+_TUNED_WS: dict | None = None
+
+
+def tuned_ws() -> dict:
+    global _TUNED_WS
+    if _TUNED_WS is None:
+        _TUNED_WS = {}
+        if os.environ.get("RS_CONV_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+            import json
+            with open(_TUNED_PATH) as f:
+                _TUNED_WS = {k: list(v) for k, v in json.load(f).get("ws", {}).items()}
+    return _TUNED_WS
+
+
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=None):
-    """segs: list of (NHWC bf16 buffer, channel offset, channels read)."""
+               aux2=None, a2off=0, tile=None, wf=None, ws_cfg=None):
+    """segs: list of (NHWC bf16 buffer, channel offset, channels read).
+    ``wf``: the same weights in frag_layout -- the weight-stationary kernel runs
+    when it has an instantiated configuration for the shape (unless ``tile``
+    forces a tile kernel or RS_CONV_WS=0)."""
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
     if _RECORD is not None:
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
-                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile))
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, wf=wf, ws_cfg=ws_cfg))
+    if wf is not None and (tile == WS_TILE or (tile is None and _WS)):
+        t0 = tensors[0]
+        cfg = ws_cfg if ws_cfg is not None else ws_config(t0.shape[0], t0.shape[1], t0.shape[2], cout, sum(chans),
+                                                          kh, kw, wf.shape[0], epi)
+        if cfg is not None:
+            if bias is not None and (bias.numel() % 4 or bias.data_ptr() % 16):
+                # the kernel reads the bias in aligned 4-channel vectors (the engines
+                # hand it padded, aligned biases; this copy is the slow path)
+                bias = pack_bias(bias, pad_to(bias.numel(), 4)).clone()
+            torch.ops.raft_stir.conv_ws(tensors, offs, chans, wf, bias, kh, kw, cout, epi, float(scale), hd,
+                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, list(cfg))
+            return
+        if tile == WS_TILE:
+            raise ValueError(f"conv_ws: no configuration for {tuple(t0.shape)} cout={cout} K={sum(chans)} {kh}x{kw}")
     if tile is None:
         t0 = tensors[0]
         tile = tuned_tiles().get(tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi))
