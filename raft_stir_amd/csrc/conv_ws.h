@@ -55,8 +55,8 @@ __device__ __forceinline__ void ws_wait_vm() {
 __device__ __forceinline__ void ws_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
 constexpr int kWsLdsSlots = 10240;  // 160 KiB in 16-B slots: one block per CU
-constexpr int kWsPieces = 6;        // halo-prefetch DMA pieces per wave per tile (host-checked)
-constexpr int kWsMaxSlices = 8;     // channel slices (NCS) per co-block (host-checked)
+constexpr int kWsPieces = 10;       // halo-prefetch DMA pieces per MFMA wave per tile (host-checked)
+constexpr int kWsSlices = 4;        // channel slices = MFMA waves per block (+ as many helper waves)
 
 template <int KH, int KW, int G, int NB>
 struct WsCfg {
@@ -269,268 +269,242 @@ constexpr int kWsStamps = 66;
   } while (0)
 #endif
 
-template <int KH, int KW, int G, int NB, int EK>
+template <int KH, int KW, int G, int EK>
 __global__ __launch_bounds__(512) void conv_ws_kernel(Args a) {
-  using C = WsCfg<KH, KW, G, NB>;
+  using C = WsCfg<KH, KW, G, 1>;
   constexpr int FR = C::FR, TH = C::TH, HWD = C::HWD, CS = C::CS, RR = C::RR, PH = C::PH, PW = C::PW;
   constexpr int CPW = C::CPW, NF = C::NF, D = C::D, NG = C::NG;
+  constexpr int NCS = kWsSlices;  // MFMA waves = channel slices; waves NCS .. 2*NCS-1 are the helpers
   __shared__ uint4 lds[kWsLdsSlots];
 
   RS_WS_STAMP(0);
   const int lane_ = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int NCS = a.ws_ncs, NCB = a.ws_ncb, NW = NCS * NCB;
-  const int s = wave % NCS, cb = wave / NCS;
-  const int RSP = a.ws_rsp;                 // slots per ring row (multiple of 64)
-  const int NPR = RSP >> 6;                 // DMA pieces per ring row
+  const bool mfma_wave = wave < NCS;
+  const int s = wave & (NCS - 1);  // MFMA wave: channel slice; helper: 8-channel output group
+  const int RSP = a.ws_rsp;        // slots per ring row (multiple of 64)
+  const int NPR = RSP >> 6;        // DMA pieces per ring row
   const int H = a.H, W = a.W;
 
-  // ---- block -> (co group, image, column strip, row chunk)
+  // ---- block -> (32-channel output block, image, column strip, row chunk)
   const int nstrips = a.ws_nstrips, nrch = a.ws_nrch;
   const int per_img = nstrips * nrch;
   const int nchunk = a.B * per_img;
+  // chunk-major block order: with the XCD remap, each XCD (private L2) takes a
+  // contiguous run of pixel chunks with ALL their output blocks, so its L2
+  // holds ~1/8 of the input rows (+ all the weights) instead of every row
+  const int ncob = gridDim.x / nchunk;
   const int lid = a.xcd_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  const int cog = lid / nchunk;
-  int rem = lid - cog * nchunk;
+  const int chunk = lid / ncob;
+  const int cob = lid - chunk * ncob;
+  int rem = chunk;
   const int img = rem / per_img;
   rem -= img * per_img;
   const int strip = rem / nrch, rch = rem - strip * nrch;
   const int x0 = strip * C::TW, R0 = rch * a.ws_rpc;
   const int R1 = min(H, R0 + a.ws_rpc);
   const int ntiles = (R1 - R0 + TH - 1) / TH;
-  const int cob = cog * NCB + cb;  // this wave's global 32-channel output block
-  const int HW = H * W;
   // segment base pointers and row strides (elements), in SGPRs
   const uint64_t sp0 = ws_sgpr64(a.seg[0].ptr), sp1 = ws_sgpr64(a.seg[1].ptr), sp2 = ws_sgpr64(a.seg[2].ptr);
   const int sr0 = __builtin_amdgcn_readfirstlane(W * a.seg[0].stride);
   const int sr1 = __builtin_amdgcn_readfirstlane(W * a.seg[1].stride);
   const int sr2 = __builtin_amdgcn_readfirstlane(W * a.seg[2].stride);
 
-  // ---- prologue 1: the tile-0 halo rows R0-PH .. R0+TH+PH-1 -> ring rows 0 .. TH+KH-2
+  // ---- prologue: the tile-0 halo rows R0-PH .. R0+TH+PH-1 -> ring rows 0 .. TH+KH-2 (all waves)
   uint4* const ring = lds;
   {
     const int np0 = (TH + KH - 1) * NPR;
-    for (int P = wave; P < np0; P += NW) {
+    for (int P = wave; P < np0; P += 2 * NCS) {
       const int rr = P / NPR, pc = P - rr * NPR;
       const int y = R0 - PH + rr;
       const int code = ws_col(a, pc * 64 + lane_, x0, HWD, CS, CPW, PW);
-      const void* src = (y >= 0 && y < H) ? ws_src(sp0, sp1, sp2, sr0, sr1, sr2, code, img * H + y) : (const void*)g_ws_zero;
+      const void* src =
+          (y >= 0 && y < H) ? ws_src(sp0, sp1, sp2, sr0, sr1, sr2, code, img * H + y) : (const void*)g_ws_zero;
       glds16(src, ring + rr * RSP + pc * 64);
     }
   }
-  // ---- prologue 2: this wave's weight fragments (fragment-packed, 1 KiB each)
-  u32x4_t wr[FR];
-  {
-    const int KG = a.ws_kg;
-    const u32x4_t* wp = reinterpret_cast<const u32x4_t*>(a.wf) + (size_t)cob * C::TAPS * KG * 64 + lane_;
-#pragma unroll
-    for (int t = 0; t < C::TAPS; ++t)
-#pragma unroll
-      for (int g = 0; g < G; ++g) wr[t * G + g] = wp[((size_t)t * KG + s * G + g) * 64];
-  }
-  // ---- per-lane sources of this wave's pieces of every later TH-row prefetch
-  // (host-checked: at most kWsPieces pieces per wave)
-  const int np = TH * NPR;
-  int pcode[kWsPieces];
-#pragma unroll
-  for (int i = 0; i < kWsPieces; ++i) {
-    const int P = wave + NW * i;
-    pcode[i] = 3;
-    if (P < np) {
-      const int rr = P / NPR, pc = P - rr * NPR;
-      pcode[i] = ws_col(a, pc * 64 + lane_, x0, HWD, CS, CPW, PW);
-    }
-  }
-
-  // ---- fragment read addresses: lane -> N-block pixel (row nr, column nc), k-half h
   const int l32 = lane_ & 31, nr_ = l32 >> 4, nc_ = l32 & 15, h_ = lane_ >> 5;
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0];
-  const uint32_t lane_off = lds0 + (uint32_t)(((s * HWD + nc_) * CS + h_) * 16);
-  const uint32_t row_bytes = (uint32_t)RSP * 16;
-  const int red0 = RR * RSP;  // partial-sum area (slots)
+  const int red0 = RR * RSP;  // partial sums: 2 buffers x [NCS slices][4 groups][64 lanes] slots
 
-  // the tile-0 halo (issued before the weights) has landed once at most the FR
-  // weight loads are outstanding; tile 0's MFMAs then wait for each weight
-  // fragment as it arrives (compiler-inserted counted waits).  The empty
-  // memory-clobbering asm keeps the weight loads above the counted wait.
-  asm volatile("" ::: "memory");
-  ws_wait_vm<FR>();
-  asm volatile("s_barrier" ::: "memory");
-  RS_WS_STAMP(1);
-
-  int rb = 0;  // ring row of tile t's first (top-halo) row = (t * TH) % RR
-  // one tile (t: its index); tile 0 runs first on its own so that only its
-  // MFMAs wait for the weight fragments (compiler-counted, fragment by fragment)
-  auto tile = [&](const int t) __attribute__((always_inline)) {
-    RS_WS_STAMP(2 + 4 * t);
-    // per (N-block, kernel row) LDS base of this lane's B fragments
-    uint32_t bbase[NB][KH];
+  if (mfma_wave) {
+    // ================= MFMA waves: weights in VGPRs, B fragments from the ring
+    u32x4_t wr[FR];
+    {
+      const int KG = a.ws_kg;
+      const u32x4_t* wp = reinterpret_cast<const u32x4_t*>(a.wf) + (size_t)cob * C::TAPS * KG * 64 + lane_;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+      for (int t = 0; t < C::TAPS; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) wr[t * G + g] = wp[((size_t)t * KG + s * G + g) * 64];
+    }
+    const uint32_t lane_off = lds0 + (uint32_t)(((s * HWD + nc_) * CS + h_) * 16);
+    const uint32_t row_bytes = (uint32_t)RSP * 16;
+    // the tile-0 halo (issued before the weights) has landed once at most the FR
+    // weight loads are outstanding; tile 0's MFMAs then wait for the weights
+    // (compiler-inserted counted waits).  The empty memory-clobbering asm keeps
+    // the weight loads above the counted wait.
+    asm volatile("" ::: "memory");
+    ws_wait_vm<FR>();
+    asm volatile("s_barrier" ::: "memory");
+    RS_WS_STAMP(1);
+    // the MFMA waves win issue arbitration against the helper wave on their SIMD
+    __builtin_amdgcn_s_setprio(1);
+
+    int rb = 0;  // ring row of tile t's first (top-halo) row = (t * TH) % RR
+    auto tile = [&](const int t) __attribute__((always_inline)) {
+      RS_WS_STAMP(2 + 4 * t);
+      // LDS base of this lane's B fragments per kernel row
+      uint32_t bbase[KH];
 #pragma unroll
       for (int ty = 0; ty < KH; ++ty) {
-        int rr = rb + 2 * nb + nr_ + ty;
+        int rr = rb + nr_ + ty;
         rr = rr >= RR ? rr - RR : rr;
-        bbase[nb][ty] = lane_off + (uint32_t)rr * row_bytes;
+        bbase[ty] = lane_off + (uint32_t)rr * row_bytes;
       }
-    const int ty0 = R0 + t * TH;
-    const bool more = t + 1 < ntiles;
-    const int ybase = R0 + (t + 1) * TH + PH;
-    // halo-prefetch piece i of the TH rows tile t+1 adds (their ring rows were
-    // last read by tile t-1); issued between the MFMA groups of this tile
-#define RS_WS_PIECE(I)                                                                             \
-  do {                                                                                             \
-    const int P = wave + NW * (I); /* wave-uniform */                                              \
-    if (more && P < np) {                                                                          \
-      const int prow = P / NPR, pdst = (P - prow * NPR) * 64;                                      \
-      const int y = ybase + prow;                                                                  \
-      const int rr = ((t + 1) * TH + KH - 1 + prow) % RR;                                          \
-      int code = pcode[I];                                                                         \
-      asm volatile("" : "+v"(code)); /* per-tile address math: nothing hoisted out of the loop */  \
-      const void* src = y < H ? ws_src(sp0, sp1, sp2, sr0, sr1, sr2, code, img * H + y)            \
-                              : (const void*)g_ws_zero;                                            \
-      glds16(src, ring + rr * RSP + pdst);                                                         \
-    }                                                                                              \
-  } while (0)
-    // epilogue operands of this wave's output units (4 channels x 1 pixel per
-    // lane): unit u = s + k*NCS of the co-block's 4*NB (N-block, 8-channel
-    // group) units -- at most NB per wave (host-checked NCS >= 4); loaded
-    // during the MFMAs, used after the reduction
-    WsPre pre[NB];
-#define RS_WS_PRE()                                                                                \
-  _Pragma("unroll") for (int k_ = 0; k_ < NB; ++k_) {                                              \
-    const int u = s + k_ * NCS; /* wave-uniform */                                                 \
-    const int nb = u >> 2, g = u & 3;                                                              \
-    const int co = cob * 32 + 8 * g + 4 * h_;                                                      \
-    const int y = ty0 + 2 * nb + nr_, x = x0 + nc_;                                                \
-    const bool ok = u < 4 * NB && co < a.Cout && y < R1 && x < W;                                  \
-    ws_pre<EK>(a, co, (img * H + y) * W + x, ok, pre[k_]);                                         \
-  }
-
-    f32x16_t acc[NB];
+      f32x16_t acc;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[nb][j] = 0.f;
-
-    // MFMA i (0 .. NF-1): N-block i / FR, fragment f = i % FR = (ty*KW + tx)*G + g
-    u32x4_t bf[2][D];
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      // MFMA i (0 .. NF-1): fragment i = (ty*KW + tx)*G + g.  B fragments are
+      // read in groups of D, two groups ahead of their MFMAs (3 buffers)
+      u32x4_t bf[3][D];
 #define RS_WS_READ(GRP, BUF)                                                                     \
   _Pragma("unroll") for (int d = 0; d < D; ++d) {                                                \
     const int i_ = (GRP) * D + d;                                                                \
     if (i_ < NF) {                                                                               \
-      const int nb_ = i_ / FR, f_ = i_ % FR;                                                     \
-      const int tap_ = f_ / G, g_ = f_ % G;                                                      \
+      const int tap_ = i_ / G, g_ = i_ % G;                                                      \
       const int ty_ = tap_ / KW, tx_ = tap_ % KW;                                                \
       asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bf[BUF][d])                           \
-                   : "v"(bbase[nb_][ty_]), "i"((tx_ * CS + 2 * g_) * 16) : "memory");           \
+                   : "v"(bbase[ty_]), "i"((tx_ * CS + 2 * g_) * 16) : "memory");                \
     }                                                                                            \
   }
-    RS_WS_READ(0, 0);
+      RS_WS_READ(0, 0);
+      if (NG > 1) RS_WS_READ(1, 1);
 #pragma unroll
-    for (int k = 0; k < NG; ++k) {
-      // per-tile overhead in the MFMA shadow: epilogue operand loads, then
-      // one halo-prefetch piece per group
-      if (k == (NG > 1 ? 1 : 0)) RS_WS_PRE();
+      for (int k = 0; k < NG; ++k) {
+        // reads still in flight after group k's: groups k+1 and k+2
+        if (k + 2 < NG) RS_WS_READ(k + 2, (k + 2) % 3);
+        const int after = (k + 1 < NG ? ((k + 2) * D <= NF ? D : NF - (k + 1) * D) : 0) +
+                          (k + 2 < NG ? ((k + 3) * D <= NF ? D : NF - (k + 2) * D) : 0);
+        if (after >= 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        else if (after == 7) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+        else if (after == 6) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+        else if (after == 5) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
+        else if (after == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+        else if (after == 3) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+        else if (after == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if (after == 1) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int i = 0; i < kWsPieces; ++i)
-        if ((2 + i < NG ? 2 + i : NG - 1) == k) RS_WS_PIECE(i);
-      if (k + 1 < NG) {
-        RS_WS_READ(k + 1, (k + 1) & 1);
-        const int n_next = (k + 2) * D <= NF ? D : NF - (k + 1) * D;
-        if (n_next >= D) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-        else if (n_next == 3) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
-        else if (n_next == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
+        for (int d = 0; d < D; ++d) asm volatile("" : "+v"(bf[k % 3][d]));
 #pragma unroll
-      for (int d = 0; d < D; ++d) asm volatile("" : "+v"(bf[k & 1][d]));
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int i = k * D + d;
-        if (i < NF) {
-          const int nb = i / FR, f = i % FR;
-          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, wr[f]),
-                                                            __builtin_bit_cast(bf16x8_t, bf[k & 1][d]), acc[nb],
-                                                            0, 0, 0);
+        for (int d = 0; d < D; ++d) {
+          const int i = k * D + d;
+          if (i < NF)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, wr[i]),
+                                                          __builtin_bit_cast(bf16x8_t, bf[k % 3][d]), acc, 0, 0, 0);
         }
       }
-    }
 #undef RS_WS_READ
-#undef RS_WS_PRE
-#undef RS_WS_PIECE
-
-    // ---- reduce the channel-slice partials, epilogue
-    // lane coordinates re-materialised per tile: keeps the compiler from
-    // hoisting per-lane epilogue addresses out of the loop (VGPR pressure)
-    int h = h_, nr = nr_, nc = nc_, lane = lane_;
-    asm volatile("" : "+v"(h), "+v"(nr), "+v"(nc), "+v"(lane));
-    RS_WS_STAMP(3 + 4 * t);
-    // partial (cb, s, nb, g) -> red slots [((cb*NCS + s)*NB + nb)*4 + g]*64 + lane
+      RS_WS_STAMP(3 + 4 * t);
+      // this slice's partial of the 4 output groups -> red[t & 1][s][g]; a
+      // compiler-visible store (it pads the MFMA-result -> LDS-store hazard,
+      // which an inline-asm ds_write right behind the last MFMA does not get)
+      const uint32_t paddr = lds0 + (uint32_t)((red0 + ((t & 1) * NCS * 4 + s * 4) * 64 + lane_) * 16);
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<__attribute__((address_space(3))) f32x4_t*>(paddr + g * 1024) =
+            f32x4_t{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+      ws_wait_lgkm0();
+      asm volatile("s_barrier" ::: "memory");
+      RS_WS_STAMP(4 + 4 * t);
+    };
+    if (ntiles > 0) tile(0);
+    // every weight load has retired: redefine the fragments so the compiler
+    // inserts no vmcnt wait for them in the loop (it would drain the prefetch)
+    ws_wait_vm<0>();
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        // a compiler-visible store: it pads the MFMA-result -> LDS-store hazard
-        // (an inline-asm ds_write right behind the last MFMA read stale accumulators)
-        const uint32_t addr = lds0 + (uint32_t)((red0 + (((cb * NCS + s) * NB + nb) * 4 + g) * 64 + lane) * 16);
-        *reinterpret_cast<__attribute__((address_space(3))) f32x4_t*>(addr) =
-            f32x4_t{acc[nb][4 * g], acc[nb][4 * g + 1], acc[nb][4 * g + 2], acc[nb][4 * g + 3]};
+    for (int f = 0; f < FR; ++f) asm volatile("" : "+v"(wr[f]));
+    for (int t = 1; t < ntiles; ++t) {
+      rb += TH;
+      rb = rb >= RR ? rb - RR : rb;
+      tile(t);
+    }
+  } else {
+    // ================= helper waves, while the MFMA waves compute tile t:
+    // the halo rows tile t+1 adds (LDS-DMA), tile t-1's reduction + epilogue,
+    // and tile t's epilogue operands (loaded a tile ahead)
+    const int np = TH * NPR;
+    int pcode[kWsPieces];  // per-lane DMA source columns of pieces s, s + NCS, ... (host-checked count)
+#pragma unroll
+    for (int i = 0; i < kWsPieces; ++i) {
+      const int P = s + NCS * i;
+      pcode[i] = 3;
+      if (P < np) {
+        const int rr = P / NPR, pc = P - rr * NPR;
+        pcode[i] = ws_col(a, pc * 64 + lane_, x0, HWD, CS, CPW, PW);
       }
-    ws_wait_vm<0>();  // this wave's pieces of the next tile's rows + the epilogue operands have landed
-    ws_wait_lgkm0();
+    }
+    ws_wait_vm<0>();
     asm volatile("s_barrier" ::: "memory");
-    RS_WS_STAMP(4 + 4 * t);
+    const int g = s;
+    WsPre preC, preN;
+    preC.bo = preN.bo = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    preC.a1 = preC.a2 = preN.a1 = preN.a2 = make_uint2(0u, 0u);
+    for (int t = 0; t <= ntiles; ++t) {
+      if (t + 1 < ntiles) {
+        // pieces of the TH rows tile t+1 adds; their ring rows were last read
+        // by tile t-1, whose MFMAs finished before the previous barrier
+        const int ybase = R0 + (t + 1) * TH + PH;
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      const int u = s + k * NCS;
-      if (u >= 4 * NB) break;
-      const int nb = u >> 2, g = u & 3;
+        for (int i = 0; i < kWsPieces; ++i) {
+          const int P = s + NCS * i;  // wave-uniform
+          if (P < np) {
+            const int prow = P / NPR, pdst = (P - prow * NPR) * 64;
+            const int y = ybase + prow;
+            const int rr = ((t + 1) * TH + KH - 1 + prow) % RR;
+            int code = pcode[i];
+            asm volatile("" : "+v"(code));  // per-tile address math: nothing hoisted out of the loop
+            const void* src =
+                y < H ? ws_src(sp0, sp1, sp2, sr0, sr1, sr2, code, img * H + y) : (const void*)g_ws_zero;
+            glds16(src, ring + rr * RSP + pdst);
+          }
+        }
+      }
+      int h = h_, nr = nr_, nc = nc_, lane = lane_;
+      asm volatile("" : "+v"(h), "+v"(nr), "+v"(nc), "+v"(lane));  // no per-lane hoisting out of the loop
       const int co = cob * 32 + 8 * g + 4 * h;
-      // NCS is 4 or 8 (host-checked): 4 unconditional reads + 4 more under one uniform branch
-      const uint32_t rbase = lds0 + (uint32_t)((red0 + ((cb * NCS * NB + nb) * 4 + g) * 64 + lane) * 16);
-      const uint32_t rstep = (uint32_t)(NB * 4 * 64 * 16);
-      f32x4_t r0, r1, r2, r3;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(r0) : "v"(rbase) : "memory");
-      asm volatile("ds_read_b128 %0, %1" : "=v"(r1) : "v"(rbase + rstep) : "memory");
-      asm volatile("ds_read_b128 %0, %1" : "=v"(r2) : "v"(rbase + 2 * rstep) : "memory");
-      asm volatile("ds_read_b128 %0, %1" : "=v"(r3) : "v"(rbase + 3 * rstep) : "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (r0[j] + r1[j]) + (r2[j] + r3[j]);
-      if (NCS == 8) {
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r0) : "v"(rbase + 4 * rstep) : "memory");
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r1) : "v"(rbase + 5 * rstep) : "memory");
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r2) : "v"(rbase + 6 * rstep) : "memory");
-        asm volatile("ds_read_b128 %0, %1" : "=v"(r3) : "v"(rbase + 7 * rstep) : "memory");
+      const int x = x0 + nc;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (t >= 1) {
+        const uint32_t rbase = lds0 + (uint32_t)((red0 + (((t - 1) & 1) * NCS * 4 + g) * 64 + lane) * 16);
+        f32x4_t r0, r1, r2, r3;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(r0) : "v"(rbase) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(r1) : "v"(rbase) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:8192" : "=v"(r2) : "v"(rbase) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:12288" : "=v"(r3) : "v"(rbase) : "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (r0[j] + r1[j]) + (r2[j] + r3[j]);
+        for (int j = 0; j < 4; ++j) v[j] = (r0[j] + r1[j]) + (r2[j] + r3[j]);
       }
-      const int y = ty0 + 2 * nb + nr, x = x0 + nc;
-      if (co < a.Cout && y < R1 && x < W) ws_fin<EK>(a, v, co, (img * H + y) * W + x, pre[k]);
+      // the DMA pieces just issued (due before the barrier) and the operands
+      // loaded in the previous phase; every store of this phase comes after
+      // this wait, so it never waits for a store
+      ws_wait_vm<0>();
+      if (t >= 1) {
+        const int y = R0 + (t - 1) * TH + nr;
+        if (co < a.Cout && y < R1 && x < W) ws_fin<EK>(a, v, co, (img * H + y) * W + x, preC);
+      }
+      if (t < ntiles) {
+        const int y = R0 + t * TH + nr;
+        ws_pre<EK>(a, co, (img * H + y) * W + x, co < a.Cout && y < R1 && x < W, preN);
+      }
+      preC = preN;
+      if (t < ntiles) asm volatile("s_barrier" ::: "memory");
     }
-    RS_WS_STAMP(5 + 4 * t);
-    asm volatile("s_barrier" ::: "memory");  // partial area free for the next tile
-  };
-  if (ntiles > 0) tile(0);
-  // every weight load has retired: redefine the fragments so the compiler
-  // inserts no vmcnt wait for them in the loop (it would drain the prefetch)
-  ws_wait_vm<0>();
-#pragma unroll
-  for (int f = 0; f < FR; ++f) asm volatile("" : "+v"(wr[f]));
-  for (int t = 1; t < ntiles; ++t) {
-    rb += TH;
-    rb = rb >= RR ? rb - RR : rb;
-    tile(t);
   }
 }
-
 
 // launch one instantiation (a == nullptr: only report whether it exists);
 // each epilogue class's instantiations live in their own translation unit
@@ -538,8 +512,8 @@ __global__ __launch_bounds__(512) void conv_ws_kernel(Args a) {
 #define RS_WS(KH_, KW_, G_)                                                                           \
   if (KH == KH_ && KW == KW_ && G == G_) {                                                            \
     if (a)                                                                                            \
-      hipLaunchKernelGGL((conv::conv_ws_kernel<KH_, KW_, G_, 1, EK_>), dim3(nblocks),                 \
-                         dim3(64 * a->ws_ncs * a->ws_ncb), 0, stream, *a);                            \
+      hipLaunchKernelGGL((conv::conv_ws_kernel<KH_, KW_, G_, EK_>), dim3(nblocks), dim3(64 * 2 * kWsSlices), \
+                         0, stream, *a);                                                              \
     return true;                                                                                      \
   }
 #define RS_WS_1X1 RS_WS(1, 1, 4) RS_WS(1, 1, 6) RS_WS(1, 1, 8) RS_WS(1, 1, 12) RS_WS(1, 1, 16) RS_WS(1, 1, 18) RS_WS(1, 1, 24)

@@ -101,17 +101,17 @@ void ws_setup(rs::ConvLaunch& L, const Tensor& wf, at::IntArrayRef cfg, int Ktot
   const int G = cfg[0], NB = cfg[1], ncs = cfg[2], ncb = cfg[3], rpc = cfg[4];
   TORCH_CHECK(rs::conv_ws_instantiated(L.KH, L.KW, G, NB, L.epi), "conv_ws: (KH=", L.KH, ", KW=", L.KW, ", G=", G,
               ", NB=", NB, ", epi=", L.epi, ") is not instantiated (csrc/conv_ws_*.hip)");
-  TORCH_CHECK((ncs == 4 || ncs == 8) && ncb >= 1 && ncs * ncb <= 8, "conv_ws: ncs in {4, 8}, ncs * ncb <= 8 waves");
-  TORCH_CHECK(G >= 1 && ncs * 16 * G == Ktot, "conv_ws: Ktot (", Ktot, ") must equal ncs * 16 * G");
+  TORCH_CHECK(ncs == 4 && ncb == 1, "conv_ws: 4 channel slices x 1 output block per workgroup");
+  TORCH_CHECK(G >= 1 && ncs * 16 * G == Ktot, "conv_ws: Ktot (", Ktot, ") must equal 64 * G");
   TORCH_CHECK(L.KH * L.KW * G <= 40, "conv_ws: too many weight fragments per wave");
   TORCH_CHECK(rpc >= 1, "conv_ws: rows per chunk");
   const int TH = 2 * NB, HWD = 16 + L.KW - 1, CS = 2 * G + 1;
   const int rsp = (ncs * HWD * CS + 63) / 64 * 64;
   const int RR = 2 * TH + L.KH - 1;
-  const int slots = RR * rsp + ncs * ncb * NB * 256;
+  const int slots = RR * rsp + 2 * ncs * 4 * 64;  // halo ring + double-buffered partial sums
   TORCH_CHECK(slots <= 10240, "conv_ws: LDS ring + partials exceed 160 KiB (", slots * 16, " B)");
   const int pieces = TH * rsp / 64;
-  TORCH_CHECK((pieces + ncs * ncb - 1) / (ncs * ncb) <= 6, "conv_ws: more than 6 halo pieces per wave");
+  TORCH_CHECK((pieces + ncs - 1) / ncs <= 10, "conv_ws: more than 10 halo pieces per MFMA wave");
   const int ncob = (L.Cout + 31) / 32, ncog = (ncob + ncb - 1) / ncb;
   TORCH_CHECK(wf.is_cuda() && wf.is_contiguous() && wf.scalar_type() == at::kBFloat16 && wf.dim() == 3 &&
                   wf.size(1) == L.KH * L.KW && wf.size(2) == Ktot && wf.size(0) % 32 == 0 &&

@@ -144,45 +144,25 @@ def frag_layout(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(cp // 32, 32, taps, k // 16, 2, 8).permute(0, 2, 3, 4, 1, 5).reshape(cp, taps, k).contiguous()
 
 
-def ws_geometry(kh: int, kw: int, G: int, ncs: int, ncb: int, NB: int = 1):
-    """(ring-row slots, LDS slots, halo pieces per wave per tile) -- the checks of
-    ops_conv.cpp ws_setup; None if the configuration does not fit."""
+def ws_geometry(kh: int, kw: int, G: int, ncs: int = 4, ncb: int = 1, NB: int = 1):
+    """(ring-row slots, LDS slots, halo pieces per MFMA wave per tile) -- the
+    checks of ops_conv.cpp ws_setup; None if the configuration does not fit."""
     TH, hwd, cs = 2 * NB, 16 + kw - 1, 2 * G + 1
     rsp = (ncs * hwd * cs + 63) // 64 * 64
-    slots = (2 * TH + kh - 1) * rsp + ncs * ncb * NB * 256
-    ppw = -(-(TH * rsp // 64) // (ncs * ncb))
-    if slots > 10240 or ppw > 6 or ncs not in (4, 8) or ncs * ncb > 8 or kh * kw * G > 40:
+    slots = (2 * TH + kh - 1) * rsp + 2 * ncs * 4 * 64
+    ppw = -(-(TH * rsp // 64) // ncs)
+    if slots > 10240 or ppw > 10 or ncs != 4 or ncb != 1 or NB != 1 or kh * kw * G > 40:
         return None
     return rsp, slots, ppw
 
 
-def _ws_cost(B, H, W, cout, ktot, kh, kw, G, ncs, ncb):
-    """Rough cycle model of one launch (per-CU view): MFMA issue of the block's
-    tiles vs L2->CU bytes (weights once per block + halo rows), in rounds of
-    <= one block per CU.  Used only to rank candidates; measured tables win."""
-    geo = ws_geometry(kh, kw, G, ncs, ncb)
-    if geo is None:
-        return None
-    nw = ncs * ncb
-    ncob = -(-cout // 32)
-    ncog = -(-ncob // ncb)
-    nstrips = -(-W // 16)
-    base = ncog * B * nstrips
-    nrch = max(1, _NUM_CUS // base)
+def ws_rows_per_chunk(B: int, H: int, W: int, cout: int, target: int = _NUM_CUS) -> int:
+    """Rows per block so that the grid is ~one block per CU (blocks =
+    ceil(cout/32) x B x ceil(W/16) x ceil(H/rpc)); even (2-row tiles)."""
+    base = -(-cout // 32) * B * (-(-W // 16))
+    nrch = max(1, target // base)
     rpc = -(-H // nrch)
-    rpc += rpc & 1
-    nrch = -(-H // rpc)
-    blocks = base * nrch
-    rounds = -(-blocks // _NUM_CUS)
-    ntiles = -(-rpc // 2)
-    fr = kh * kw * G
-    tile_cyc = -(-nw // 4) * fr * 32 + 250 + (300 if ncs > 1 else 0)
-    wbytes = ncb * 32 * kh * kw * ktot * 2
-    hbytes = (rpc + kh - 1) * (16 + kw - 1) * ktot * 2
-    mem_cyc = (wbytes + hbytes) / 48.0
-    blk = max(1500 + wbytes / 64.0 + ntiles * tile_cyc, mem_cyc)
-    waste = ncog * ncb / ncob
-    return rounds * blk * (1.0 + 0.0 * waste), [G, 1, ncs, ncb, rpc]
+    return rpc + (rpc & 1)
 
 
 _WS_CFG: dict = {}
@@ -191,30 +171,17 @@ _WS_CFG: dict = {}
 def ws_config(B: int, H: int, W: int, cout: int, ktot: int, kh: int, kw: int, cout_pad: int, epi: int = EPI_BIAS):
     """[G, NB, ncs, ncb, rows_per_chunk] for conv_ws, or None (no instantiated fit)."""
     cls = ws_class(epi)
-    if cls is None:
+    if cls is None or ktot % 64:
         return None
     key = (B, H, W, cout, ktot, kh, kw, cout_pad, cls)
     if key in _WS_CFG:
         return _WS_CFG[key]
-    tuned = tuned_ws().get(f"{B}x{H}x{W}|{cout}|{ktot}|{kh}x{kw}")
-    best = None
-    if tuned is not None and tuned[0] in WS_INST[cls].get((kh, kw), ()):
-        best = (0.0, list(tuned))
-    else:
-        for G in WS_INST[cls].get((kh, kw), ()):
-            if ktot % (16 * G):
-                continue
-            ncs = ktot // (16 * G)
-            for ncb in (1, 2):
-                if ncs * ncb > 8 or ncs < 4:
-                    continue
-                ncob = -(-cout // 32)
-                if -(-ncob // ncb) * ncb * 32 > cout_pad:
-                    continue
-                c = _ws_cost(B, H, W, cout, ktot, kh, kw, G, ncs, ncb)
-                if c is not None and (best is None or c[0] < best[0]):
-                    best = c
-    cfg = best[1] if best is not None else None
+    G = ktot // 64
+    cfg = None
+    if G in WS_INST[cls].get((kh, kw), ()) and ws_geometry(kh, kw, G) is not None and -(-cout // 32) * 32 <= cout_pad:
+        tuned = tuned_ws().get(f"{B}x{H}x{W}|{cout}|{ktot}|{kh}x{kw}")
+        rpc = int(tuned[4]) if tuned is not None else ws_rows_per_chunk(B, H, W, cout)
+        cfg = [G, 1, 4, 1, rpc]
     _WS_CFG[key] = cfg
     return cfg
 

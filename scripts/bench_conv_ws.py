@@ -25,26 +25,15 @@ import torch  # noqa: E402
 
 
 def candidates(C, B, H, W, cout, ktot, kh, kw, cout_pad, epi):
+    """rows-per-chunk variants of the one configuration (grid ~1x / 2x the CUs)"""
+    base = C.ws_config(B, H, W, cout, ktot, kh, kw, cout_pad, epi)
+    if base is None:
+        return []
     out = []
-    for G in C.WS_INST[C.ws_class(epi)].get((kh, kw), ()):
-        if ktot % (16 * G):
-            continue
-        ncs = ktot // (16 * G)
-        for ncb in (1, 2, 4, 8):
-            if ncs * ncb > 8 or ncs < 4:
-                continue
-            ncob = -(-cout // 32)
-            if -(-ncob // ncb) * ncb * 32 > cout_pad or C.ws_geometry(kh, kw, G, ncs, ncb) is None:
-                continue
-            ncog = -(-ncob // ncb)
-            base = ncog * B * (-(-W // 16))
-            for target in (256, 512):
-                nrch = max(1, target // base)
-                rpc = -(-H // nrch)
-                rpc += rpc & 1
-                cfg = [G, 1, ncs, ncb, rpc]
-                if cfg not in out:
-                    out.append(cfg)
+    for target in (128, 256, 512):
+        cfg = base[:4] + [C.ws_rows_per_chunk(B, H, W, cout, target)]
+        if cfg not in out:
+            out.append(cfg)
     return out
 
 

@@ -24,13 +24,8 @@ def _cases():
     out = []
     for (kh, kw), gs in WS_INST["acc"].items():
         for G in gs:
-            for ncs in (4, 8):
-                if (G * ncs) % 2 or G * ncs * 16 > 640:
-                    continue
-                for ncb in (1, 2, 4):
-                    if ws_geometry(kh, kw, G, ncs, ncb) is None or ncs * ncb > 8:
-                        continue
-                    out.append((kh, kw, G, ncs, ncb))
+            if ws_geometry(kh, kw, G) is not None:
+                out.append((kh, kw, G, 4, 1))
     return out
 
 
