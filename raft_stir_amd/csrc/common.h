@@ -53,6 +53,33 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Reduce-scatter across groups of L lanes (L a power of two; the lanes that
+// differ only in their low log2(L) bits): every lane enters with N partial
+// values and leaves with the group totals of N/L of them in v[0 .. N/L), the
+// totals of entries (N/L) * (lane & (L-1)) + k.  log2(L) exchange steps, each
+// sending half of the still-live values (N - N/L shuffles in all, instead of
+// N * log2(L) for a butterfly all-reduce of every value).  All lanes of the
+// wave must be active.
+template <int N0, int n, int m>
+__device__ __forceinline__ void rscat_step(float (&v)[N0], int lane) {
+  if constexpr (m >= 1) {
+    constexpr int half = n / 2;
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float send = up ? v[i] : v[i + half];
+      const float keep = up ? v[i + half] : v[i];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+    rscat_step<N0, half, m / 2>(v, lane);
+  }
+}
+template <int N, int L>
+__device__ __forceinline__ void lane_reduce_scatter(float (&v)[N], int lane) {
+  static_assert(N % L == 0 && (L & (L - 1)) == 0, "N must be a multiple of the power-of-two group size");
+  rscat_step<N, N, L / 2>(v, lane);
+}
+
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ __forceinline__ int round_up(int a, int b) { return cdiv(a, b) * b; }
 

@@ -884,6 +884,10 @@ struct ConvLaunch {
   const void* wf;
   int ws_G, ws_NB, ws_ncs, ws_ncb, ws_rpc, ws_nstrips, ws_nrch, ws_rsp, ws_blocks;
   void* ws_stamps;
+  // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
+  const float* chs;
+  float* stats;
+  int stats_ps;
 };
 
 void conv_launch(const ConvLaunch& L, hipStream_t stream) {
@@ -907,6 +911,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
   for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
   a.w_bytes = L.w_bytes;
+  a.chs = L.chs; a.stats = L.stats; a.stats_ps = L.stats_ps;
   static const int xcd_env = [] {
     const char* e = getenv("RS_CONV_XCD_REMAP");
     return e ? atoi(e) : 1;
@@ -948,10 +953,6 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   }
   if (L.tile >= 42 && L.tile <= 47) {  // lean unrolled-tap tiles (conv_v2.hip)
     conv_v2_launch(a, L.tile, stream);
-    return;
-  }
-  if (L.tile >= 34 && L.tile <= 41) {  // pipelined halo tiles (conv_hx.hip)
-    conv_hx_launch(a, L.tile, stream);
     return;
   }
   if (L.tile == 5) {

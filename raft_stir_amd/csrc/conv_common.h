@@ -1,4 +1,4 @@
-// Shared pieces of the implicit-GEMM convolution kernels (conv.hip, conv_hx.hip):
+// Shared pieces of the implicit-GEMM convolution kernels (conv.hip, conv_v2.hip, conv_ws.h):
 // epilogue kinds, the launch-argument block, the fused epilogues and the
 // staging helpers (buffer / global LDS-DMA, counted vmcnt waits, XCD remap).
 #pragma once
@@ -21,6 +21,8 @@ enum Epi : int {
   EPI_ACC_F32 = 7,   // out(fp32) += v                        (gradient accumulation)
   EPI_GRU_QBWD = 8,  // co < hd: drh = v -> out2(bf16)[co] = drh*h*r*(1-r) (dr_pre), out[co] += drh*r
                      // co >= hd: out(fp32)[co] += v          (h = aux1, r = aux2)
+  // encoder normalisation folded into the conv (eval-mode BatchNorm):
+  EPI_NORM = 9,  // v = acc * chs[co] + bias[co]; hd != 0: ReLU; aux1: v = relu(v + aux1) -> out (bf16)
 };
 
 struct Seg {
@@ -67,6 +69,13 @@ struct Args {
   const bf16_t* wf;
   int ws_ncs, ws_ncb, ws_nstrips, ws_nrch, ws_rpc, ws_rsp, ws_kg;
   unsigned long long* ws_stamps;  // RS_WS_STAMPS builds only: per-wave s_memtime stamps
+  // EPI_NORM per-channel scale; normalisation statistics of the stored output
+  // (bf16-rounded acc + bias): stats[(g * Cout + co) * 2 + {0, 1}] += {sum, sum of
+  // squares} with g = image (stats_ps) or 0 (vector atomics; the buffer is
+  // zeroed by whoever consumes it, ops/norm.py)
+  const float* chs;
+  float* stats;
+  int stats_ps;
 };
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
@@ -251,6 +260,26 @@ __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, i
           if (cb + j < a.Cout) o[j] += v[j];
       }
     }
+  } else if constexpr (E == EPI_NORM) {
+    if (a.hd) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
+    const bf16_t* r = a.aux1 ? a.aux1 + (size_t)p * a.a1str + a.a1off + cb : nullptr;
+    if (vec && full) {
+      if (r) {
+        float rv[4];
+        ld4(r, rv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j] + rv[j], 0.f);
+      }
+      st4(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = f2bf(r ? fmaxf(v[j] + bf2f(r[j]), 0.f) : v[j]);
+    }
   } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE -> bf16
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -287,7 +316,14 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
       const int cb = m0 + mt * 16 + cq;
       if (cb >= a.Cout) continue;
       float v[4];
-      if (bvec && cb + 3 < a.Cout) {
+      if constexpr (E == EPI_NORM) {  // host-checked: chs / bias hold round_up(Cout, 4), 16-B aligned
+        const float4 sv = *reinterpret_cast<const float4*>(a.chs + cb);
+        const float4 bv = *reinterpret_cast<const float4*>(a.bias + cb);
+        v[0] = acc[mt][nt][0] * sv.x + bv.x;
+        v[1] = acc[mt][nt][1] * sv.y + bv.y;
+        v[2] = acc[mt][nt][2] * sv.z + bv.z;
+        v[3] = acc[mt][nt][3] * sv.w + bv.w;
+      } else if (bvec && cb + 3 < a.Cout) {
         const float4 bv = *reinterpret_cast<const float4*>(a.bias + cb);
         v[0] = acc[mt][nt][0] + bv.x;
         v[1] = acc[mt][nt][1] + bv.y;
@@ -302,10 +338,84 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
   }
 }
 
+// Normalisation statistics of this wave's output tile (Args::stats).  The 16
+// lanes sharing lane >> 4 hold the same 4*WM channels at 16 pixels each: per
+// lane sums over the n-tiles, a reduce-scatter over those 16 lanes, then one
+// atomic per (channel, statistic) per wave.  A tile whose pixels span two
+// images (per-sample statistics only) takes per-element atomics instead.
+template <int WM, int WN>
+__device__ __forceinline__ void stats_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                          const int (&pb)[WN]) {
+  const int b0 = __builtin_amdgcn_readfirstlane(pb[0]);  // lane 0 / n-tile 0 holds the wave's first pixel
+  if (b0 < 0) return;
+  bool same = true;
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) same = same && (pb[nt] < 0 || pb[nt] == b0);
+  const int cq = (lane >> 4) * 4;
+  float bs[WM][4];
+#pragma unroll
+  for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = m0 + mt * 16 + cq + j;
+      bs[mt][j] = a.bias && c < a.Cout ? a.bias[c] : 0.f;
+    }
+  if (!a.stats_ps || __all(same)) {
+    constexpr int NV = (WM * 8 + 15) / 16 * 16;
+    float v[NV];
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt) {
+          const float x = pb[nt] >= 0 ? bf2f(f2bf(acc[mt][nt][j] + bs[mt][j])) : 0.f;
+          s1 += x;
+          s2 += x * x;
+        }
+        v[mt * 4 + j] = s1;
+        v[WM * 4 + mt * 4 + j] = s2;
+      }
+#pragma unroll
+    for (int i = WM * 8; i < NV; ++i) v[i] = 0.f;
+    lane_reduce_scatter<NV, 16>(v, lane);
+    constexpr int K = NV / 16;
+    float* st = a.stats + (size_t)(a.stats_ps ? b0 : 0) * a.Cout * 2;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int e = K * (lane & 15) + k;
+      if (e < WM * 8) {
+        const int stat = e / (WM * 4), slot = e % (WM * 4);
+        const int c = m0 + (slot / 4) * 16 + cq + (slot % 4);
+        if (c < a.Cout) atomicAdd(st + c * 2 + stat, v[k]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int nt = 0; nt < WN; ++nt) {
+      if (pb[nt] < 0) continue;
+      float* st = a.stats + (size_t)pb[nt] * a.Cout * 2;
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = m0 + mt * 16 + cq + j;
+          if (c < a.Cout) {
+            const float x = bf2f(f2bf(acc[mt][nt][j] + bs[mt][j]));
+            atomicAdd(st + c * 2, x);
+            atomicAdd(st + c * 2 + 1, x * x);
+          }
+        }
+    }
+  }
+}
+
 template <int WM, int WN>
 __device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
                                              const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
                                              const int (&px)[WN]) {
+  if (a.stats) stats_pix<WM, WN>(a, acc, m0, lane, pb);
   switch (a.epi) {
 #define RS_EPI(E) \
   case E: epi_loop<WM, WN, E>(a, acc, m0, lane, pp, pb, py, px); break
@@ -317,6 +427,7 @@ __device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)
     RS_EPI(EPI_GRU_QBWD);
     RS_EPI(EPI_RELU);
     RS_EPI(EPI_SCALE);
+    RS_EPI(EPI_NORM);
 #undef RS_EPI
     default: epi_loop<WM, WN, EPI_BIAS>(a, acc, m0, lane, pp, pb, py, px); break;
   }
@@ -456,8 +567,6 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base
 
 }  // namespace conv
 
-// conv_hx.hip: launch one of the pipelined halo tiles 34-39 (grid over Cout tiles x patches)
-void conv_hx_launch(const conv::Args& a, int tile, hipStream_t stream);
 // conv_v2.hip: tiles 42-45 (3x3 / 1x5 / 5x1 only); false if the kernel size is not instantiated
 bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream);
 // conv_ws.hip: weight-stationary kernel; false if (KH, KW, G, NB) is not instantiated

@@ -19,7 +19,7 @@ static bool ws_dispatch(const Args* a, int epi, int KH, int KW, int G, int NB, i
     case EK_RELUBWD: return ws_relubwd(a, KH, KW, G, NB, nblocks, stream);
     case EK_ACC: return ws_acc(a, KH, KW, G, NB, nblocks, stream);
     case EK_QBWD: return ws_qbwd(a, KH, KW, G, NB, nblocks, stream);
-    default: return epi == EPI_FLOW ? false : ws_plain(a, KH, KW, G, NB, nblocks, stream);
+    default: return (epi == EPI_FLOW || epi == EPI_NORM) ? false : ws_plain(a, KH, KW, G, NB, nblocks, stream);
   }
 }
 

@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "enc_epi.h"
 
 namespace rs {
 namespace ench {
@@ -40,6 +41,15 @@ struct HArgs {
   int B, H, W, Cout;
   int tiles_w, tiles_img, ntiles;
   int tpb;  // consecutive tiles per block
+  // optional epilogue extras (ops_conv.cpp conv3x3_halo):
+  //   chs / shift: y = [relu](acc * chs + shift) [then relu(y + res)] (eval-mode BatchNorm)
+  //   stats: += per-channel (sum, sum of squares) of the bf16 output, [G][Cout][2]
+  const float* chs;
+  const float* shift;
+  const bf16_t* res;
+  int rstr, relu;
+  float* stats;
+  int stats_ps;
 };
 
 template <int CIN, int COB>
@@ -215,20 +225,81 @@ __global__ __launch_bounds__(256) void enc_halo_kernel(HArgs a) {
       const int bi = tile / a.tiles_img, rr = tile - bi * a.tiles_img;
       const int th = rr / a.tiles_w;
       const int ox = (rr - th * a.tiles_w) * C::TW + (lane & 31);
+      if (a.chs) {  // eval-mode BatchNorm folded in: per-channel scale / shift (host-checked: padded, aligned)
+#pragma unroll
+        for (int mi = 0; mi < C::NMF; ++mi)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int c = co0 + mi * 32 + 8 * g + 4 * (lane >> 5);
+            const float4 sv = *reinterpret_cast<const float4*>(a.chs + c);
+            const float4 bv = *reinterpret_cast<const float4*>(a.shift + c);
+            const float scv[4] = {sv.x, sv.y, sv.z, sv.w}, shv[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+            for (int r = 0; r < C::RPW; ++r)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                float v = acc[r][mi][4 * g + j] * scv[j] + shv[j];
+                acc[r][mi][4 * g + j] = a.relu ? fmaxf(v, 0.f) : v;
+              }
+          }
+      }
+      if (a.stats) {
+        // per-channel (sum, sum of squares) over the wave's 32 x RPW pixels:
+        // sums over the rows in-lane, then a reduce-scatter over the 32 lanes
+        // of each half-wave; each lane then owns NV/32 totals (one atomic each)
+        constexpr int NS = C::NMF * 16, NV = 2 * NS;
+        float v[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = 0.f;
+#pragma unroll
+        for (int r = 0; r < C::RPW; ++r) {
+          const int oy = th * C::TH + wave * C::RPW + r;
+          if (oy < a.H && ox < a.W) {
+#pragma unroll
+            for (int mi = 0; mi < C::NMF; ++mi)
+#pragma unroll
+              for (int k = 0; k < 16; ++k) {
+                const float x = bf2f(f2bf(acc[r][mi][k]));
+                v[mi * 16 + k] += x;
+                v[NS + mi * 16 + k] += x * x;
+              }
+          }
+        }
+        lane_reduce_scatter<NV, 32>(v, lane);
+        float* st = a.stats + (size_t)(a.stats_ps ? bi : 0) * a.Cout * 2;
+#pragma unroll
+        for (int q = 0; q < NV / 32; ++q) {
+          const int e = (NV / 32) * (lane & 31) + q;
+          const int stat = e / NS, slot = e % NS;  // slot = mi*16 + 4g + j
+          const int c = co0 + (slot / 16) * 32 + 8 * ((slot % 16) / 4) + 4 * (lane >> 5) + (slot % 4);
+          if (c < a.Cout) atomicAdd(st + c * 2 + stat, v[q]);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < C::RPW; ++r) {
         const int oy = th * C::TH + wave * C::RPW + r;
         if (oy < a.H && ox < a.W) {
-          bf16_t* o = a.y + ((size_t)(bi * a.H + oy) * a.W + ox) * a.ystr + co0;
+          const size_t pix = (size_t)(bi * a.H + oy) * a.W + ox;
+          bf16_t* o = a.y + pix * a.ystr + co0;
+          const bf16_t* rp = a.res ? a.res + pix * a.rstr + co0 : nullptr;
 #pragma unroll
           for (int mi = 0; mi < C::NMF; ++mi)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const int cb = mi * 32 + 8 * g + 4 * (lane >> 5);
               if (co0 + cb < a.Cout) {
-                const f32x16_t& v = acc[r][mi];
-                const uint2 pk = make_uint2(uint32_t(f2bf(v[4 * g])) | (uint32_t(f2bf(v[4 * g + 1])) << 16),
-                                            uint32_t(f2bf(v[4 * g + 2])) | (uint32_t(f2bf(v[4 * g + 3])) << 16));
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = acc[r][mi][4 * g + j];
+                if (rp) {
+                  const uint2 u = *reinterpret_cast<const uint2*>(rp + cb);
+                  v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
+                  v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xffff0000u), 0.f);
+                  v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
+                  v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xffff0000u), 0.f);
+                }
+                const uint2 pk = make_uint2(uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                                            uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16));
                 *reinterpret_cast<uint2*>(o + cb) = pk;
               }
             }
@@ -247,9 +318,11 @@ bool enc_halo_supported(int cin, int cout) {
 }
 
 bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_t* y, int ystr, int B, int H, int W,
-                     int cin, int cout, int num_cus, hipStream_t stream) {
+                     int cin, int cout, int num_cus, const EncEpi& e, hipStream_t stream) {
   if (!enc_halo_supported(cin, cout)) return false;
   ench::HArgs a{};
+  a.chs = e.chs; a.shift = e.shift; a.res = e.res; a.rstr = e.rstr; a.relu = e.relu;
+  a.stats = e.stats; a.stats_ps = e.stats_ps;
   a.x = x; a.w = w; a.y = y;
   a.xstr = xstr; a.ystr = ystr; a.Ktot = Ktot;
   a.B = B; a.H = H; a.W = W; a.Cout = cout;

@@ -36,6 +36,8 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                             bool dout_bf16, hipStream_t stream, int dstride);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
                           float scale, hipStream_t stream, void* out_bf16 = nullptr);
+void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
+                         const long long* lo, const long long* hi, const float* s, int nr, hipStream_t stream);
 bool corr_otf_supported_channels(int C);
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
@@ -483,7 +485,36 @@ bool is_deterministic() { return rs::deterministic(); }
 
 }  // namespace
 
+// Packed-weight gather (csrc/wpack.hip): out[i] = scale * source[code[i]] with
+// code = (source row << 24) | logical index (-1: zero); tab int64 [nsrc][10]
+// = (data_ptr, is_bf16, size[4], stride[4]) of the sources (host-built, on
+// the device); ranges: up to 4 [lo, hi) output ranges multiplied by rs[k].
+void wpack_gather(const Tensor& code, const Tensor& tab, const Tensor& out, at::IntArrayRef rlo,
+                  at::IntArrayRef rhi, at::ArrayRef<double> rs_) {
+  check_gpu(code, "code");
+  check_gpu(tab, "tab");
+  check_gpu(out, "out");
+  TORCH_CHECK(code.scalar_type() == at::kInt && code.dim() == 1, "wpack_gather: code must be int32 [n]");
+  TORCH_CHECK(tab.scalar_type() == at::kLong && tab.dim() == 2 && tab.size(1) == 10 && tab.size(0) <= 128,
+              "wpack_gather: tab must be int64 [<=128][10]");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "wpack_gather: out bf16/fp32");
+  TORCH_CHECK(out.numel() == code.numel(), "wpack_gather: out / code size");
+  TORCH_CHECK(rlo.size() == rhi.size() && rlo.size() == rs_.size() && rlo.size() <= 4, "wpack_gather: ranges");
+  long long lo[4], hi[4];
+  float sc[4];
+  for (size_t r = 0; r < rlo.size(); ++r) {
+    lo[r] = rlo[r];
+    hi[r] = rhi[r];
+    sc[r] = (float)rs_[r];
+  }
+  const c10::DeviceGuard guard(out.device());
+  rs::wpack_gather_launch(code.data_ptr<int>(), code.numel(), reinterpret_cast<const long long*>(tab.data_ptr<int64_t>()), out.data_ptr(),
+                          out.scalar_type() == at::kBFloat16, lo, hi, sc, (int)rlo.size(), cur_stream());
+  RS_CHECK_LAUNCH();
+}
+
 TORCH_LIBRARY(raft_stir, m) {
+  m.def("wpack_gather(Tensor code, Tensor tab, Tensor(a!) out, int[] rlo, int[] rhi, float[] rs) -> ()");
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);
   m.def("is_deterministic() -> bool", &is_deterministic);
   m.def("corr_volume(Tensor f1, Tensor f2, int levels, float scale, bool out_bf16=False) -> Tensor[]");
@@ -504,6 +535,7 @@ TORCH_LIBRARY(raft_stir, m) {
 }
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
+  m.impl("wpack_gather", &wpack_gather);
   m.impl("corr_volume", &corr_volume);
   m.impl("corr_lookup", &corr_lookup);
   m.impl("corr_lookup_into", &corr_lookup_into);

@@ -3,6 +3,7 @@
 // here on the host; the kernel assumes them.
 #include <ATen/ATen.h>
 #include "host_common.h"
+#include "enc_epi.h"
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
@@ -34,6 +35,10 @@ struct ConvLaunch {
   const void* wf;
   int ws_G, ws_NB, ws_ncs, ws_ncb, ws_rpc, ws_nstrips, ws_nrch, ws_rsp, ws_blocks;
   void* ws_stamps;
+  // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
+  const float* chs;
+  float* stats;
+  int stats_ps;
 };
 constexpr int kWsTile = 48;
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
@@ -73,14 +78,15 @@ void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df
                        float* db, float* part, hipStream_t stream);
 bool deterministic();
 bool enc_halo_launch(const uint16_t* x, int xstr, const uint16_t* w, int Ktot, uint16_t* y, int ystr, int B, int H,
-                     int W, int cin, int cout, int num_cus, hipStream_t stream);
+                     int W, int cin, int cout, int num_cus, const EncEpi& e, hipStream_t stream);
 bool enc_halo_supported(int cin, int cout);
 }  // namespace rs
 
 namespace {
 using at::Tensor;
 
-constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8;
+constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8,
+              EPI_NORM = 9;
 
 hipStream_t stream() { return rs::current_stream(); }
 
@@ -88,6 +94,43 @@ void check_nhwc(const Tensor& t, int B, int H, int W, const char* n, at::ScalarT
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, n, ": contiguous NHWC GPU tensor required");
   TORCH_CHECK(t.size(0) == B && t.size(1) == H && t.size(2) == W, n, ": spatial shape mismatch");
   TORCH_CHECK(t.scalar_type() == dt, n, ": ", dt, " required");
+}
+
+// Encoder-normalisation extras shared by conv_fused / conv_geo / conv3x3_halo:
+//   stats (fp32 [G][Cout][2], G = B if per_sample else 1): the kernel ADDS the
+//     per-channel sum and sum of squares of its bf16 output (the buffer is
+//     zeroed by its consumer, norm_finalize);
+//   nscale (fp32, >= round_up(Cout, 4), 16-B aligned; epi EPI_NORM only) with
+//     the bias as the shift: out = [relu](acc * nscale + bias) [then relu(. + aux1)].
+struct NormX {
+  float* stats = nullptr;
+  int stats_ps = 0;
+  const float* chs = nullptr;
+};
+void check_vec4(const c10::optional<Tensor>& t, int Cout, const char* op, const char* n) {
+  TORCH_CHECK(t && t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat &&
+                  t->numel() >= (Cout + 3) / 4 * 4 && (uintptr_t)t->data_ptr() % 16 == 0,
+              op, ": ", n, " must be 16-B aligned fp32 with round_up(Cout, 4) values");
+}
+NormX norm_extras(const c10::optional<Tensor>& stats, bool per_sample, const c10::optional<Tensor>& nscale,
+                  const c10::optional<Tensor>& bias, int epi, int B, int Cout, const char* op) {
+  NormX x;
+  if (stats) {
+    const int64_t G = per_sample ? B : 1;
+    TORCH_CHECK(stats->is_cuda() && stats->is_contiguous() && stats->scalar_type() == at::kFloat &&
+                    stats->numel() == G * Cout * 2,
+                op, ": stats must be contiguous fp32 [", G, "][", Cout, "][2]");
+    TORCH_CHECK(epi == 0, op, ": statistics are taken with the plain (bias) epilogue only");
+    x.stats = stats->data_ptr<float>();
+    x.stats_ps = per_sample ? 1 : 0;
+  }
+  TORCH_CHECK(bool(nscale) == (epi == EPI_NORM), op, ": nscale is the EPI_NORM scale (and only that)");
+  if (nscale) {
+    check_vec4(nscale, Cout, op, "nscale");
+    check_vec4(bias, Cout, op, "bias (the EPI_NORM shift)");
+    x.chs = nscale->data_ptr<float>();
+  }
+  return x;
 }
 
 // Weight-stationary kernel geometry (csrc/conv_ws.hip), checked against what
@@ -133,7 +176,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
                const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
                int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
-               const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile, at::IntArrayRef ws_cfg) {
+               const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile, at::IntArrayRef ws_cfg,
+               const NormX& nx = NormX()) {
   const bool ws = tile == rs::kWsTile;
   TORCH_CHECK(!segs.empty() && segs.size() <= 3, "conv_fused: 1..3 input segments");
   TORCH_CHECK(seg_off.size() == segs.size() && seg_C.size() == segs.size(), "conv_fused: segment spec");
@@ -167,12 +211,6 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   if (tile >= 42 && tile <= 47)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
-  if (tile >= 34 && tile <= 41) {  // pipelined halo tiles: ring depth <= taps, halo within the LDS slot, 16-wide patches
-    const int S = (tile == 35 || tile == 38) ? 3 : 4;
-    const int TH = (tile == 36 || tile == 37) ? 4 : 8, HCAP = (tile == 36 || tile == 37) ? 128 : 192;
-    TORCH_CHECK(KH * KW >= S, "conv_fused: halo tile ", tile, " needs at least ", S, " taps");
-    TORCH_CHECK((TH + KH - 1) * (16 + KW - 1) <= HCAP, "conv_fused: kernel too large for halo tile ", tile);
-  }
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-33) support at most 32 taps");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
   if (tile >= 24 && tile <= 26) {  // halo tiles: the (TH+KH-1) x (16+KW-1) halo must fit the LDS buffer
@@ -183,9 +221,6 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                      tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
   const int tileM = (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
-                    : (tile == 35 || tile == 37) ? 128
-                    : (tile == 34 || tile == 36 || tile == 38 || tile == 40 || tile == 41) ? 64
-                    : tile == 39 ? 32
                     : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
@@ -251,6 +286,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   } else if (epi == EPI_RELU_BWD) {
     TORCH_CHECK(aux1, "conv_fused(relu_bwd): needs aux1 (the ReLU output)");
     opt_nhwc(aux1, a1off, Cout, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
+  } else if (epi == EPI_NORM) {
+    if (aux1) { opt_nhwc(aux1, a1off, Cout, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p; }
   } else if (epi == EPI_GRU_QBWD) {
     TORCH_CHECK(hd % 4 == 0 && hd <= Cout && out2 && aux1 && aux2,
                 "conv_fused(gru_qbwd): needs out2 (dr_pre), aux1 (h), aux2 (r)");
@@ -258,6 +295,10 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
+  if (nx.stats || nx.chs)
+    TORCH_CHECK(!ws && !(tile >= 42 && tile <= 47),
+                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-48)");
+  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
   if (ws) {
     ws_setup(L, w, ws_cfg, Ktot);
     // the weight-stationary epilogues use vector accesses only (conv_ws.h ws_pre / ws_fin)
@@ -281,10 +322,12 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
                 int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
                 const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
                 int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
-                const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile) {
+                const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile,
+                const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale) {
   TORCH_CHECK(tile != rs::kWsTile, "conv_fused: the weight-stationary kernel is conv_ws");
+  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, segs.at(0).size(0), Cout, "conv_fused");
   conv_impl(segs, seg_off, seg_C, w, bias, KH, KW, Cout, epi, scale, hd, out, ooff, out2, o2off, out3, o3off,
-            aux1, a1off, aux2, a2off, tile, {});
+            aux1, a1off, aux2, a2off, tile, {}, nx);
 }
 
 // torch.ops.raft_stir.conv_ws: the same convolution + epilogue contract as
@@ -311,7 +354,8 @@ void conv_ws(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntAr
 void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C, const Tensor& w,
               const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t PH, int64_t PW, int64_t SY,
               int64_t SX, int64_t Ho, int64_t Wo, int64_t Cout, const Tensor& out, int64_t ooff, int64_t OSY,
-              int64_t OSX, int64_t OOY, int64_t OOX, int64_t tile) {
+              int64_t OSX, int64_t OOY, int64_t OOX, int64_t tile, const c10::optional<Tensor>& stats,
+              bool stats_per_sample, const c10::optional<Tensor>& nscale, bool relu) {
   TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size(),
               "conv_geo: 1..3 input segments");
   TORCH_CHECK(tile == 2 || tile == 3 || tile == 4 || tile == 6 || tile == 7 || tile == 8,
@@ -359,7 +403,11 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.B = B; L.H = Ho; L.W = Wo; L.KH = KH; L.KW = KW; L.PH = PH; L.PW = PW;
   L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;
-  L.epi = 0; L.scale = 1.f; L.hd = 0;
+  const int epi = nscale ? EPI_NORM : 0;
+  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, B, Cout, "conv_geo");
+  TORCH_CHECK(!relu || nscale, "conv_geo: relu goes with the EPI_NORM epilogue");
+  L.epi = epi; L.scale = 1.f; L.hd = relu ? 1 : 0;
+  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
   L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = ooff;
   L.tile = tile;
   L.geo = 1;
@@ -629,7 +677,9 @@ int num_cus(int dev) {
 // Stride-1 3x3 'same' conv on the halo-tile kernel (csrc/enc_halo.hip):
 // x NHWC (cin of its x.size(3) channels), w packed [Cout_pad][9][Ktot], y NHWC
 // (cout of its y.size(3) channels), no bias.
-void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin, int64_t cout) {
+void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin, int64_t cout,
+                  const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale,
+                  const c10::optional<Tensor>& nshift, const c10::optional<Tensor>& res, bool relu) {
   TORCH_CHECK(x.dim() == 4, "conv3x3_halo: x must be NHWC");
   const int B = x.size(0), H = x.size(1), W = x.size(2);
   check_nhwc(x, B, H, W, "conv3x3_halo: x");
@@ -643,17 +693,33 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
   TORCH_CHECK(((uintptr_t)x.data_ptr() | (uintptr_t)w.data_ptr()) % 16 == 0 && (uintptr_t)y.data_ptr() % 8 == 0,
               "conv3x3_halo: alignment");
   TORCH_CHECK(x.numel() < (int64_t(1) << 31) && y.numel() < (int64_t(1) << 31), "conv3x3_halo: tensor too large");
+  rs::EncEpi e;
+  const NormX nx = norm_extras(stats, stats_per_sample, nscale, nshift, nscale ? EPI_NORM : 0, B, cout, "conv3x3_halo");
+  e.stats = nx.stats; e.stats_ps = nx.stats_ps; e.chs = nx.chs;
+  e.shift = nscale ? nshift->data_ptr<float>() : nullptr;
+  TORCH_CHECK(!relu || nscale, "conv3x3_halo: relu goes with nscale / nshift");
+  TORCH_CHECK(!res || nscale, "conv3x3_halo: the residual goes with nscale / nshift");
+  e.relu = relu ? 1 : 0;
+  if (res) {
+    check_nhwc(*res, B, H, W, "conv3x3_halo: res");
+    TORCH_CHECK(cout <= res->size(3) && res->size(3) % 4 == 0 && (uintptr_t)res->data_ptr() % 8 == 0,
+                "conv3x3_halo: res channels / alignment");
+    e.res = static_cast<const uint16_t*>(res->data_ptr());
+    e.rstr = res->size(3);
+  }
   const c10::DeviceGuard guard(x.device());
   rs::enc_halo_launch(static_cast<const uint16_t*>(x.data_ptr()), x.size(3), static_cast<const uint16_t*>(w.data_ptr()),
                       w.size(2), static_cast<uint16_t*>(y.data_ptr()), y.size(3), B, H, W, cin, cout,
-                      num_cus(x.get_device()), stream());
+                      num_cus(x.get_device()), e, stream());
   RS_CHECK_LAUNCH();
 }
 
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
-  m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout) -> ()");
+  m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout, Tensor(b!)? stats=None, "
+        "bool stats_per_sample=False, Tensor? nscale=None, Tensor? nshift=None, Tensor? res=None, "
+        "bool relu=False) -> ()");
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
         "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
   m.def("flow_head(Tensor x, int xoff, int cin, Tensor w, Tensor bias, Tensor(a!) crd, Tensor? src) -> ()");
@@ -666,13 +732,15 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("relu_take(Tensor(a!) G, int goff, int n, int nz, Tensor act, int aoff, Tensor(b!) out) -> ()");
   m.def("conv_fused(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, "
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
-        "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile) -> ()");
+        "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
+        "Tensor(d!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None) -> ()");
   m.def("conv_ws(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor wf, Tensor? bias, int KH, int KW, "
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int[] cfg) -> ()");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
         "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
-        "int OOX, int tile) -> ()");
+        "int OOX, int tile, Tensor(b!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None, "
+        "bool relu=False) -> ()");
   m.def("flow_encode(Tensor coords, Tensor w, Tensor bias, Tensor(a!) out, int ooff, Tensor(b!)? fout, "
         "int foff) -> ()");
 }

@@ -214,6 +214,9 @@ class FusedTrainEngine:
             f32_maps.append(b.reshape(-1))
         f1w = pidx[id(self.f1.weight)].permute(2, 3, 1, 0).contiguous()  # [7][7][2][f1c]
         f32_maps += [f1w.reshape(-1), pidx[id(self.f1.bias)].reshape(-1)]
+        # the 2-channel flow output conv in csrc/flowhead.hip's fp32 [2][3][3][Cin] layout
+        fcw = self.model.update_block.flow_head.conv2.weight
+        f32_maps.append(pidx[id(fcw)].permute(0, 2, 3, 1).reshape(-1))
         nbf = sum(m.numel() for m in bf_maps)
         gather = torch.cat(bf_maps + f32_maps)
         # scale (mask x 0.25) folded into the dgrad weights: element range in the bf16 region
@@ -246,22 +249,58 @@ class FusedTrainEngine:
                 o += gw.numel() + gb.numel()
         f1g = gids[gf1[0]:gf1[1]].view(7, 7, 2, fc).permute(3, 2, 0, 1).contiguous()
         gmaps += [f1g.reshape(-1), gids[gf1[1]:gf1[1] + fc]]
+        # the same gather as per-element codes (source param << 24 | index) for
+        # csrc/wpack.hip: one launch per dtype region reading the parameters in place
+        starts = torch.tensor([0] + sizes[:-1]).cumsum(0)
+        row = torch.searchsorted(starts, gather, right=True) - 1
+        code = torch.where(gather == fill, torch.full_like(gather, -1),
+                           ((row.clamp_min(0) << 24) | (gather - starts[row.clamp_min(0)])))
+        assert len(self.params) <= 127 and max(sizes) < (1 << 24)
+        code = code.to(torch.int32).to(dev)
         self._maps = dict(dev=dev, gather=gather.to(dev), nbf=nbf, layout=layout, scaled=scaled,
+                          code_bf=code[:nbf], code_f32=code[nbf:], tab=None, tab_key=None,
+                          out_bf=torch.empty(nbf, dtype=torch.bfloat16, device=dev),
+                          out_f32=torch.empty(gather.numel() - nbf, dtype=torch.float32, device=dev),
                           glayout=glayout, gf1=gf1, gtotal=gtotal, ggather=torch.cat(gmaps).to(dev),
                           gscaled=gscaled, zero=torch.zeros(1, device=dev))
 
+    def _src_table(self):
+        M = self._maps
+        key = tuple((p.data_ptr(), p.dtype, p.stride()) for p in self.params)
+        if key != M["tab_key"]:
+            rows = []
+            for p in self.params:
+                pad = 4 - p.dim()
+                rows.append([p.data_ptr(), int(p.dtype == torch.bfloat16)] + [1] * pad + list(p.shape)
+                            + [0] * pad + list(p.stride()))
+            M["tab"] = torch.tensor(rows, dtype=torch.int64).to(M["dev"])
+            M["tab_key"] = key
+        return M["tab"]
+
     @torch.no_grad()
     def pack(self, dev):
-        """Per-step weight packing (see _build_maps): cat + gather + bf16 cast."""
+        """Per-step weight packing (see _build_maps): two gather launches
+        (csrc/wpack.hip: bf16 weights, fp32 biases / flow-encoder / flow-head
+        weights) into persistent buffers, reading the parameters in place."""
         if self._maps is None or self._maps["dev"] != dev:
             self._build_maps(dev)
         M = self._maps
-        src = torch.cat([p.detach().reshape(-1).float() for p in self.params] + [M["zero"]])
-        vals = src.index_select(0, M["gather"])
-        for a, b, s in M["scaled"]:
-            vals[a:b].mul_(s)
         nbf = M["nbf"]
-        bf = vals[:nbf].to(torch.bfloat16)
+        if all(p.dtype in (torch.float32, torch.bfloat16) and p.dim() <= 4 for p in self.params):
+            tab = self._src_table()
+            sc = M["scaled"]
+            R.wpack_gather(M["code_bf"], tab, M["out_bf"], [a for a, _, _ in sc], [b for _, b, _ in sc],
+                           [float(x) for _, _, x in sc])
+            R.wpack_gather(M["code_f32"], tab, M["out_f32"], [], [], [])
+            bf = M["out_bf"]
+            vals = _Offset(M["out_f32"], nbf)
+        else:  # reference path: cat + gather + cast
+            src = torch.cat([p.detach().reshape(-1).float() for p in self.params] + [M["zero"]])
+            v = src.index_select(0, M["gather"])
+            for a, b, s in M["scaled"]:
+                v[a:b].mul_(s)
+            bf = v[:nbf].to(torch.bfloat16)
+            vals = _Offset(v[nbf:], nbf)
         ob, of = 0, nbf
         for pc, ws, wds, bs in M["layout"]:
             n = ws.numel()
@@ -272,12 +311,14 @@ class FusedTrainEngine:
             ob += n
             pc.b = vals[of:of + bs.numel()]
             of += bs.numel()
-        fc = self.model.update_block.flow_head.conv2  # 2-channel output conv: csrc/flowhead.hip
-        self.flow_w32 = fc.weight.detach().float().permute(0, 2, 3, 1).contiguous()  # [2][3][3][256]
         fc = self.f1c
         self.f1w = vals[of:of + 49 * 2 * fc].view(7, 7, 2, fc)
         of += 49 * 2 * fc
         self.f1b = vals[of:of + fc]
+        of += fc
+        # 2-channel output conv (csrc/flowhead.hip): fp32 [2][3][3][Cin]
+        fcw = self.model.update_block.flow_head.conv2.weight
+        self.flow_w32 = vals[of:of + fcw.numel()].view(fcw.shape[0], fcw.shape[2], fcw.shape[3], fcw.shape[1])
 
     def side_stream(self, dev, slot: int = 0, flow: bool = False):
         from .raft import OVERLAP
@@ -309,15 +350,13 @@ class FusedTrainEngine:
     @staticmethod
     def config_capable(cfg) -> bool:
         """The configuration half of ``eligible`` (no tensors needed)."""
-        return (bool(cfg.mixed_precision) and cfg.fused_gru
-                and not (cfg.small and cfg.alternate_corr)  # on-the-fly correlation: radius-4 kernels only
-                and getattr(cfg, "fused_train", True))
+        return bool(cfg.mixed_precision) and cfg.fused_gru and getattr(cfg, "fused_train", True)
 
     @staticmethod
     def eligible(model, image, corr_fn) -> bool:
         corr_ok = getattr(corr_fn, "state", None) is not None or (  # all-pairs pyramid, or on-the-fly
-            getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == 4 and not model.cfg.small
-            and corr_fn.f1.dtype == torch.bfloat16)
+            getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == (3 if model.cfg.small else 4)
+            and len(corr_fn.f2s) == 4 and corr_fn.f1.dtype == torch.bfloat16)
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
                 and FusedTrainEngine.config_capable(model.cfg)
                 and getattr(corr_fn, "hip", False) and corr_ok
@@ -393,6 +432,18 @@ class DeferGrads(torch.autograd.Function):
         return (None, *grads)
 
 
+class _Offset:
+    """fp32 values addressed in the packed gather's coordinates (the bf16
+    region [0, nbf) precedes them): vals[a:b] -> t[a - nbf : b - nbf]."""
+    __slots__ = ("t", "o")
+
+    def __init__(self, t, o):
+        self.t, self.o = t, o
+
+    def __getitem__(self, s):
+        return self.t[s.start - self.o:s.stop - self.o]
+
+
 class FusedTrainLoop(torch.autograd.Function):
     """``otf``: None (all-pairs pyramid in corr_state) or (radius, scale, n_levels):
     the first n_levels + 1 of ``tensors`` are the on-the-fly correlation's f1 and
@@ -401,10 +452,10 @@ class FusedTrainLoop(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, eng, corr_state, token, net, inp, coords0, coords1, iters, defer, otf, *tensors):
-        if eng.small:
-            return _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer)
         nt = 0 if otf is None else otf[2] + 1
         otf_t, params = tensors[:nt], tensors[nt:]
+        if eng.small:
+            return _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer, otf, otf_t)
         B, _, H, W = coords1.shape
         dev = coords1.device
         eng.pack(dev)
@@ -649,7 +700,10 @@ def _interp_matrix(n_in: int, n_out: int, dev) -> torch.Tensor:
     return m
 
 
-def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer):
+def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defer, otf=None, otf_t=()):
+    """``otf``: None (all-pairs pyramid) or (radius 3, scale, 4 levels) with
+    ``otf_t`` = (f1, pooled f2 levels): the on-the-fly correlation (reference
+    AlternateCorrBlock with RAFT-small's radius, core/raft.py:29-33)."""
     B, _, H, W = coords1.shape
     dev = coords1.device
     hd = SHD
@@ -662,6 +716,8 @@ def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defe
     C = S["C"]
     sl(C, 0).copy_(coords1.detach())
     c0 = coords0.detach().float().contiguous()
+    if otf is not None:
+        S["corr"][..., otf[2] * 49:].zero_()  # K padding of the correlation slot (lookup_into zeroes its own)
     main, side = torch.cuda.current_stream(dev), eng.side_stream(dev, flow=True)
     zr, q = eng.zr[0], eng.q[0]
     for i in range(iters):
@@ -673,7 +729,11 @@ def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defe
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             R.flow_encode(coords, eng.f1w, eng.f1b, sl(S["f1"], i), 0, hx, 240)
             conv_fused([(sl(S["f1"], i), 0, 64)], eng.f2.w, eng.f2.b, 3, 3, 32, EPI_RELU, mot, 96)
-        R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+        if otf is None:
+            R.corr_lookup_into(corr_state.pyr, coords, corr_state.radius, sl(S["corr"], i))
+        else:
+            cf = R.corr_otf(otf_t[0], list(otf_t[1:]), coords, otf[0], otf[1], True)
+            sl(S["corr"], i)[..., :cf.shape[-1]].copy_(cf)
         conv_fused([(sl(S["corr"], i), 0, SCORR_PAD)], eng.c1.w, eng.c1.b, 1, 1, hd, EPI_RELU, mot, 0)
         if side is not None:
             main.wait_stream(side)
@@ -689,7 +749,9 @@ def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defe
     n = iters * B
     flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
     up = 8 * torch.nn.functional.interpolate(flows, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)
-    ctx.eng, ctx.state, ctx.S, ctx.iters, ctx.otf = eng, corr_state, S, iters, None
+    ctx.eng, ctx.state, ctx.S, ctx.iters, ctx.otf = eng, corr_state, S, iters, otf
+    if otf is not None:
+        ctx.save_for_backward(*otf_t)
     ctx.defer = bool(defer) and eng.side_stream(dev) is not None
     ctx.c0 = c0
     ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
@@ -706,8 +768,13 @@ def _small_backward(ctx, g_up):
     main = torch.cuda.current_stream(dev)
     side = eng.side_stream(dev, 1 if ctx.defer else 0, flow=not ctx.defer)
     lside = eng.side_stream(dev, 0) if ctx.defer else None
-    if st.gpyr is None:
-        st.gpyr = st.zero_grads()
+    otf = ctx.otf
+    if otf is None:
+        if st.gpyr is None:
+            st.gpyr = st.zero_grads()
+    else:
+        otf_t = ctx.saved_tensors
+        d_otf = None  # fp32 sums over the iterations: [df1, df2_0 .. df2_3]
     G = S["G"]  # fp32 [dh 96 | d inp 64 | d motion 80 | d flow 2 | 0]
     G.zero_()
     C = S["C"]
@@ -743,13 +810,30 @@ def _small_backward(ctx, g_up):
         if lside is not None:
             lside.wait_stream(main)
         with torch.cuda.stream(lside) if lside is not None else contextlib.nullcontext():
-            R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+            if otf is None:
+                R.corr_lookup_backward(st.gpyr, sl(C, i), st.radius, dcorr)
+            else:
+                gi = R.corr_otf_backward(otf_t[0], list(otf_t[1:]), sl(C, i), otf[0], otf[1],
+                                         dcorr[..., :otf[2] * 49].contiguous())
+                if d_otf is None:
+                    d_otf = list(gi)
+                else:
+                    for acc, g in zip(d_otf, gi):
+                        acc.add_(g)
     if lside is not None:
         main.wait_stream(lside)
+        if otf is not None:
+            for g in d_otf:
+                g.record_stream(main)
     d_net = G[..., :hd].permute(0, 3, 1, 2).to(ctx.net_dtype)
     d_inp = G[..., hd:hd + 64].permute(0, 3, 1, 2).to(ctx.inp_dtype)
     grads = FusedTrainLoop._param_grads(ctx, _small_wgrads, S, C, B, H, W, n, main, side)
-    return (None, None, torch.zeros((), device=dev), d_net, d_inp, None, None, None, None, None, *grads)
+    if otf is None:
+        token_grad, otf_grads = torch.zeros((), device=dev), ()
+    else:
+        token_grad = None
+        otf_grads = tuple(g.to(t.dtype) for g, t in zip(d_otf, otf_t))
+    return (None, None, token_grad, d_net, d_inp, None, None, None, None, None, *otf_grads, *grads)
 
 
 def _small_wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):

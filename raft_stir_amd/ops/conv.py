@@ -16,7 +16,7 @@ from typing import List, Sequence, Tuple
 import torch
 
 (EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_GRU_ZR, EPI_GRU_Q, EPI_FLOW,
- EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD) = range(9)
+ EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_NORM) = range(10)
 
 Piece = Tuple[int, int, int]          # (weight in-channel start, length, segment channel offset)
 SegSpec = Tuple[int, Sequence[Piece]]  # (segment channels read (multiple of 32), pieces)
@@ -126,7 +126,7 @@ WS_INST = {
 
 def ws_class(epi: int):
     return {EPI_GRU_ZR: "zr", EPI_GRU_Q: "q", EPI_RELU_BWD: "relubwd", EPI_ACC_F32: "acc",
-            EPI_GRU_QBWD: "qbwd", EPI_FLOW: None}.get(epi, "plain")
+            EPI_GRU_QBWD: "qbwd", EPI_FLOW: None, EPI_NORM: None}.get(epi, "plain")
 
 
 WS_G = {k: v for d in WS_INST.values() for k, v in d.items()}  # union (tests)
@@ -202,11 +202,16 @@ def tuned_ws() -> dict:
 
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=None, wf=None, ws_cfg=None):
+               aux2=None, a2off=0, tile=None, wf=None, ws_cfg=None, stats=None, stats_per_sample=False,
+               nscale=None):
     """segs: list of (NHWC bf16 buffer, channel offset, channels read).
     ``wf``: the same weights in frag_layout -- the weight-stationary kernel runs
     when it has an instantiated configuration for the shape (unless ``tile``
-    forces a tile kernel or RS_CONV_WS=0)."""
+    forces a tile kernel or RS_CONV_WS=0).
+    ``stats`` (fp32 [G][cout][2]): the epilogue adds each channel's (sum, sum of
+    squares) of the output (ops/norm.py); ``nscale`` with ``epi=EPI_NORM``:
+    out = [relu if hd](acc * nscale + bias) [then relu(. + aux1)].  Both run on
+    the tile kernels only."""
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
@@ -214,7 +219,7 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
                             a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, wf=wf, ws_cfg=ws_cfg))
-    if wf is not None and (tile == WS_TILE or (tile is None and _WS)):
+    if wf is not None and stats is None and nscale is None and (tile == WS_TILE or (tile is None and _WS)):
         t0 = tensors[0]
         cfg = ws_cfg if ws_cfg is not None else ws_config(t0.shape[0], t0.shape[1], t0.shape[2], cout, sum(chans),
                                                           kh, kw, wf.shape[0], epi)
@@ -233,5 +238,10 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
         tile = tuned_tiles().get(tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi))
         if tile is None:
             tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans, kh * kw)
-    torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
-                                   out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)
+    if stats is None and nscale is None:
+        torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
+                                       out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)
+    else:
+        torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
+                                       out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile,
+                                       stats, bool(stats_per_sample), nscale)

@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_BIAS, conv_fused, pack_weight, pad_to
+from .conv import EPI_BIAS, EPI_NORM, conv_fused, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -61,11 +61,18 @@ def _halo_ok(cin: int, cout: int) -> bool:
     return cin in (96, 128) and cout % 32 == 0
 
 
-def _conv3x3_into(xn, wp, cin, cout, out, P):
+def _conv3x3_into(xn, wp, cin, cout, out, P, stats=None):
+    """``stats`` = (fp32 [G][cout][2] buffer, per_sample) or None: the conv
+    epilogue adds the output's per-channel sums (ops/norm.py)."""
+    st, ps = stats if stats is not None else (None, False)
     if _halo_ok(cin, cout):
-        torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout)
+        if st is None:
+            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout)
+        else:
+            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout, st, ps)
     else:
-        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout))
+        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout),
+                   stats=st, stats_per_sample=ps)
 
 
 def _wgrad_covers(cin: int, cout: int) -> bool:
@@ -171,7 +178,7 @@ def _wgrad_on(stream, fn, inputs):
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, hold, wstream):
+    def forward(ctx, x, weight, hold, wstream, stats):
         weight = hold.p
         ctx.param, ctx.wstream = weight, wstream
         xn = _nhwc(x)
@@ -180,7 +187,7 @@ class _Conv3x3(torch.autograd.Function):
         P = N * H * W
         wp = _packed(weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
-        _conv3x3_into(xn, wp, cin, cout, out, P)
+        _conv3x3_into(xn, wp, cin, cout, out, P, stats)
         ctx.save_for_backward(x)
         return out.permute(0, 3, 1, 2)
 
@@ -201,7 +208,7 @@ class _Conv3x3(torch.autograd.Function):
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
@@ -224,10 +231,42 @@ def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
         [0, 0], 1, [False, True, False])[1].to(weight.dtype)
 
 
-def conv3x3(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """conv(x) without its bias (see :func:`eligible`)."""
+def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
+    """conv(x) without its bias (see :func:`eligible`); ``stats``: see
+    :func:`_conv3x3_into`."""
     w, st = _weight_in(conv.weight)
-    return _Conv3x3.apply(x, w, _Hold(conv.weight), st)
+    return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats)
+
+
+def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residual=None) -> torch.Tensor:
+    """Inference (no autograd): ``[relu](conv_nobias(x) * scale + shift)``, then
+    ``relu(. + residual)`` -- an eval-mode BatchNorm (scale / shift per output
+    channel, the conv bias folded into shift: ops/norm.py) and the block's
+    activations in the conv epilogue.  Stride-1 3x3 convs (:func:`eligible`) and
+    strided / 1x1 ones (:func:`eligible_geo`, no residual)."""
+    xn = _nhwc(x)
+    N, H, W, cin = xn.shape
+    cout = conv.out_channels
+    rn = _nhwc(residual) if residual is not None else None
+    if conv.stride == (1, 1) and conv.kernel_size == (3, 3):
+        wp = _packed(conv.weight, False)
+        out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
+        if _halo_ok(cin, cout):
+            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout, None, False, scale, shift, rn, bool(relu))
+        else:
+            conv_fused([(xn, 0, cin)], wp, shift, 3, 3, cout, EPI_NORM, out, 0, hd=int(bool(relu)), aux1=rn,
+                       tile=choose_enc_tile(N * H * W, cin, cout), nscale=scale)
+        return out.permute(0, 3, 1, 2)
+    assert residual is None, "conv_norm: the strided / 1x1 convs have no residual input"
+    kh, kw = conv.kernel_size
+    pad, stride = conv.padding, conv.stride
+    Ho = (H + 2 * pad[0] - kh) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - kw) // stride[1] + 1
+    out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.bfloat16)
+    torch.ops.raft_stir.conv_geo([xn], [0], [cin], _fwd_weight(conv.weight), shift, kh, kw, pad[0], pad[1],
+                                 stride[0], stride[1], Ho, Wo, cout, out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]),
+                                 None, False, scale, bool(relu))
+    return out.permute(0, 3, 1, 2)
 
 
 # ----------------------------------------------------------------- strided / 1x1
@@ -317,7 +356,7 @@ def _geo_tile(cout: int, chans) -> int:
     return 6 if k64 else 3
 
 
-def _conv_geo_fwd(x, weight, bias, stride, pad):
+def _conv_geo_fwd(x, weight, bias, stride, pad, stats=None):
     xn = _nhwc(x)
     N, Hi, Wi, cin = xn.shape
     cout, _, kh, kw = weight.shape
@@ -325,8 +364,12 @@ def _conv_geo_fwd(x, weight, bias, stride, pad):
     Wo = (Wi + 2 * pad[1] - kw) // stride[1] + 1
     out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.bfloat16)
     b = None if bias is None else bias.detach().float().contiguous()
-    torch.ops.raft_stir.conv_geo([xn], [0], [cin], _fwd_weight(weight), b, kh, kw, pad[0], pad[1], stride[0],
-                                 stride[1], Ho, Wo, cout, out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]))
+    args = ([xn], [0], [cin], _fwd_weight(weight), b, kh, kw, pad[0], pad[1], stride[0], stride[1], Ho, Wo, cout,
+            out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]))
+    if stats is None:
+        torch.ops.raft_stir.conv_geo(*args)
+    else:
+        torch.ops.raft_stir.conv_geo(*args, stats[0], stats[1])
     return out
 
 
@@ -384,9 +427,9 @@ def _conv_geo_wgrad(dy, x, weight, stride, want_bias):
 
 class _ConvGeo(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, hold, wstream):
+    def forward(ctx, x, weight, bias, stride, pad, hold, wstream, stats):
         weight = hold.p
-        out = _conv_geo_fwd(x, weight, bias, stride, pad)
+        out = _conv_geo_fwd(x, weight, bias, stride, pad, stats)
         ctx.save_for_backward(x)
         ctx.param, ctx.wstream = weight, wstream
         ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
@@ -403,17 +446,18 @@ class _ConvGeo(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             want_b = ctx.has_bias and ctx.needs_input_grad[2]
             dw, db = _wgrad_on(ctx.wstream, lambda: _conv_geo_wgrad(dyn, x, weight, ctx.stride, want_b), [dyn, x])
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
-def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
+def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None) -> torch.Tensor:
     """conv(x) on the HIP kernels (see :func:`eligible_geo`); ``bias=False``
-    drops the conv's bias (folded into a following normalisation)."""
+    drops the conv's bias (folded into a following normalisation); ``stats``:
+    see :func:`_conv3x3_into`."""
     b = conv.bias if bias else None
     w, st = _weight_in(conv.weight)
     if b is not None and st is not None:
         b = _DEFER["views"].get(id(conv.bias), b)
-    return _ConvGeo.apply(x, w, b, tuple(conv.stride), tuple(conv.padding), _Hold(conv.weight), st)
+    return _ConvGeo.apply(x, w, b, tuple(conv.stride), tuple(conv.padding), _Hold(conv.weight), st, stats)
 
 
 class _ConvPair(torch.autograd.Function):
@@ -422,10 +466,11 @@ class _ConvPair(torch.autograd.Function):
     gradient, with the shortcut's term fused into the 3x3's (0, 0) phase."""
 
     @staticmethod
-    def forward(ctx, x, w1, wd, stride, holds, wstream):
+    def forward(ctx, x, w1, wd, stride, holds, wstream, stats):
         w1, wd = holds.p
-        y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1))
-        yd = _conv_geo_fwd(x, wd, None, stride, (0, 0))
+        s1, sd = stats if stats is not None else (None, None)
+        y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1), s1)
+        yd = _conv_geo_fwd(x, wd, None, stride, (0, 0), sd)
         ctx.save_for_backward(x)
         ctx.params, ctx.wstream = (w1, wd), wstream
         ctx.stride = stride
@@ -446,7 +491,7 @@ class _ConvPair(torch.autograd.Function):
             dw1, dwd = _wgrad_on(ctx.wstream, lambda: (_conv_geo_wgrad(d1, x, w1, s, False)[0] if n1 else None,
                                                        _conv_geo_wgrad(dd, x, wd, s, False)[0] if n2 else None),
                                  [d1, dd, x])
-        return dx, dw1, dwd, None, None, None
+        return dx, dw1, dwd, None, None, None, None
 
 
 def _pair_dgrad(d1, dd, w1, wd, x_shape, stride):
@@ -495,8 +540,9 @@ def pair_eligible(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor) -> bool:
             and down.kernel_size == (1, 1) and down.stride == (2, 2) and down.out_channels == conv1.out_channels)
 
 
-def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor):
-    """(conv1(x), down(x)) without biases (both folded into their norms)."""
+def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor, stats=None):
+    """(conv1(x), down(x)) without biases (both folded into their norms);
+    ``stats`` = (conv1's, down's) statistics requests (:func:`_conv3x3_into`)."""
     w1, st = _weight_in(conv1.weight)
     wd, _ = _weight_in(down.weight)
-    return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st)
+    return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st, stats)

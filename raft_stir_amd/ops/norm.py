@@ -17,6 +17,7 @@ Everything else (CPU, export, GroupNorm, identity) takes the composite path.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -25,6 +26,7 @@ import torch.nn.functional as F
 from . import _ext
 from . import enc_conv
 from . import fp32conv
+from ..runtime import weights
 
 _CL = torch.channels_last
 _FOLD_BIAS = os.environ.get("RS_FOLD_BIAS", "1") != "0"
@@ -94,10 +96,124 @@ def _hip_ok(norm, x, residual):
     return False
 
 
-def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None):
+# ------------------------------------------------------------ fused statistics
+# Instance norm and train-mode batch norm need per-channel statistics of the
+# conv output.  Where the conv runs on the hand-written kernels its epilogue
+# accumulates (sum, sum of squares) per channel into a per-norm-module fp32
+# buffer (vector atomics), and one tiny launch turns them into mean / rstd
+# and zeroes the buffer again (torch.ops.raft_stir.norm_finalize): no
+# separate reduction pass over the activation.  The fp32 atomics make the
+# sums order-dependent, so deterministic mode keeps the two-level reduction.
+_FUSED_STATS = os.environ.get("RS_NORM_FUSED_STATS", "1") != "0"
+
+
+def _deterministic() -> bool:
+    from ..runtime.determinism import is_deterministic
+    return is_deterministic()
+
+
+def _stats_request(norm: nn.Module, x: torch.Tensor, cout: int):
+    """(fp32 [G][cout][2] zeroed sums buffer, per_sample) for a fused-statistics
+    conv feeding ``norm``, or None (norm kind / mode without batch statistics,
+    deterministic mode, opt-out)."""
+    if not _FUSED_STATS:
+        return None
+    if isinstance(norm, nn.InstanceNorm2d):
+        per_sample = True
+    elif isinstance(norm, nn.BatchNorm2d) and norm.training:
+        per_sample = False
+    else:
+        return None
+    if _deterministic():
+        return None
+    G = x.shape[0] if per_sample else 1
+    buf = norm.__dict__.get("_rs_sums")
+    if buf is None or buf.shape != (G, cout, 2) or buf.device != x.device:
+        buf = torch.zeros(G, cout, 2, device=x.device, dtype=torch.float32)
+        norm.__dict__["_rs_sums"] = buf  # plain attribute: not a buffer, not in the state dict
+    return buf, per_sample
+
+
+def _cached(norm: nn.Module, name: str, srcs, compute):
+    """Per-module cache of tensors derived from ``srcs`` (eval-mode BatchNorm
+    constants).  Keyed on the weight generation and the sources' version
+    counters; a stale entry is recomputed INTO its existing storage, so hipGraphs
+    captured with it stay valid (runtime/weights.py refresh_all re-runs every
+    entry through the registered refresher)."""
+    key = (weights.generation(),) + tuple((t.data_ptr(), t._version) for t in srcs) + (norm.eps,)
+    hit = norm.__dict__.get(name)
+    if hit is not None and hit[0] == key:
+        return hit[2]
+    with torch.no_grad():
+        vals = compute()
+        if hit is not None and all(a.shape == b.shape for a, b in zip(hit[2], vals)):
+            for a, b in zip(hit[2], vals):
+                a.copy_(b)
+            vals = hit[2]
+    norm.__dict__[name] = (key, (srcs, compute), vals)
+    _LIVE.add(norm)
+    return vals
+
+
+_LIVE = weakref.WeakSet()
+
+
+def _refresh_cached() -> None:
+    for norm in list(_LIVE):
+        for name in ("_rs_affine", "_rs_moments"):
+            hit = norm.__dict__.get(name)
+            if hit is not None:
+                srcs, compute = hit[1]
+                norm.__dict__[name] = (None,) + hit[1:]
+                _cached(norm, name, srcs, compute)
+
+
+weights.register_refresher(_refresh_cached)
+
+
+def _eval_affine(norm: nn.BatchNorm2d, bias):
+    """Eval-mode BatchNorm (+ the folded conv bias) as per-channel (scale,
+    shift), padded to a multiple of 4 channels: y = x_nobias * scale + shift."""
+    srcs = [norm.running_mean, norm.running_var, norm.weight, norm.bias] + ([bias] if bias is not None else [])
+
+    def compute():
+        C = norm.running_mean.numel()
+        scale = norm.weight.detach().float() * torch.rsqrt(norm.running_var.float() + norm.eps)
+        mean = norm.running_mean.float() - (bias.detach().float() if bias is not None else 0.0)
+        shift = norm.bias.detach().float() - mean * scale
+        pad = (-C) % 4
+        sc = torch.zeros(C + pad, device=scale.device, dtype=torch.float32)
+        sh = torch.zeros(C + pad, device=scale.device, dtype=torch.float32)
+        sc[:C] = scale
+        sh[:C] = shift
+        return sc, sh
+    return _cached(norm, "_rs_affine", srcs, compute)
+
+
+def _eval_fused_ok(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, residual) -> bool:
+    """Eval-mode BatchNorm with nothing to differentiate: the whole norm ->
+    ReLU (-> residual add -> ReLU) chain goes into the conv epilogue."""
+    if not isinstance(norm, nn.BatchNorm2d) or norm.training or not _norm_kind_ok(norm):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad or norm.weight.requires_grad
+                                    or norm.bias.requires_grad
+                                    or (residual is not None and residual.requires_grad)):
+        return False
+    if residual is not None and (residual.shape[0] != x.shape[0] or residual.dtype != torch.bfloat16
+                                 or not residual.is_contiguous(memory_format=_CL)):
+        return False
+    if enc_conv.eligible(conv, x):
+        return True
+    return residual is None and enc_conv.eligible_geo(conv, x)
+
+
+def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None, stats=None):
     """``bias``: the producing convolution's bias, folded into the statistics
-    (see :func:`conv_norm_act`); None if already applied."""
+    (see :func:`conv_norm_act`); None if already applied.  ``stats``: the
+    (sums buffer, per_sample) the producing conv filled (:func:`_stats_request`)."""
     if not _hip_ok(norm, x, residual):
+        if stats is not None:  # the conv filled the sums: consume (zero) them for its next use
+            torch.ops.raft_stir.norm_finalize(stats[0], 1, 1e-5)
         if bias is not None:
             x = x + bias.to(x.dtype).view(1, -1, 1, 1)
         y = norm(x)
@@ -109,15 +225,21 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
     if residual is not None:
         residual = residual.contiguous(memory_format=_CL)
     xn = _nhwc(x)
-    if isinstance(norm, nn.InstanceNorm2d):
+
+    def batch_moments(per_sample):
         with torch.no_grad():  # the stats' gradient is part of _NormAct.backward
-            mean, rstd = torch.ops.raft_stir.norm_stats(xn, True, norm.eps)
+            if stats is not None:
+                n = x.numel() // x.shape[1] // (x.shape[0] if per_sample else 1)
+                return torch.ops.raft_stir.norm_finalize(stats[0], n, norm.eps)
+            return torch.ops.raft_stir.norm_stats(xn, per_sample, norm.eps)
+    if isinstance(norm, nn.InstanceNorm2d):
+        mean, rstd = batch_moments(True)
         return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True, bias)
     # BatchNorm2d
     batch_stats = norm.training
     if batch_stats:
+        mean, rstd = batch_moments(False)
         with torch.no_grad():
-            mean, rstd = torch.ops.raft_stir.norm_stats(xn, False, norm.eps)
             n = x.numel() // x.shape[1]
             rm, rv = norm.running_mean, norm.running_var
             if rm.dtype == torch.float32 and rv.dtype == torch.float32 and rm.is_contiguous() and rv.is_contiguous():
@@ -134,12 +256,23 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
                 rv.mul_(1 - m).add_(unbiased, alpha=m)
                 norm.num_batches_tracked.add_(1)
     else:
+        mean, rstd = _eval_moments(norm, bias)
+    return _NormAct.apply(x, norm.weight, norm.bias, residual, mean.contiguous(), rstd.contiguous(),
+                          relu, batch_stats, bias)
+
+
+def _eval_moments(norm: nn.BatchNorm2d, bias):
+    """(running mean - conv bias, rsqrt(running var + eps)) as (1, C) fp32,
+    cached on the module (:func:`_cached`)."""
+    srcs = [norm.running_mean, norm.running_var] + ([bias] if bias is not None else [])
+
+    def compute():
         mean = norm.running_mean.float().reshape(1, -1)
         if bias is not None:  # gamma * (x + b - mean) * rstd + beta
             mean = mean - bias.detach().float().reshape(1, -1)
         rstd = torch.rsqrt(norm.running_var.float() + norm.eps).reshape(1, -1)
-    return _NormAct.apply(x, norm.weight, norm.bias, residual, mean.contiguous(), rstd.contiguous(),
-                          relu, batch_stats, bias)
+        return mean.contiguous(), rstd.contiguous()
+    return _cached(norm, "_rs_moments", srcs, compute)
 
 
 def _norm_kind_ok(norm):
@@ -158,10 +291,16 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
     forward and no bias-gradient reduction over it backward."""
     if conv.bias is None or not _FOLD_BIAS or not _ext.use_hip(x) or not _norm_kind_ok(norm):
         return norm_act(norm, conv(x), relu, residual)
+    if _eval_fused_ok(conv, norm, x, residual):  # eval BatchNorm: everything in the conv epilogue
+        sc, sh = _eval_affine(norm, conv.bias)
+        return enc_conv.conv_norm(conv, x, sc, sh, relu, residual)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
-        return norm_act(norm, enc_conv.conv3x3(conv, x), relu, residual, bias=conv.bias)
+        st = _stats_request(norm, x, conv.out_channels)
+        return norm_act(norm, enc_conv.conv3x3(conv, x, st), relu, residual, bias=conv.bias, stats=st)
     if enc_conv.eligible_geo(conv, x):  # stride-2 3x3 / 1x1 (strided geometry of the same kernels)
-        return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False), relu, residual, bias=conv.bias)
+        st = _stats_request(norm, x, conv.out_channels)
+        return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False, stats=st), relu, residual, bias=conv.bias,
+                        stats=st)
     y = fp32conv.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return norm_act(norm, y, relu, residual, bias=conv.bias)
 
@@ -175,7 +314,14 @@ def conv_pair_norm_act(conv1: nn.Conv2d, norm1: nn.Module, down: nn.Conv2d, norm
     fold = (conv1.bias is not None and down.bias is not None and _FOLD_BIAS and _ext.use_hip(x)
             and _norm_kind_ok(norm1) and _norm_kind_ok(norm_d))
     if fold and enc_conv.pair_eligible(conv1, down, x):
-        y1, yd = enc_conv.conv_pair(conv1, down, x)
-        return (norm_act(norm1, y1, True, None, bias=conv1.bias),
-                norm_act(norm_d, yd, False, None, bias=down.bias))
+        if _eval_fused_ok(conv1, norm1, x, None) and _eval_fused_ok(down, norm_d, x, None):
+            sc1, sh1 = _eval_affine(norm1, conv1.bias)
+            scd, shd = _eval_affine(norm_d, down.bias)
+            return (enc_conv.conv_norm(conv1, x, sc1, sh1, True),
+                    enc_conv.conv_norm(down, x, scd, shd, False))
+        s1 = _stats_request(norm1, x, conv1.out_channels)
+        sd = _stats_request(norm_d, x, down.out_channels)
+        y1, yd = enc_conv.conv_pair(conv1, down, x, (s1, sd))
+        return (norm_act(norm1, y1, True, None, bias=conv1.bias, stats=s1),
+                norm_act(norm_d, yd, False, None, bias=down.bias, stats=sd))
     return conv_norm_act(conv1, norm1, x), conv_norm_act(down, norm_d, x, relu=False)

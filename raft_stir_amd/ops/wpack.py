@@ -8,11 +8,13 @@ step is ~250 launches and ~2 ms of host time per training step; instead every
 layout is registered once as a static INDEX MAP into the concatenation of
 its source parameters (the layout function evaluated on an index tensor).
 
-Layouts registered together live as views of one flat bf16 buffer (a
-CHUNK); a repack of a chunk is three kernels: cat(parameters) ->
-index_select -> cast into the flat buffer.  A chunk's storage never moves:
-layouts registered later (a second model, a deep copy, re-registration of a
-key) go into a NEW chunk, so a hipGraph captured against earlier views --
+Layouts registered together live as views of a CHUNK, a contiguous region
+of an ARENA: one flat bf16 buffer plus one int32 code per element (source
+row << 24 | index into that source).  A repack is ONE gather launch per arena
+(csrc/wpack.hip) that reads the parameters in place with their own strides
+and casts.  Storage never moves: layouts registered later (a second model, a
+deep copy, re-registration of a key) go into a NEW chunk appended to the
+arena (or a new arena), so a hipGraph captured against earlier views --
 ``GraphedInference`` or the repack recorded by ``GraphedTrainStep`` -- keeps
 reading live, current storage (``snapshot()`` hands a captured graph strong
 references to every chunk it recorded).  A chunk is dropped once every
@@ -22,7 +24,7 @@ Staleness: runtime/weights.generation() (bumped by every optimizer step --
 fused AdamW does not bump ``_version``) plus the parameters' own version
 counters.  Under ``runtime.weights.repack_in_graph()`` (a captured training
 step) lookups never repack; the step body calls :func:`repack` itself so the
-three kernels per chunk are part of every replay.
+gather launches are part of every replay.
 """
 from __future__ import annotations
 
@@ -31,6 +33,7 @@ from typing import Callable, Dict, List, Sequence
 
 import torch
 
+from . import _ext
 from ..runtime import weights as _wgen
 
 
@@ -50,62 +53,123 @@ class _Entry:
         return all(r() is not None for r in self.refs)
 
 
-class _Chunk:
-    """Entries packed together: one flat bf16 buffer, one gather map over
-    cat(the chunk's own distinct source parameters) + a trailing zero."""
+_MAX_SRC = 127          # source rows per arena (code = src << 24 | index)
+_ARENA_MIN = 1 << 23    # packed elements per arena (bf16 flat + int32 codes: 48 MiB)
 
-    def __init__(self, entries: List[_Entry], dev):
-        srcs, ids = [], {}
-        for e in entries:
-            for r in e.refs:
-                w = r()
-                if id(w) not in ids:
-                    ids[id(w)] = len(srcs)
-                    srcs.append(r)
-        offs, o = {}, 0
-        for r in srcs:
-            offs[id(r())] = o
-            o += r().numel()
-        zero = o
-        maps, n = [], 0
+
+class _Arena:
+    """Consecutive chunks in one flat bf16 buffer with one int32 code per
+    element (source row << 24 | logical index into that source, -1 = zero)
+    over the arena's source table: a repack of the whole arena is ONE gather
+    launch (csrc/wpack.hip) reading the parameters in place -- their own
+    strides, channels_last included.  Storage never moves or shrinks."""
+
+    def __init__(self, dev, cap):
+        self.dev = dev
+        self.cap = cap
+        self.flat = torch.zeros(cap, dtype=torch.bfloat16, device=dev)
+        self.code = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        self.used = 0
+        self.srcs = []      # weakrefs, row order of the source table
+        self.sid = {}       # id(param) -> row
+        self.tab = None     # device int64 [rows][10]
+        self.tab_key = None
+        self.hip = dev.type == "cuda"
+        self.gmap = None    # CPU fallback: index into cat(sources) + zero, int64 [used]
+
+    def fits(self, n, refs) -> bool:
+        new = len({id(r()) for r in refs
+                   if id(r()) not in self.sid or self.srcs[self.sid[id(r())]]() is not r()})
+        return self.used + n <= self.cap and len(self.srcs) + new <= _MAX_SRC
+
+    def add(self, entries) -> int:
+        """Append the entries' codes; returns the chunk offset."""
+        codes = []
         for e in entries:
             lo, trans = 0, []
             for r in e.refs:
                 w = r()
-                trans.append((lo, lo + w.numel(), offs[id(w)]))
+                row = self.sid.get(id(w))
+                if row is None or self.srcs[row]() is not w:  # new source (or a dead one's reused id)
+                    self.sid[id(w)] = len(self.srcs)
+                    self.srcs.append(r)
+                trans.append((lo, lo + w.numel(), self.sid[id(w)]))
                 lo += w.numel()
             lm = e.local_map
-            g = torch.full_like(lm, zero)
-            for a, b, go in trans:
+            c = torch.full_like(lm, -1)
+            for a, b, row in trans:
                 sel = (lm >= a) & (lm < b)
-                g[sel] = lm[sel] - a + go
-            maps.append(g)
-            n += g.numel()
-        self.srcs = srcs
-        self.numels = [r().numel() for r in srcs]
+                c[sel] = (lm[sel] - a) | (row << 24)
+            codes.append(c)
+        code = torch.cat(codes).to(torch.int32)
+        off = self.used
+        self.code[off:off + code.numel()].copy_(code.to(self.dev))
+        self.used += code.numel()
+        self.gmap = None
+        return off
+
+    def _table(self):
+        ws = [r() for r in self.srcs]
+        key = tuple(None if w is None else (w.data_ptr(), w.dtype, tuple(w.shape), w.stride()) for w in ws)
+        if key != self.tab_key:
+            rows = []
+            for w in ws:
+                if w is None or w.dim() > 4 or w.dtype not in (torch.float32, torch.bfloat16):
+                    rows.append([0] * 10)
+                    continue
+                pad = 4 - w.dim()
+                rows.append([w.data_ptr(), int(w.dtype == torch.bfloat16)] + [1] * pad + list(w.shape)
+                            + [0] * pad + list(w.stride()))
+            self.tab = torch.tensor(rows or [[0] * 10], dtype=torch.int64).to(self.dev)
+            self.tab_key = key
+        return self.tab
+
+    @torch.no_grad()
+    def repack(self):
+        if self.used == 0:
+            return
+        if self.hip and _ext.use_hip(self.flat):
+            torch.ops.raft_stir.wpack_gather(self.code[:self.used], self._table(), self.flat[:self.used],
+                                             [], [], [])
+            return
+        # reference path (CPU): cat(sources) + zero, gathered by the decoded codes
+        ws = [r() for r in self.srcs]
+        numels = [(w.numel() if w is not None else 0) for w in ws]
+        if self.gmap is None or self.gmap[1] != numels:
+            offs, o = [], 0
+            for n in numels:
+                offs.append(o)
+                o += n
+            code = self.code[:self.used].long().cpu()
+            row, li = code >> 24, code & 0xffffff
+            g = torch.full_like(code, o)
+            ok = code >= 0
+            g[ok] = torch.tensor(offs, dtype=torch.long)[row[ok]] + li[ok]
+            self.gmap = (g.to(self.dev), numels)
+        parts = [w.detach().reshape(-1).float() for w in ws if w is not None]
+        src = torch.cat(parts + [torch.zeros(1, device=self.dev)])
+        self.flat[:self.used].copy_(src.index_select(0, self.gmap[0]))
+
+
+class _Chunk:
+    """Entries registered together: a contiguous region of an arena."""
+
+    def __init__(self, entries: List[_Entry], arena: _Arena):
+        self.arena = arena
         self.entries = list(entries)
-        self.gmap = torch.cat(maps).to(dev)
-        self.flat = torch.empty(n, dtype=torch.bfloat16, device=dev)
-        o = 0
+        n = sum(e.local_map.numel() for e in entries)
+        o = arena.add(entries)
+        self.flat = arena.flat[o:o + n]
         for e in entries:
             k = e.local_map.numel()
-            e.view = self.flat[o:o + k].view(e.shape)
+            e.view = arena.flat[o:o + k].view(e.shape)
             e.chunk = self
             o += k
 
     def alive(self) -> bool:
         return any(e.alive() for e in self.entries)
 
-    @torch.no_grad()
-    def repack(self):
-        dev = self.flat.device
-        ws = [r() for r in self.srcs]
-        # a source that died (another model of the chunk was freed) packs as zeros:
-        # its layouts are unreachable, the live ones keep their offsets
-        parts = [w.detach().reshape(-1).float() if w is not None else torch.zeros(n, device=dev)
-                 for w, n in zip(ws, self.numels)]
-        src = torch.cat(parts + [torch.zeros(1, device=dev)])
-        self.flat.copy_(src.index_select(0, self.gmap))
+    def mark_packed(self):
         for e in self.entries:
             if e.alive():
                 e.vers = tuple((r().data_ptr(), r()._version) for r in e.refs)
@@ -116,6 +180,7 @@ class _Registry:
         self.dev = dev
         self.entries: Dict[tuple, _Entry] = {}   # key -> current entry
         self.chunks: List[_Chunk] = []
+        self.arenas: List[_Arena] = []
         self.pending: List[_Entry] = []          # registered, not yet in a chunk
         self.gen = None
 
@@ -130,18 +195,29 @@ class _Registry:
         self.chunks = [c for c in self.chunks if c.alive()]
         self.entries = {k: e for k, e in self.entries.items() if e.alive()}
         if live:
-            self.chunks.append(_Chunk(live, self.dev))
+            n = sum(e.local_map.numel() for e in live)
+            refs = [r for e in live for r in e.refs]
+            arena = self.arenas[-1] if self.arenas else None
+            if arena is None or not arena.fits(n, refs):
+                arena = _Arena(self.dev, max(n, _ARENA_MIN))
+                self.arenas.append(arena)
+            self.chunks.append(_Chunk(live, arena))
+        live_arenas = {id(c.arena) for c in self.chunks}
+        self.arenas = [a for a in self.arenas if id(a) in live_arenas or a is self.arenas[-1]]
         del hold
 
     # ---------------------------------------------------------------- values
     @torch.no_grad()
     def repack(self):
-        """Every registered layout from the current parameter values (3 kernels per chunk)."""
+        """Every registered layout from the current parameter values (one
+        gather launch per arena)."""
         STATS["repacks"] += 1
         if self.pending:
             self._flush()
+        for a in {id(c.arena): c.arena for c in self.chunks}.values():
+            a.repack()
         for c in self.chunks:
-            c.repack()
+            c.mark_packed()
         self.gen = _wgen.generation()
 
     def get(self, key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
@@ -197,9 +273,13 @@ def repack() -> None:
 
 
 def snapshot() -> list:
-    """Strong references to every chunk's storage and gather map: a hipGraph
-    that recorded ``repack()`` keeps them for its whole life."""
-    return [(c.flat, c.gmap, list(c.srcs)) for reg in _REGS.values() for c in reg.chunks]
+    """Strong references to every arena's storage, codes and source table: a
+    hipGraph that recorded ``repack()`` keeps them for its whole life."""
+    out = []
+    for reg in _REGS.values():
+        for a in {id(c.arena): c.arena for c in reg.chunks}.values():
+            out.append((a.flat, a.code, a._table(), list(a.srcs)))
+    return out
 
 
 def refresh() -> None:

@@ -15,12 +15,51 @@ import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
 
+GLUE = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::cat", "aten::scatter", "aten::gather", "aten::add",
+        "aten::add_", "aten::mul", "aten::sub", "aten::rsqrt", "aten::sum", "aten::index", "aten::clone",
+        "aten::contiguous", "aten::_to_copy", "aten::empty_like", "aten::zeros_like", "aten::index_select",
+        "aten::copy", "aten::permute_copy", "aten::where", "aten::masked_fill", "aten::div", "aten::clamp", "aten::stack")
+
+
+class GlueTrace:
+    """TorchDispatchMode that attributes every glue aten op (GLUE) to the
+    innermost repo source line on the Python stack (the profiler's own stacks
+    come back empty for ops issued from autograd.Function bodies on ROCm)."""
+
+    def __init__(self):
+        import traceback
+        from torch.utils._python_dispatch import TorchDispatchMode
+        agg = self.agg = {}
+
+        class Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                name = "aten::" + func.__name__.split(".")[0]
+                if name in GLUE:
+                    where = "(no repo frame)"
+                    for fr in reversed(traceback.extract_stack()):
+                        if ("raft_stir_amd" in fr.filename or "/scripts/" in fr.filename) and \
+                                "torch_prof.py" not in fr.filename:
+                            where = f"{fr.filename.split('raft_stir_amd/')[-1]}:{fr.lineno} {fr.name}"
+                            break
+                    agg[(name, where)] = agg.get((name, where), 0) + 1
+                return func(*args, **(kwargs or {}))
+        self.mode = Mode()
+
+    def write(self, path):
+        with open(path, "w") as f:
+            f.write(f"{'calls':>6}  op  @ innermost repo frame\n")
+            for (name, where), c in sorted(self.agg.items(), key=lambda kv: -kv[1]):
+                f.write(f"{c:6d}  {name}  @ {where}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--mode", default="both")
     ap.add_argument("--out", default="gpurun_out")
+    ap.add_argument("--stacks", action="store_true",
+                    help="also attribute the glue ops (copy_, fill_, cat, scatter, ...) to Python source lines")
     a = ap.parse_args()
     from raft_stir_amd.config import make_args
     from raft_stir_amd.data.synthetic import make_batch
@@ -47,6 +86,12 @@ def main():
         for _ in range(3):
             step()
         torch.cuda.synchronize()
+        if a.stacks:
+            gt = GlueTrace()
+            with gt.mode:
+                step()
+            torch.cuda.synchronize()
+            gt.write(os.path.join(a.out, "torch_glue_train.txt"))
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             step()
             torch.cuda.synchronize()
@@ -66,6 +111,12 @@ def main():
             for _ in range(3):
                 model(i1, i2, iters=12, test_mode=True)
             torch.cuda.synchronize()
+            if a.stacks:
+                gt = GlueTrace()
+                with gt.mode:
+                    model(i1, i2, iters=12, test_mode=True)
+                torch.cuda.synchronize()
+                gt.write(os.path.join(a.out, "torch_glue_infer.txt"))
             with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
                 model(i1, i2, iters=12, test_mode=True)
                 torch.cuda.synchronize()

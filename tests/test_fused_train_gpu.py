@@ -137,15 +137,18 @@ def test_fused_training_matches_module_graph(cuda, small):
     assert not bad, bad
 
 
-def test_fused_training_onthefly_corr_matches_module_graph(cuda):
+@pytest.mark.parametrize("small", [False, True], ids=["raft_r4", "raft_small_r3"])
+def test_fused_training_onthefly_corr_matches_module_graph(cuda, small):
     """--alternate_corr training through the fused engine (on-the-fly
     correlation forward + atomic backward per iteration, gradients returned to
-    f1 / the pooled f2 levels) vs the module graph with the same correlation."""
+    f1 / the pooled f2 levels) vs the module graph with the same correlation;
+    RAFT-small runs it at its radius 3 (reference core/raft.py:29-33)."""
     from raft_stir_amd.data.synthetic import make_batch
     from raft_stir_amd.models.fused_train import FusedTrainEngine
     from raft_stir_amd.train.loss import sequence_loss
     torch.manual_seed(0)
-    m = RAFT(make_args(mixed_precision=True, alternate_corr=True)).to(cuda).to(memory_format=torch.channels_last)
+    m = RAFT(make_args(mixed_precision=True, alternate_corr=True, small=small)).to(cuda).to(
+        memory_format=torch.channels_last)
     m.train()
     ref = copy.deepcopy(m)
     ref.cfg = ref.cfg.__class__(**{**ref.cfg.to_dict(), "fused_train": False})

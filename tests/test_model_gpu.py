@@ -1,5 +1,6 @@
 """End-to-end model on the GPU (HIP path) vs the CPU ATen oracle."""
 import copy
+import os
 
 import pytest
 import torch
@@ -70,6 +71,56 @@ def test_bf16_pyramid_epe_drift(cuda):
     e_mix = (a - b).norm(dim=1).mean().item()
     e_bp = (a - c).norm(dim=1).mean().item()
     print(f"EPE vs fp32: bf16 engine {e_mix:.4f}, + bf16 pyramid {e_bp:.4f}")
+    assert e_bp <= 1.25 * e_mix + 0.02, (e_bp, e_mix)
+
+
+SINTEL = os.path.join(os.path.dirname(__file__), "data", "sintel_demo")
+
+
+def test_bf16_drift_real_frames_trained_model(cuda):
+    """EPE-drift gate on the reference's real Sintel demo pair (frame_0016 /
+    frame_0017, 1024x436, copied from reference demo-frames/) with a model
+    first trained for 200 synthetic steps, so its flows are non-trivial: the
+    bf16 engine (fp32 pyramid) and the bf16 engine + bf16 pyramid (the bench
+    configuration) vs the fp32 model (the reference's default precision,
+    evaluate.py:174)."""
+    import numpy as np
+    from PIL import Image
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.train.loss import sequence_loss
+    from raft_stir_amd.utils.padder import InputPadder
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=4e-4, weight_decay=1e-4, eps=1e-8)
+    for step in range(200):
+        i1, i2, fl, v = make_batch(4, 192, 256, seed=1000 + step, device=cuda)
+        opt.zero_grad(set_to_none=True)
+        loss, _ = sequence_loss(m(i1, i2, iters=6), fl, v, 0.8, sync_metrics=False)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+    m.eval()
+
+    def load(name):
+        a = np.asarray(Image.open(os.path.join(SINTEL, name)).convert("RGB"), dtype=np.float32)
+        return torch.from_numpy(a).permute(2, 0, 1)[None].to(cuda)
+    i1, i2 = load("frame_0016.png"), load("frame_0017.png")
+    i1, i2 = InputPadder(i1.shape).pad(i1, i2)
+    m32 = copy.deepcopy(m)
+    m32.cfg = m32.cfg.__class__(**{**m32.cfg.to_dict(), "mixed_precision": False})
+    mbp = copy.deepcopy(m)
+    mbp.cfg = mbp.cfg.__class__(**{**mbp.cfg.to_dict(), "corr_dtype": "bfloat16"})
+    with torch.no_grad():
+        _, a = m32(i1, i2, iters=12, test_mode=True)
+        _, b = m(i1, i2, iters=12, test_mode=True)
+        _, c = mbp(i1, i2, iters=12, test_mode=True)
+    mag = a.norm(dim=1).mean().item()
+    e_mix = (a - b).norm(dim=1).mean().item()
+    e_bp = (a - c).norm(dim=1).mean().item()
+    print(f"trained model on Sintel demo: mean |flow| {mag:.3f} px, EPE vs fp32: bf16 engine {e_mix:.4f}, "
+          f"+ bf16 pyramid {e_bp:.4f}")
+    assert mag > 0.5, mag  # the gate is only meaningful on non-trivial flows
+    assert e_mix <= 0.05 * mag + 0.05, (e_mix, mag)
     assert e_bp <= 1.25 * e_mix + 0.02, (e_bp, e_mix)
 
 
