@@ -51,13 +51,22 @@ __device__ __forceinline__ int swz(int r, int c) {
 
 // GEO: strided input / remapped output pixels (Args geometry fields): the
 // encoder's stride-2 convolutions and the phase-split dgrads of them.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool GEO = false>
+// F32: fp32 activations in and out (the reference's default inference
+// precision) on the bf16 MFMAs by operand splitting: x = xh + xl and
+// w = wh + wl (hi = bf16(x), lo = bf16(x - hi)), x.w ~= xh.wh + xl.wh + xh.wl
+// (relative error ~2^-17; the dropped xl.wl term is ~2^-18).  A K step covers
+// 32 input channels: the staged B row is [xh 32 | xl 32] (converted while
+// staging), the packed A row [wh 32 | wl 32] (ops/conv.py pack_weight_split),
+// and the three products are three MFMAs over the same LDS rows -- 3x the
+// MFMA work of bf16, no extra passes over the activations.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool GEO = false, bool F32 = false>
 __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
   static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(!F32 || BK == 64, "F32: 64-wide staged rows ([hi 32 | lo 32])");
   constexpr int CPR = BK / 8;  // 16-byte chunks per staged row
   constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
-  constexpr int NA = BM * CPR / 256, NB = BN * CPR / 256;
+  constexpr int NA = BM * CPR / 256, NB = F32 ? BN * 4 / 256 : BN * CPR / 256;  // F32: 8-channel units
   static_assert(NA >= 1 && NB >= 1, "BM, BN must be multiples of 64");
   __shared__ uint4 lds[2][(BM + BN) * CPR];
 
@@ -80,11 +89,12 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
     arow[i] = a.w + (size_t)(bm0 + id / CPR) * taps * Ktot + (id % CPR) * 8;
     acol[i] = id % CPR;
   }
+  constexpr int BCPR = F32 ? 4 : CPR;  // B staging units per row
   int sb[NB], sy[NB], sx[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int id = t + 256 * i;
-    const int p = bn0 + id / CPR;
+    const int p = bn0 + id / BCPR;
     if (p < a.P) {
       sb[i] = p / HW;
       const int q = p - sb[i] * HW;
@@ -97,13 +107,15 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   }
 
   const Seg s0 = a.seg[0], s1 = a.seg[1], s2 = a.seg[2];
-  constexpr int SH = BK == 32 ? 5 : 6;
+  constexpr int SH = (BK == 32 || F32) ? 5 : 6;  // input channels per K step: 32 (BK 32, F32) or 64
+  constexpr int KSTEP = F32 ? 32 : BK;
+  constexpr int WMUL = F32 ? 2 : 1;               // packed weight K per input channel ([wh | wl])
   const int e1 = taps * (s0.C >> SH);
   const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> SH) : 0);
   const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> SH) : 0);
   const uint4 zero = make_uint4(0, 0, 0, 0);
 
-  uint4 ra[NA], rb[NB];
+  uint4 ra[NA], rb[NB], rl[F32 ? NB : 1];
 #define RS_GLOAD(STEP)                                                                          \
   do {                                                                                          \
     const int step_ = (STEP);                                                                   \
@@ -115,15 +127,25 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
     const int local = step_ - (si == 0 ? 0 : (si == 1 ? e1 : e2));                             \
     const int chunks = sC >> SH;                                                                \
     const int tap = local / chunks;                                                             \
-    const int c0 = (local - tap * chunks) * BK;                                                 \
+    const int c0 = (local - tap * chunks) * KSTEP;                                              \
     const int dy = tap / KW - PH, dx = tap % KW - PW;                                           \
     _Pragma("unroll") for (int i = 0; i < NA; ++i)                                              \
-      ra[i] = ld16(arow[i] + (size_t)tap * Ktot + kseg + c0);                                   \
+      ra[i] = ld16(arow[i] + (size_t)tap * Ktot + (kseg + c0) * WMUL);                          \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
       const int yy = sy[i] * SY + dy, xx = sx[i] * SX + dx;                                     \
       const bool ok = sb[i] >= 0 && yy >= 0 && yy < Hi && xx >= 0 && xx < Wi;                  \
-      rb[i] = ok ? ld16(sp + ((size_t)(sb[i] * Hi + yy) * Wi + xx) * sst + c0 + ((t + 256 * i) % CPR) * 8) \
-                 : zero;                                                                        \
+      const size_t pix_ = (size_t)(sb[i] * Hi + yy) * Wi + xx;                                  \
+      if constexpr (F32) {                                                                      \
+        const float* fp_ = reinterpret_cast<const float*>(sp) + pix_ * sst + c0 + ((t + 256 * i) % 4) * 8; \
+        float4 q0 = make_float4(0.f, 0.f, 0.f, 0.f), q1 = q0;                                   \
+        if (ok) {                                                                               \
+          q0 = *reinterpret_cast<const float4*>(fp_);                                           \
+          q1 = *reinterpret_cast<const float4*>(fp_ + 4);                                       \
+        }                                                                                       \
+        split8(q0, q1, rb[i], rl[i]);                                                           \
+      } else {                                                                                  \
+        rb[i] = ok ? ld16(sp + pix_ * sst + c0 + ((t + 256 * i) % CPR) * 8) : zero;             \
+      }                                                                                         \
     }                                                                                           \
   } while (0)
 #define RS_LSTORE(BUF)                                                                          \
@@ -134,7 +156,12 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
     }                                                                                           \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
       const int id = t + 256 * i;                                                               \
-      lds[BUF][BM * CPR + swz<CPR>(id / CPR, id % CPR)] = rb[i];                                \
+      if constexpr (F32) {  /* unit j of the row: hi -> chunk j, lo -> chunk j + 4 */           \
+        lds[BUF][BM * CPR + swz<CPR>(id / 4, id % 4)] = rb[i];                                  \
+        lds[BUF][BM * CPR + swz<CPR>(id / 4, id % 4 + 4)] = rl[i];                              \
+      } else {                                                                                  \
+        lds[BUF][BM * CPR + swz<CPR>(id / CPR, id % CPR)] = rb[i];                              \
+      }                                                                                         \
     }                                                                                           \
   } while (0)
 
@@ -151,14 +178,18 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   for (int step = 0; step < nsteps; ++step) {
     const int buf = step & 1;
     if (step + 1 < nsteps) RS_GLOAD(step + 1);
+    // (A half, B half) per MFMA pass: bf16 -> the two 32-deep halves of the
+    // 64-deep step; F32 -> (wh, xh), (wh, xl), (wl, xh)
+    constexpr int NPASS = F32 ? 3 : BK / 32;
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int ka = F32 ? (ps == 2 ? 1 : 0) : ps, kb = F32 ? (ps == 1 ? 1 : 0) : ps;
       uint4 fa[WM], fb[WN];
 #pragma unroll
-      for (int mt = 0; mt < WM; ++mt) fa[mt] = lds[buf][swz<CPR>(wm * WM * 16 + mt * 16 + lr, kk * 4 + lc)];
+      for (int mt = 0; mt < WM; ++mt) fa[mt] = lds[buf][swz<CPR>(wm * WM * 16 + mt * 16 + lr, ka * 4 + lc)];
 #pragma unroll
       for (int nt = 0; nt < WN; ++nt)
-        fb[nt] = lds[buf][BM * CPR + swz<CPR>(wn * WN * 16 + nt * 16 + lr, kk * 4 + lc)];
+        fb[nt] = lds[buf][BM * CPR + swz<CPR>(wn * WN * 16 + nt * 16 + lr, kb * 4 + lc)];
 #pragma unroll
       for (int mt = 0; mt < WM; ++mt)
 #pragma unroll
@@ -187,15 +218,15 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
       py[nt] = px[nt] = 0;
     }
   }
-  if constexpr (GEO) {
-    int pp[WN];
+  int pp[WN];
 #pragma unroll
-    for (int nt = 0; nt < WN; ++nt)
-      pp[nt] = (pb[nt] * a.oH + py[nt] * a.OSY + a.OOY) * a.oW + px[nt] * a.OSX + a.OOX;
+  for (int nt = 0; nt < WN; ++nt)
+    pp[nt] = GEO ? (pb[nt] * a.oH + py[nt] * a.OSY + a.OOY) * a.oW + px[nt] * a.OSX + a.OOX
+                 : n0 + nt * 16 + lr;
+  if constexpr (F32)
+    epilogue_pix_f32<WM, WN>(a, acc, m0, lane, pp, pb);
+  else
     epilogue_pix<WM, WN>(a, acc, m0, lane, pp, pb, py, px);
-  } else {
-    epilogue<WM, WN>(a, acc, m0, n0, lane, pb, py, px);
-  }
 }
 
 // ------------------------------------------------------------------ direct-to-LDS variant
@@ -888,6 +919,7 @@ struct ConvLaunch {
   const float* chs;
   float* stats;
   int stats_ps;
+  int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 
 void conv_launch(const ConvLaunch& L, hipStream_t stream) {
@@ -912,6 +944,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
   a.w_bytes = L.w_bytes;
   a.chs = L.chs; a.stats = L.stats; a.stats_ps = L.stats_ps;
+  a.f32 = L.f32;
   static const int xcd_env = [] {
     const char* e = getenv("RS_CONV_XCD_REMAP");
     return e ? atoi(e) : 1;
@@ -921,8 +954,12 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     a.Hi = L.Hi; a.Wi = L.Wi; a.SY = L.SY; a.SX = L.SX;
     a.oH = L.oH; a.oW = L.oW; a.OSY = L.OSY; a.OSX = L.OSX; a.OOY = L.OOY; a.OOX = L.OOX;
 #define RS_GEO(BM_, BN_, WM_, WN_, BK_)                                                             \
-  hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, WM_, WN_, BK_, true>),                      \
-                     dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
+  if (L.f32)                                                                                       \
+    hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, WM_, WN_, 64, true, true>),               \
+                       dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a);          \
+  else                                                                                             \
+    hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, WM_, WN_, BK_, true>),                    \
+                       dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
     switch (L.tile) {
       case 2: RS_GEO(64, 128, 1, 4, 32); break;
       case 3: RS_GEO(64, 64, 2, 2, 32); break;
@@ -941,6 +978,16 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     a.ws_stamps = static_cast<unsigned long long*>(L.ws_stamps);
     if (!conv_ws_launch(a, L.ws_G, L.ws_NB, L.ws_blocks, stream))
       fprintf(stderr, "conv_ws: (KH=%d, KW=%d, G=%d, NB=%d) not instantiated\n", L.KH, L.KW, L.ws_G, L.ws_NB), abort();
+    return;
+  }
+  if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8 (host-checked)
+#define RS_F32(BM_, BN_)                                                                            \
+  hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, 2, 2, 64, false, true>),                     \
+                     dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
+    if (L.tile == 6) RS_F32(64, 64);
+    else if (L.tile == 8) RS_F32(128, 128);
+    else RS_F32(128, 64);
+#undef RS_F32
     return;
   }
   if (L.tile >= 24 && L.tile <= 26) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)

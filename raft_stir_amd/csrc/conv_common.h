@@ -76,7 +76,24 @@ struct Args {
   const float* chs;
   float* stats;
   int stats_ps;
+  int f32;  // fp32 activations / outputs (conv_lds_kernel<..., F32>, epilogue_pix_f32)
 };
+
+// fp32 -> (hi, lo) bf16 pairs for 8 consecutive channels: hi = rne(x),
+// lo = rne(x - hi) (F32 tiles: x.w ~= xh.wh + xl.wh + xh.wl)
+__device__ __forceinline__ void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16_t h0 = f2bf(x[2 * i]), h1 = f2bf(x[2 * i + 1]);
+    const bf16_t l0 = f2bf(x[2 * i] - bf2f(h0)), l1 = f2bf(x[2 * i + 1] - bf2f(h1));
+    h[i] = uint32_t(h0) | (uint32_t(h1) << 16);
+    l[i] = uint32_t(l0) | (uint32_t(l1) << 16);
+  }
+  hi = make_uint4(h[0], h[1], h[2], h[3]);
+  lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
@@ -343,9 +360,11 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
 // lane sums over the n-tiles, a reduce-scatter over those 16 lanes, then one
 // atomic per (channel, statistic) per wave.  A tile whose pixels span two
 // images (per-sample statistics only) takes per-element atomics instead.
-template <int WM, int WN>
+template <int WM, int WN, bool RND = true>
 __device__ __forceinline__ void stats_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
                                           const int (&pb)[WN]) {
+  // RND: statistics of the bf16-rounded stored values (bf16 outputs), else of the fp32 values
+  auto rnd = [](float x) { return RND ? bf2f(f2bf(x)) : x; };
   const int b0 = __builtin_amdgcn_readfirstlane(pb[0]);  // lane 0 / n-tile 0 holds the wave's first pixel
   if (b0 < 0) return;
   bool same = true;
@@ -370,7 +389,7 @@ __device__ __forceinline__ void stats_pix(const Args& a, const f32x4_t (&acc)[WM
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int nt = 0; nt < WN; ++nt) {
-          const float x = pb[nt] >= 0 ? bf2f(f2bf(acc[mt][nt][j] + bs[mt][j])) : 0.f;
+          const float x = pb[nt] >= 0 ? rnd(acc[mt][nt][j] + bs[mt][j]) : 0.f;
           s1 += x;
           s2 += x * x;
         }
@@ -402,7 +421,7 @@ __device__ __forceinline__ void stats_pix(const Args& a, const f32x4_t (&acc)[WM
         for (int j = 0; j < 4; ++j) {
           const int c = m0 + mt * 16 + cq + j;
           if (c < a.Cout) {
-            const float x = bf2f(f2bf(acc[mt][nt][j] + bs[mt][j]));
+            const float x = rnd(acc[mt][nt][j] + bs[mt][j]);
             atomicAdd(st + c * 2, x);
             atomicAdd(st + c * 2 + 1, x * x);
           }
@@ -430,6 +449,125 @@ __device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)
     RS_EPI(EPI_NORM);
 #undef RS_EPI
     default: epi_loop<WM, WN, EPI_BIAS>(a, acc, m0, lane, pp, pb, py, px); break;
+  }
+}
+
+// ---------------------------------------------------------------- fp32 epilogues
+// The F32 tiles' epilogues: the forward kinds of the inference engine and
+// the encoders (bias / ReLU / scale, ConvGRU gates and update, eval-BN
+// EPI_NORM with residual) on fp32 NHWC outputs and aux inputs (every
+// "bf16_t*" of Args is read as float*), plus the normalisation statistics of
+// the unrounded output.
+__device__ __forceinline__ void ld4f(const bf16_t* p, float (&f)[4]) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+__device__ __forceinline__ void st4f(void* p, const float (&f)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+}
+
+template <int E>
+__device__ __forceinline__ void epi_frag_f32(const Args& a, float (&v)[4], int cb, int p, bool vec) {
+  const bool full = cb + 3 < a.Cout;
+  auto fo = [](void* b, int str, int off, int p_, int c) { return static_cast<float*>(b) + (size_t)p_ * str + off + c; };
+  auto fi = [](const bf16_t* b, int str, int off, int p_, int c) {
+    return reinterpret_cast<const float*>(b) + (size_t)p_ * str + off + c;
+  };
+  if constexpr (E == EPI_GRU_ZR) {
+    if (cb < a.hd) {
+      float* z = fo(a.out, a.ostr, a.ooff, p, cb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z[j] = sigmoidf_(v[j]);
+    } else {
+      const int c = cb - a.hd;
+      const float* h = fi(a.aux1, a.a1str, a.a1off, p, c);
+      float* rh = fo(a.out2, a.o2str, a.o2off, p, c);
+      float* r = a.out3 ? fo(a.out3, a.o3str, a.o3off, p, c) : nullptr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float rv = sigmoidf_(v[j]);
+        rh[j] = rv * h[j];
+        if (r) r[j] = rv;
+      }
+    }
+  } else if constexpr (E == EPI_GRU_Q) {
+    const float* h = fi(a.aux1, a.a1str, a.a1off, p, cb);
+    const float* z = fi(a.aux2, a.a2str, a.a2off, p, cb);
+    float* hn = fo(a.out, a.ostr, a.ooff, p, cb);
+    float* qs = a.out2 ? fo(a.out2, a.o2str, a.o2off, p, cb) : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float q = tanhf(v[j]);
+      hn[j] = (1.f - z[j]) * h[j] + z[j] * q;
+      if (qs) qs[j] = q;
+    }
+  } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE / EPI_NORM
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (E == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+      if constexpr (E == EPI_SCALE) v[j] *= a.scale;
+      if constexpr (E == EPI_NORM)
+        if (a.hd) v[j] = fmaxf(v[j], 0.f);
+    }
+    float* o = fo(a.out, a.ostr, a.ooff, p, cb);
+    const float* r = (E == EPI_NORM && a.aux1) ? fi(a.aux1, a.a1str, a.a1off, p, cb) : nullptr;
+    if (vec && full) {
+      if (r) {
+        float rv[4];
+        ld4f(reinterpret_cast<const bf16_t*>(r), rv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j] + rv[j], 0.f);
+      }
+      st4f(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = r ? fmaxf(v[j] + r[j], 0.f) : v[j];
+    }
+  }
+}
+
+template <int WM, int WN, int E>
+__device__ __forceinline__ void epi_loop_f32(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                             const int (&pp)[WN], const int (&pb)[WN]) {
+  const int cq = (lane >> 4) * 4;
+  const bool vec =
+      ((a.ooff | a.ostr | a.o2off | a.o2str | a.o3off | a.o3str | a.a1off | a.a1str | a.a2off | a.a2str) & 3) == 0 &&
+      (((uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.out3 | (uintptr_t)a.aux1 | (uintptr_t)a.aux2) & 15) == 0;
+#pragma unroll
+  for (int nt = 0; nt < WN; ++nt) {
+    if (pb[nt] < 0) continue;
+#pragma unroll
+    for (int mt = 0; mt < WM; ++mt) {
+      const int cb = m0 + mt * 16 + cq;
+      if (cb >= a.Cout) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = cb + j;
+        const bool in = c < a.Cout;
+        const float sc = (E == EPI_NORM && in) ? a.chs[c] : 1.f;
+        v[j] = acc[mt][nt][j] * sc + (in && a.bias ? a.bias[c] : 0.f);
+      }
+      epi_frag_f32<E>(a, v, cb, pp[nt], vec);
+    }
+  }
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void epilogue_pix_f32(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
+                                                 const int (&pp)[WN], const int (&pb)[WN]) {
+  if (a.stats) stats_pix<WM, WN, false>(a, acc, m0, lane, pb);
+  switch (a.epi) {
+#define RS_EPI32(E) \
+  case E: epi_loop_f32<WM, WN, E>(a, acc, m0, lane, pp, pb); break
+    RS_EPI32(EPI_GRU_ZR);
+    RS_EPI32(EPI_GRU_Q);
+    RS_EPI32(EPI_RELU);
+    RS_EPI32(EPI_SCALE);
+    RS_EPI32(EPI_NORM);
+#undef RS_EPI32
+    default: epi_loop_f32<WM, WN, EPI_BIAS>(a, acc, m0, lane, pp, pb); break;
   }
 }
 

@@ -34,11 +34,13 @@ __device__ __forceinline__ void split_bf16(float x, uint32_t& hi, uint32_t& lo) 
   lo = f2bf(x - bf2f(h));
 }
 
+// OT: output activation type (bf16_t, or float for the fp32 inference engine)
+template <typename OT>
 __global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__ coords, int B, int H,
                                                        int W, const float* __restrict__ w,  // [49][2][Cout]
                                                        const float* __restrict__ bias, int Cout,
-                                                       bf16_t* __restrict__ out, int ostr, int ooff,
-                                                       bf16_t* __restrict__ fout, int fstr, int foff) {
+                                                       OT* __restrict__ out, int ostr, int ooff,
+                                                       OT* __restrict__ fout, int fstr, int foff) {
   __shared__ uint32_t fh[FE_PH * FE_PW], flo[FE_PH * FE_PW];  // (u | v << 16) bf16 pairs
   // the block's 64 channels of split weights, [co][ky][16 = kx * 2 + ci] (kx = 7: zero)
   __shared__ __attribute__((aligned(16))) bf16_t wh[64 * 7 * 16], wlo[64 * 7 * 16];
@@ -124,27 +126,40 @@ __global__ __launch_bounds__(256) void flow_enc_kernel(const float* __restrict__
     float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = fmaxf(acc[4 * g + j] + bias[c + j], 0.f);
-    uint2 u;
-    u.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-    u.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-    *reinterpret_cast<uint2*>(out + p * ostr + ooff + c) = u;
+    if constexpr (sizeof(OT) == 4) {
+      *reinterpret_cast<float4*>(out + p * ostr + ooff + c) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 u;
+      u.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+      u.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+      *reinterpret_cast<uint2*>(out + p * ostr + ooff + c) = u;
+    }
   }
   if (cb == 0 && lane < 32 && fout) {
-    const int pi = (pr + 3) * FE_PW + pc + 3;
-    const uint32_t h = fh[pi], l = flo[pi];
-    fout[p * fstr + foff] = f2bf(bf2f((bf16_t)(h & 0xffffu)) + bf2f((bf16_t)(l & 0xffffu)));
-    fout[p * fstr + foff + 1] = f2bf(bf2f((bf16_t)(h >> 16)) + bf2f((bf16_t)(l >> 16)));
+    if constexpr (sizeof(OT) == 4) {  // the exact fp32 flow
+      fout[p * fstr + foff] = cx[(size_t)y * W + x] - (float)x;
+      fout[p * fstr + foff + 1] = cy[(size_t)y * W + x] - (float)y;
+    } else {
+      const int pi = (pr + 3) * FE_PW + pc + 3;
+      const uint32_t h = fh[pi], l = flo[pi];
+      fout[p * fstr + foff] = f2bf(bf2f((bf16_t)(h & 0xffffu)) + bf2f((bf16_t)(l & 0xffffu)));
+      fout[p * fstr + foff + 1] = f2bf(bf2f((bf16_t)(h >> 16)) + bf2f((bf16_t)(l >> 16)));
+    }
   }
 }
 
 }  // namespace fe
 
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
-                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
+                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff, bool f32,
                      hipStream_t stream) {
   const dim3 grid((unsigned)(B * cdiv(H, fe::FE_T) * cdiv(W, fe::FE_T)), (unsigned)cdiv(Cout, 64));
-  hipLaunchKernelGGL(fe::flow_enc_kernel, grid, dim3(256), 0, stream, coords, B, H, W, w, bias,
-                     Cout, static_cast<bf16_t*>(out), ostr, ooff, static_cast<bf16_t*>(fout), fstr, foff);
+  if (f32)
+    hipLaunchKernelGGL(fe::flow_enc_kernel<float>, grid, dim3(256), 0, stream, coords, B, H, W, w, bias, Cout,
+                       static_cast<float*>(out), ostr, ooff, static_cast<float*>(fout), fstr, foff);
+  else
+    hipLaunchKernelGGL(fe::flow_enc_kernel<bf16_t>, grid, dim3(256), 0, stream, coords, B, H, W, w, bias, Cout,
+                       static_cast<bf16_t*>(out), ostr, ooff, static_cast<bf16_t*>(fout), fstr, foff);
 }
 
 }  // namespace rs

@@ -40,6 +40,18 @@ __device__ __forceinline__ void ldc(const bf16_t* p, float (&f)[CPL]) {
   }
 }
 
+// fp32 activations (the fp32 inference engine)
+template <int CPL>
+__device__ __forceinline__ void ldc(const float* p, float (&f)[CPL]) {
+  if constexpr (CPL == 4) {
+    const float4 u = *reinterpret_cast<const float4*>(p);
+    f[0] = u.x; f[1] = u.y; f[2] = u.z; f[3] = u.w;
+  } else {
+    const float2 u = *reinterpret_cast<const float2*>(p);
+    f[0] = u.x; f[1] = u.y;
+  }
+}
+
 template <int CPL>
 __device__ __forceinline__ void stc(bf16_t* p, const float (&f)[CPL]) {
   if constexpr (CPL == 4) {
@@ -52,10 +64,10 @@ __device__ __forceinline__ void stc(bf16_t* p, const float (&f)[CPL]) {
   }
 }
 
-// x: NHWC bf16 (pixel stride xstr, channel offset xoff), w: fp32 [2][9][Cin],
-// crd / src: (B, 2, H, W) fp32 (src may alias crd).
-template <int CPL>
-__global__ __launch_bounds__(256) void flowhead_fwd_kernel(const bf16_t* __restrict__ x, int xstr, int xoff,
+// x: NHWC bf16 or fp32 (pixel stride xstr, channel offset xoff), w: fp32
+// [2][9][Cin], crd / src: (B, 2, H, W) fp32 (src may alias crd).
+template <int CPL, typename XT>
+__global__ __launch_bounds__(256) void flowhead_fwd_kernel(const XT* __restrict__ x, int xstr, int xoff,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, int B, int H, int W,
                                                            float* crd, const float* src) {
@@ -84,7 +96,7 @@ __global__ __launch_bounds__(256) void flowhead_fwd_kernel(const bf16_t* __restr
   for (int ty = 0; ty < 3; ++ty) {
     const int yy = y + ty - 1;
     const bool iny = yy >= 0 && yy < H;
-    const bf16_t* row = x + ((size_t)(b * H + (iny ? yy : y)) * W) * xstr + xoff + lane * CPL;
+    const XT* row = x + ((size_t)(b * H + (iny ? yy : y)) * W) * xstr + xoff + lane * CPL;
 #pragma unroll
     for (int c = 0; c < PX + 2; ++c) {
       const int xx = x0 + c - 1;
@@ -214,16 +226,26 @@ __global__ __launch_bounds__(256) void flowhead_dgrad_kernel(const float* __rest
 }  // namespace fh
 
 void flowhead_fwd_launch(const void* x, int xstr, int xoff, int cin, const float* w, const float* bias, int B,
-                         int H, int W, float* crd, const float* src, hipStream_t s) {
+                         int H, int W, float* crd, const float* src, bool x_f32, hipStream_t s) {
   const int segs = B * H * cdiv(W, fh::PX);
   const dim3 grid(cdiv(segs, 4));
+  if (x_f32) {
+    const float* xf = static_cast<const float*>(x);
+    if (cin == 256)
+      hipLaunchKernelGGL((fh::flowhead_fwd_kernel<4, float>), grid, dim3(256), 0, s, xf, xstr, xoff, w, bias, B, H, W,
+                         crd, src);
+    else
+      hipLaunchKernelGGL((fh::flowhead_fwd_kernel<2, float>), grid, dim3(256), 0, s, xf, xstr, xoff, w, bias, B, H, W,
+                         crd, src);
+    return;
+  }
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   if (cin == 256)
-    hipLaunchKernelGGL(fh::flowhead_fwd_kernel<4>, grid, dim3(256), 0, s, xb, xstr, xoff, w, bias, B, H, W, crd,
-                       src);
+    hipLaunchKernelGGL((fh::flowhead_fwd_kernel<4, bf16_t>), grid, dim3(256), 0, s, xb, xstr, xoff, w, bias, B, H, W,
+                       crd, src);
   else
-    hipLaunchKernelGGL(fh::flowhead_fwd_kernel<2>, grid, dim3(256), 0, s, xb, xstr, xoff, w, bias, B, H, W, crd,
-                       src);
+    hipLaunchKernelGGL((fh::flowhead_fwd_kernel<2, bf16_t>), grid, dim3(256), 0, s, xb, xstr, xoff, w, bias, B, H, W,
+                       crd, src);
 }
 
 void flowhead_dgrad_launch(const float* dflow, const float* w, int cin, int B, int H, int W, const void* act,

@@ -39,15 +39,16 @@ struct ConvLaunch {
   const float* chs;
   float* stats;
   int stats_ps;
+  int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 constexpr int kWsTile = 48;
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
 bool conv_ws_instantiated(int KH, int KW, int G, int NB, int epi);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
-                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff,
+                     int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff, bool f32,
                      hipStream_t stream);
 void flowhead_fwd_launch(const void* x, int xstr, int xoff, int cin, const float* w, const float* bias, int B,
-                         int H, int W, float* crd, const float* src, hipStream_t s);
+                         int H, int W, float* crd, const float* src, bool x_f32, hipStream_t s);
 void flowhead_dgrad_launch(const float* dflow, const float* w, int cin, int B, int H, int W, const void* act,
                            int astr, int aoff, void* out, int ostr, int ooff, hipStream_t s);
 void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
@@ -184,10 +185,19 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   const int B = segs[0].size(0), H = segs[0].size(1), W = segs[0].size(2);
   const c10::DeviceGuard guard(segs[0].device());
   rs::ConvLaunch L{};
+  // fp32 activations: the split-bf16 register-staged tiles (conv.hip conv_lds_kernel<..., F32>)
+  const bool f32 = segs[0].scalar_type() == at::kFloat;
+  const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
+  if (f32) {
+    TORCH_CHECK(tile == 6 || tile == 7 || tile == 8, "conv_fused: fp32 activations run on tiles 6, 7, 8 only");
+    TORCH_CHECK(epi == 0 || epi == 1 || epi == 2 || epi == EPI_GRU_ZR || epi == EPI_GRU_Q || epi == EPI_NORM,
+                "conv_fused: fp32 activations support the forward epilogues (bias, relu, scale, gru_zr, gru_q, norm)");
+  }
+  L.f32 = f32 ? 1 : 0;
   int Ktot = 0;
   for (size_t s = 0; s < 3; ++s) {
     if (s < segs.size()) {
-      check_nhwc(segs[s], B, H, W, "segment");
+      check_nhwc(segs[s], B, H, W, "segment", adt);
       const int C = seg_C[s], off = seg_off[s], Cb = segs[s].size(3);
       TORCH_CHECK(C > 0 && C % 32 == 0, "conv_fused: segment channels must be a positive multiple of 32");
       TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb,
@@ -196,7 +206,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
       L.seg_C[s] = C;
       L.seg_stride[s] = Cb;
       TORCH_CHECK(segs[s].numel() * 2 < (int64_t(1) << 31), "conv_fused: segment tensor must be < 2 GiB");
-      L.seg_bytes[s] = (unsigned)((segs[s].numel() - off) * 2);
+      L.seg_bytes[s] = (unsigned)((segs[s].numel() - off) * segs[s].element_size());
       Ktot += C;
     } else {
       L.seg_ptr[s] = L.seg_ptr[0];
@@ -225,13 +235,14 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
                     : (bm128 || bm128w) ? 128 : (tile == 5 ? 16 : 64);
-  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && !ws)  // 64-deep K steps
+  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && !ws && !f32)  // 64-deep K steps
     for (size_t s = 0; s < segs.size(); ++s)
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: 64-deep-K tiles need segment channels % 64 == 0");
   if (!ws) {
     TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
                 "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
-    TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == Ktot, "conv_fused: packed weight K mismatch");
+    TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == (f32 ? 2 : 1) * Ktot,
+                "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
     TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
                 "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
   }
@@ -244,7 +255,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   L.w_bytes = (unsigned)(w.numel() * 2);
   L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.B = B; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.PH = KH / 2; L.PW = KW / 2;
-  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;
+  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = ws ? Ktot : w.size(2);  // weight row length
   L.epi = epi; L.scale = scale; L.hd = hd; L.tile = tile;
   if (epi == EPI_FLOW) {
     TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kFloat && out.dim() == 4 &&
@@ -259,7 +270,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
       L.out2 = out2->data_ptr();
     }
   } else {
-    const bool f32out = epi == EPI_ACC_F32 || epi == EPI_GRU_QBWD;
+    const bool f32out = f32 || epi == EPI_ACC_F32 || epi == EPI_GRU_QBWD;
     check_nhwc(out, B, H, W, "out", f32out ? at::kFloat : at::kBFloat16);
     const int cw = epi == EPI_GRU_ZR ? hd : Cout;
     TORCH_CHECK(ooff >= 0 && ooff + cw <= out.size(3), "conv_fused: output window out of bounds");
@@ -268,7 +279,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   auto opt_nhwc = [&](const c10::optional<Tensor>& t, int64_t off, int width, const char* n, void** p,
                       int* str, int* o) {
     if (!t) { *p = nullptr; *str = 0; *o = 0; return; }
-    check_nhwc(*t, B, H, W, n);
+    check_nhwc(*t, B, H, W, n, adt);
     TORCH_CHECK(off >= 0 && off + width <= t->size(3), "conv_fused: ", n, " window out of bounds");
     *p = t->data_ptr(); *str = t->size(3); *o = off;
   };
@@ -360,7 +371,9 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
               "conv_geo: 1..3 input segments");
   TORCH_CHECK(tile == 2 || tile == 3 || tile == 4 || tile == 6 || tile == 7 || tile == 8,
               "conv_geo: tile must be one of the register-staged variants 2, 3, 4, 6, 7, 8");
-  const int bk = tile >= 6 ? 64 : 32;
+  const bool f32 = segs[0].scalar_type() == at::kFloat;  // split-bf16 F32 tiles (32 input channels per step)
+  const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
+  const int bk = (tile >= 6 && !f32) ? 64 : 32;
   const int tileM = (tile == 2 || tile == 3 || tile == 6) ? 64 : 128;
   const int B = segs[0].size(0), Hi = segs[0].size(1), Wi = segs[0].size(2);
   const c10::DeviceGuard guard(segs[0].device());
@@ -368,7 +381,7 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   int Ktot = 0;
   for (size_t s = 0; s < 3; ++s) {
     if (s < segs.size()) {
-      check_nhwc(segs[s], B, Hi, Wi, "conv_geo segment");
+      check_nhwc(segs[s], B, Hi, Wi, "conv_geo segment", adt);
       const int C = seg_C[s], off = seg_off[s], Cb = segs[s].size(3);
       TORCH_CHECK(C > 0 && C % bk == 0, "conv_geo: segment channels must be a multiple of ", bk, " for tile ", tile);
       TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb, "conv_geo: segment window");
@@ -385,15 +398,16 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && SY >= 1 && SX >= 1 && Ho >= 1 && Wo >= 1 && Cout >= 1, "conv_geo: geometry");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3 &&
-                  w.size(1) == KH * KW && w.size(2) == Ktot && w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
+                  w.size(1) == KH * KW && w.size(2) == (f32 ? 2 : 1) * Ktot &&
+                  w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
               "conv_geo: packed weight must be bf16 [>= round_up(Cout, ", tileM, ")][KH*KW][Ktot]");
   if (bias)
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
                     bias->numel() >= Cout,
                 "conv_geo: bias fp32 (Cout,)");
-  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.scalar_type() == at::kBFloat16 &&
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.scalar_type() == adt &&
                   out.size(0) == B && ooff >= 0 && ooff + Cout <= out.size(3),
-              "conv_geo: out must be contiguous NHWC bf16 with room for the channel window");
+              "conv_geo: out must be contiguous NHWC (the input dtype) with room for the channel window");
   const int oH = out.size(1), oW = out.size(2);
   TORCH_CHECK(OSY >= 1 && OSX >= 1 && OOY >= 0 && OOX >= 0 && (Ho - 1) * OSY + OOY < oH &&
                   (Wo - 1) * OSX + OOX < oW,
@@ -402,7 +416,8 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   L.w = w.data_ptr();
   L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.B = B; L.H = Ho; L.W = Wo; L.KH = KH; L.KW = KW; L.PH = PH; L.PW = PW;
-  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = Ktot;
+  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = w.size(2);
+  L.f32 = f32 ? 1 : 0;
   const int epi = nscale ? EPI_NORM : 0;
   const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, B, Cout, "conv_geo");
   TORCH_CHECK(!relu || nscale, "conv_geo: relu goes with the EPI_NORM epilogue");
@@ -428,19 +443,20 @@ void flow_encode(const Tensor& coords, const Tensor& w, const Tensor& bias, cons
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.numel() == 98 * Cout,
               "flow_encode: w must be fp32 [49][2][Cout]");
   TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.is_contiguous(), "flow_encode: bias fp32");
-  check_nhwc(out, B, H, W, "out");
+  const bool f32 = out.scalar_type() == at::kFloat;  // fp32 inference engine
+  check_nhwc(out, B, H, W, "out", f32 ? at::kFloat : at::kBFloat16);
   TORCH_CHECK(ooff % 8 == 0 && out.size(3) % 8 == 0 && ooff + Cout <= out.size(3), "flow_encode: out window");
   void* fp = nullptr;
   int fstr = 0;
   if (fout) {
-    check_nhwc(*fout, B, H, W, "fout");
+    check_nhwc(*fout, B, H, W, "fout", f32 ? at::kFloat : at::kBFloat16);
     TORCH_CHECK(foff >= 0 && foff + 2 <= fout->size(3), "flow_encode: fout window");
     fp = fout->data_ptr();
     fstr = fout->size(3);
   }
   const c10::DeviceGuard guard(coords.device());
   rs::flow_enc_launch(coords.data_ptr<float>(), B, H, W, w.data_ptr<float>(), bias.data_ptr<float>(), Cout,
-                      out.data_ptr(), out.size(3), ooff, fp, fstr, foff, stream());
+                      out.data_ptr(), out.size(3), ooff, fp, fstr, foff, f32, stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -454,7 +470,8 @@ void flow_head(const Tensor& x, int64_t xoff, int64_t cin, const Tensor& w, cons
                   crd.size(1) == 2,
               "flow_head: coords must be contiguous fp32 (B,2,H,W)");
   const int B = crd.size(0), H = crd.size(2), W = crd.size(3);
-  check_nhwc(x, B, H, W, "x");
+  const bool xf = x.scalar_type() == at::kFloat;  // fp32 inference engine
+  check_nhwc(x, B, H, W, "x", xf ? at::kFloat : at::kBFloat16);
   const int vn = cin == 256 ? 4 : 2;  // channels per lane: aligned vector loads
   TORCH_CHECK(xoff >= 0 && xoff + cin <= x.size(3) && xoff % vn == 0 && x.size(3) % vn == 0,
               "flow_head: x channel window");
@@ -465,7 +482,7 @@ void flow_head(const Tensor& x, int64_t xoff, int64_t cin, const Tensor& w, cons
                        "flow_head: src must match coords");
   const c10::DeviceGuard guard(crd.device());
   rs::flowhead_fwd_launch(x.data_ptr(), x.size(3), xoff, cin, w.data_ptr<float>(), bias.data_ptr<float>(), B, H, W,
-                          crd.data_ptr<float>(), src ? src->data_ptr<float>() : crd.data_ptr<float>(), stream());
+                          crd.data_ptr<float>(), src ? src->data_ptr<float>() : crd.data_ptr<float>(), xf, stream());
   RS_CHECK_LAUNCH();
 }
 

@@ -3,7 +3,8 @@
 // read in place with the parameters' own strides (channels_last conv weights
 // included) and cast to the packed dtype:
 //
-//   out[i] = scale(i) * src_s[unravel(li)],   code[i] = (s << 24) | li,  code < 0 -> 0
+//   out[i] = scale(i) * src_s[unravel(li)],   code[i] = (lo << 30) | (s << 24) | li,  code < 0 -> 0
+//   (lo: the split-weight low part src - bf16(src) of the F32 conv tiles)
 //
 // One launch per chunk replaces flatten-copies of every channels_last source,
 // a cat of all sources, an index_select and a cast (4 + #sources launches and
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const int* __restrict__ cod
     const int c = code[i];
     float v = 0.f;
     if (c >= 0) {
-      const long long* t = tab + (long long)(c >> 24) * kTabCols;
+      const long long* t = tab + (long long)((c >> 24) & 63) * kTabCols;
       const long long ptr = t[0];
       if (ptr != 0) {
         long long li = c & 0xffffff;
@@ -44,6 +45,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const int* __restrict__ cod
         const long long i0 = li / t[3];
         const long long off = i0 * t[6] + i1 * t[7] + i2 * t[8] + i3 * t[9];
         v = t[1] ? bf2f(reinterpret_cast<const bf16_t*>(ptr)[off]) : reinterpret_cast<const float*>(ptr)[off];
+        if (c & (1 << 30)) v -= bf2f(f2bf(v));  // the lo half of a split (F32-tile) weight
       }
     }
     for (int r = 0; r < rg.n; ++r)

@@ -168,7 +168,10 @@ class _Encoder(nn.Module):
         return run
 
     def _head_conv(self, x):
-        """1x1 projection (with bias): HIP implicit GEMM on the GPU bf16 path."""
+        """1x1 projection (with bias): HIP implicit GEMM on the GPU bf16 path
+        and on the split-bf16 F32 tiles for fp32 inference."""
+        if enc_conv.eligible_f32(self.conv2, x):
+            return enc_conv.conv_f32(self.conv2, x)
         if enc_conv.eligible_geo(self.conv2, x):
             return enc_conv.conv_geo(self.conv2, x)
         return conv_module(self.conv2, x)

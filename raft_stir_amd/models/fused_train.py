@@ -255,7 +255,7 @@ class FusedTrainEngine:
         row = torch.searchsorted(starts, gather, right=True) - 1
         code = torch.where(gather == fill, torch.full_like(gather, -1),
                            ((row.clamp_min(0) << 24) | (gather - starts[row.clamp_min(0)])))
-        assert len(self.params) <= 127 and max(sizes) < (1 << 24)
+        assert len(self.params) <= 63 and max(sizes) < (1 << 24)
         code = code.to(torch.int32).to(dev)
         self._maps = dict(dev=dev, gather=gather.to(dev), nbf=nbf, layout=layout, scaled=scaled,
                           code_bf=code[:nbf], code_f32=code[nbf:], tab=None, tab_key=None,

@@ -31,28 +31,40 @@ corr radius 3 -> 196 channels, bilinear x8 upsampling).
 
 Packed weights are cached per (parameter versions) and rebuilt after any
 in-place update, so an optimizer step between evaluations is picked up.
+
+fp32 (the reference's default inference precision, evaluate.py:174 /
+rafttoonnx.py): the same sequence on fp32 buffers, every conv on the
+split-bf16 F32 tiles (csrc/conv.hip conv_lds_kernel<..., F32>: x.w as three
+bf16 MFMA products, ~2^-17 relative error), the flow encoder / flow head /
+lookup / upsampling in their fp32 forms.  RS_F32_ENGINE=0 sends fp32 back to
+the module graph (MIOpen convolutions).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
 
 from ..ops import _ext
-from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, conv_fused, pack_bias,
-                        pack_weight, pad_to)
+from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, choose_tile_f32, conv_fused,
+                        pack_bias, pack_weight, pack_weight_split, pad_to)
+
+_F32_ENGINE = os.environ.get("RS_F32_ENGINE", "1") != "0"
 from ..ops.upsample import convex_upsample
 
 
 class _Conv:
     """One packed convolution: weight [Cout_pad][taps][Ktot] bf16 + fp32 bias."""
 
-    def __init__(self, convs, segs, cout_pad_mult=32):
+    def __init__(self, convs, segs, f32=False):
         convs = convs if isinstance(convs, (list, tuple)) else [convs]
         weight = torch.cat([c.weight for c in convs], 0)
         bias = torch.cat([c.bias for c in convs], 0)
         self.cout = weight.shape[0]
         self.kh, self.kw = weight.shape[2], weight.shape[3]
-        self.w = pack_weight(weight, segs, pad_to(self.cout, 128))
+        pack = pack_weight_split if f32 else pack_weight
+        self.w = pack(weight, segs, pad_to(self.cout, 128))
         self.b = pack_bias(bias)
 
 
@@ -67,7 +79,7 @@ class FusedUpdate:
     def eligible(model, image, corr_fn) -> bool:
         if image.device.type != "cuda" or torch.is_grad_enabled():
             return False
-        if not model.cfg.mixed_precision or not model.cfg.fused_gru:
+        if not model.cfg.fused_gru or not (model.cfg.mixed_precision or _F32_ENGINE):
             return False
         if not _ext.use_hip(image):
             return False
@@ -76,12 +88,15 @@ class FusedUpdate:
     # ------------------------------------------------------------ weights
     def _version_key(self):
         from ..runtime.weights import generation
-        return (generation(),) + tuple((p.data_ptr(), p._version) for p in self.model.update_block.parameters())
+        return ((generation(), bool(self.model.cfg.mixed_precision))
+                + tuple((p.data_ptr(), p._version) for p in self.model.update_block.parameters()))
 
     @torch.no_grad()
     def _pack(self):
         ub = self.model.update_block
         small = self.model.cfg.small
+        self.f32 = f32 = not self.model.cfg.mixed_precision
+        _C = lambda convs, segs: _Conv(convs, segs, f32)  # noqa: E731
         if small:
             hd, cd, corr_c = 96, 64, 4 * 49
             self.corr_pad = pad_to(corr_c, 64)   # 256 (64-deep K steps)
@@ -89,18 +104,18 @@ class FusedUpdate:
             # hx = [h 96 | inp 64 | mot 80 | flow 2 | pad 14] = 256
             self.hx_c, self.off_inp, self.off_mot, self.off_flow = 256, 96, 160, 240
             self.mot_c = 128                    # [c1 96 | f2 32]
-            self.convc1 = _Conv(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
-            self.convf2 = _Conv(enc.convf2, [(64, [(0, 64, 0)])])
-            self.conv = _Conv(enc.conv, [(128, [(0, 128, 0)])])
+            self.convc1 = _C(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
+            self.convf2 = _C(enc.convf2, [(64, [(0, 64, 0)])])
+            self.conv = _C(enc.conv, [(128, [(0, 128, 0)])])
             self.f1_c = 64
             gru = ub.gru
             self.gru = [(
-                _Conv([gru.convz, gru.convr], [(256, [(0, hd, 0), (hd, cd + 82, hd)])]),
-                _Conv(gru.convq, [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]),
+                _C([gru.convz, gru.convr], [(256, [(0, hd, 0), (hd, cd + 82, hd)])]),
+                _C(gru.convq, [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]),
             )]
-            self.head = _Conv(ub.flow_head.conv1, [(96, [(0, hd, 0)])])
+            self.head = _C(ub.flow_head.conv1, [(96, [(0, hd, 0)])])
             self.head_c = 128
-            self.flow = _Conv(ub.flow_head.conv2, [(128, [(0, 128, 0)])])
+            self.flow = _C(ub.flow_head.conv2, [(128, [(0, 128, 0)])])
             self.mask0 = self.mask2 = None
         else:
             hd, cd, corr_c = 128, 128, 4 * 81
@@ -109,22 +124,22 @@ class FusedUpdate:
             # hx = [h 128 | inp 128 | mot 126 | flow 2] = 384
             self.hx_c, self.off_inp, self.off_mot, self.off_flow = 384, 128, 256, 382
             self.mot_c = 256                    # [c2 192 | f2 64]
-            self.convc1 = _Conv(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
-            self.convc2 = _Conv(enc.convc2, [(256, [(0, 256, 0)])])
-            self.convf2 = _Conv(enc.convf2, [(128, [(0, 128, 0)])])
-            self.conv = _Conv(enc.conv, [(256, [(0, 256, 0)])])
+            self.convc1 = _C(enc.convc1, [(self.corr_pad, [(0, corr_c, 0)])])
+            self.convc2 = _C(enc.convc2, [(256, [(0, 256, 0)])])
+            self.convf2 = _C(enc.convf2, [(128, [(0, 128, 0)])])
+            self.conv = _C(enc.conv, [(256, [(0, 256, 0)])])
             self.f1_c = 128
             g = ub.gru
             self.gru = []
             for zc, rc, qc in ((g.convz1, g.convr1, g.convq1), (g.convz2, g.convr2, g.convq2)):
                 self.gru.append((
-                    _Conv([zc, rc], [(384, [(0, 384, 0)])]),
-                    _Conv(qc, [(128, [(0, hd, 0)]), (256, [(hd, 256, 0)])]),
+                    _C([zc, rc], [(384, [(0, 384, 0)])]),
+                    _C(qc, [(128, [(0, hd, 0)]), (256, [(hd, 256, 0)])]),
                 ))
-            self.head = _Conv([ub.flow_head.conv1, ub.mask[0]], [(128, [(0, hd, 0)])])
+            self.head = _C([ub.flow_head.conv1, ub.mask[0]], [(128, [(0, hd, 0)])])
             self.head_c = 512
-            self.flow = _Conv(ub.flow_head.conv2, [(256, [(0, 256, 0)])])
-            self.mask2 = _Conv(ub.mask[2], [(256, [(0, 256, 0)])])
+            self.flow = _C(ub.flow_head.conv2, [(256, [(0, 256, 0)])])
+            self.mask2 = _C(ub.mask[2], [(256, [(0, 256, 0)])])
         self.hd, self.cd = hd, cd
         f1 = ub.encoder.convf1
         self.f1_w = f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()  # [7][7][2][Cout]
@@ -153,11 +168,12 @@ class FusedUpdate:
                 self.__dict__[name] = prev
 
     def _buffers(self, B, H, W, dev):
-        key = (B, H, W, dev)
+        key = (B, H, W, dev, self.f32)
         bufs = self.bufs.get(key)
         if bufs is None:
-            e = lambda c: torch.empty(B, H, W, c, device=dev, dtype=torch.bfloat16)
-            z = lambda c: torch.zeros(B, H, W, c, device=dev, dtype=torch.bfloat16)
+            dt = torch.float32 if self.f32 else torch.bfloat16
+            e = lambda c: torch.empty(B, H, W, c, device=dev, dtype=dt)  # noqa: E731
+            z = lambda c: torch.zeros(B, H, W, c, device=dev, dtype=dt)  # noqa: E731
             bufs = dict(corr=z(self.corr_pad), f1=e(self.f1_c), mot=e(self.mot_c), hx=z(self.hx_c),
                         z=e(self.hd), rh=z(pad_to(self.hd, 32)), head=e(self.head_c))
             if not self.model.cfg.small:
@@ -185,6 +201,13 @@ class FusedUpdate:
         bufs = self._buffers(B, H, W, coords1.device)
         hx = bufs["hx"]
         hd = self.hd
+        if self.f32:  # split-bf16 F32 tiles (fp32 activations)
+            P = B * H * W
+
+            def cf(segs, w, b, kh, kw, cout, epi, out, ooff=0, **kw_):
+                conv_fused(segs, w, b, kh, kw, cout, epi, out, ooff, tile=choose_tile_f32(P, cout), **kw_)
+        else:
+            cf = conv_fused
         hx[..., :hd].copy_(net.permute(0, 2, 3, 1))
         hx[..., self.off_inp:self.off_inp + self.cd].copy_(inp.permute(0, 2, 3, 1))
         coords1 = coords1.float().contiguous().clone()
@@ -203,47 +226,47 @@ class FusedUpdate:
                 side.wait_stream(main)  # coords1 of the previous iteration
                 with torch.cuda.stream(side):
                     torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
-                    conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                    cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
                                bufs["mot"], 192)
             if st is not None:
                 torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
             else:  # memory-efficient path: correlate the pooled fmap2 pyramid on the fly
                 c = torch.ops.raft_stir.corr_otf(corr_fn.f1, corr_fn.f2s, coords1, corr_fn.radius, corr_fn.scale,
-                                                 True)
+                                                 not self.f32)
                 bufs["corr"][..., :c.shape[-1]].copy_(c)
             if side is None:
                 torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
             cp = self.corr_pad
             if small:
-                conv_fused([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
+                cf([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
                            bufs["mot"], 0)
-                conv_fused([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
+                cf([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
                            bufs["mot"], 96)
-                conv_fused([(bufs["mot"], 0, 128)], self.conv.w, self.conv.b, 3, 3, 80, EPI_RELU,
+                cf([(bufs["mot"], 0, 128)], self.conv.w, self.conv.b, 3, 3, 80, EPI_RELU,
                            hx, self.off_mot)
             else:
-                conv_fused([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 256, EPI_RELU,
+                cf([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 256, EPI_RELU,
                            bufs["c1"], 0)
-                conv_fused([(bufs["c1"], 0, 256)], self.convc2.w, self.convc2.b, 3, 3, 192, EPI_RELU,
+                cf([(bufs["c1"], 0, 256)], self.convc2.w, self.convc2.b, 3, 3, 192, EPI_RELU,
                            bufs["mot"], 0)
                 if side is None:
-                    conv_fused([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                    cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
                                bufs["mot"], 192)
                 else:
                     main.wait_stream(side)
-                conv_fused([(bufs["mot"], 0, 256)], self.conv.w, self.conv.b, 3, 3, 126, EPI_RELU,
+                cf([(bufs["mot"], 0, 256)], self.conv.w, self.conv.b, 3, 3, 126, EPI_RELU,
                            hx, self.off_mot)
             for zr, q in self.gru:
                 rhc = bufs["rh"].shape[-1]
-                conv_fused([(hx, 0, self.hx_c)], zr.w, zr.b, zr.kh, zr.kw, 2 * hd, EPI_GRU_ZR,
+                cf([(hx, 0, self.hx_c)], zr.w, zr.b, zr.kh, zr.kw, 2 * hd, EPI_GRU_ZR,
                            bufs["z"], 0, hd=hd, out2=bufs["rh"], o2off=0, aux1=hx, a1off=0)
-                conv_fused([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
+                cf([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
                            EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0)
             if small:
-                conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0)
+                cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0)
                 torch.ops.raft_stir.flow_head(bufs["head"], 0, 128, self.flow_w32, self.flow_b32, coords1, None)
             else:
-                conv_fused([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
+                cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
                            bufs["head"], 0)
                 torch.ops.raft_stir.flow_head(bufs["head"], 0, 256, self.flow_w32, self.flow_b32, coords1, None)
             if not want_up:
@@ -252,7 +275,7 @@ class FusedUpdate:
             if small:
                 flow_up = 8 * F.interpolate(flow, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)
             else:
-                conv_fused([(bufs["head"], 256, 256)], self.mask2.w, self.mask2.b, 1, 1, 576, EPI_SCALE,
+                cf([(bufs["head"], 256, 256)], self.mask2.w, self.mask2.b, 1, 1, 576, EPI_SCALE,
                            bufs["mask"], 0, scale=0.25)
                 flow_up = convex_upsample(flow, bufs["mask"].permute(0, 3, 1, 2))
             preds.append(flow_up)

@@ -45,6 +45,36 @@ def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int,
 
 
 @torch.no_grad()
+@torch.no_grad()
+def split_weight(packed: torch.Tensor) -> torch.Tensor:
+    """A packed fp32 weight [Cout_pad][taps][Ktot] -> the F32 tiles' split
+    layout [Cout_pad][taps][2 * Ktot] bf16: per 32-channel K chunk [wh 32 | wl 32]
+    with wh = bf16(w), wl = bf16(w - wh) (csrc/conv.hip conv_lds_kernel<..., F32>)."""
+    cp, taps, k = packed.shape
+    assert k % 32 == 0
+    w = packed.float().view(cp, taps, k // 32, 1, 32)
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, lo], 3).reshape(cp, taps, 2 * k).contiguous()
+
+
+@torch.no_grad()
+def pack_weight_split(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int) -> torch.Tensor:
+    """:func:`pack_weight` in the F32 tiles' split [wh | wl] layout."""
+    return split_weight(pack_weight(weight, segs, cout_pad, torch.float32))
+
+
+F32_TILES = (6, 7, 8)
+
+
+def choose_tile_f32(P: int, cout: int) -> int:
+    """Split-bf16 fp32 tile: 64x64 for narrow outputs / small grids, else
+    128x64 (128x128 at large pixel counts)."""
+    if cout <= 64:
+        return 6
+    return 8 if (P >= 16384 and cout >= 256) else 7
+
+
 def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
     b = bias.detach().float()
     if n is not None and n > b.numel():

@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_BIAS, EPI_NORM, conv_fused, pack_weight, pad_to
+from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -238,12 +238,83 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
     return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats)
 
 
+# ------------------------------------------------------------- fp32 inference
+# fp32 (the reference's default inference precision) on the split-bf16 F32
+# tiles of csrc/conv.hip: every stride-1 / stride-2 3x3 and 1x1 encoder conv,
+# no autograd (fp32 training keeps the module graph).  Weights in the split
+# [wh | wl] layout through the same packed-weight registry (wpack.packed_split).
+_F32_ENC = os.environ.get("RS_F32_ENC", "1") != "0"
+
+
+def _split_weight(weight: torch.Tensor) -> torch.Tensor:
+    cout, cin = weight.shape[:2]
+    return wpack.packed_split(("fwd", id(weight)), [weight], lambda ws: pack_weight(
+        ws[0], [(cin, [(0, cin, 0)])], pad_to(cout, 128), _F32))
+
+
+def eligible_f32(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:
+    """fp32 inference conv on the F32 tiles: 3x3 (stride 1 / 2, pad 1) or 1x1
+    (stride 1 / 2), channel counts multiples of 32, nothing to differentiate."""
+    if not (_ENABLED and _F32_ENC) or x.dtype != torch.float32 or x.dim() != 4 or not _ext.use_hip(x):
+        return False
+    if torch.is_autocast_enabled("cuda"):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad
+                                    or (conv.bias is not None and conv.bias.requires_grad)
+                                    or (residual is not None and residual.requires_grad)):
+        return False
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros" or isinstance(p, str):
+        return False
+    if not ((k == (3, 3) and p == (1, 1) and s in ((1, 1), (2, 2))) or (k == (1, 1) and p == (0, 0) and s in ((1, 1), (2, 2)))):
+        return False
+    if conv.in_channels % 32 or conv.out_channels % 4 or not x.is_contiguous(memory_format=_CL):
+        return False
+    if residual is not None and (k != (3, 3) or s != (1, 1)):
+        return False
+    return x.numel() * 4 < (1 << 31)
+
+
+@torch.no_grad()
+def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None, scale=None, shift=None,
+             relu: bool = False, residual=None) -> torch.Tensor:
+    """fp32 ``conv(x)`` (:func:`eligible_f32`) with the optional epilogue extras:
+    ``stats`` (see :func:`_conv3x3_into`) or eval-BN ``scale`` / ``shift``
+    (+ ReLU, + residual; the conv bias must already be folded into shift)."""
+    xn = _nhwc(x)
+    N, H, W, cin = xn.shape
+    cout = conv.out_channels
+    kh, kw = conv.kernel_size
+    pad, stride = conv.padding, conv.stride
+    wp = _split_weight(conv.weight)
+    st, ps = stats if stats is not None else (None, False)
+    norm = scale is not None
+    b = shift if norm else (conv.bias.detach().float().contiguous() if (bias and conv.bias is not None) else None)
+    if stride == (1, 1) and (kh, kw) == (3, 3):
+        out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.float32)
+        rn = _nhwc(residual) if residual is not None else None
+        conv_fused([(xn, 0, cin)], wp, b, 3, 3, cout, EPI_NORM if norm else EPI_BIAS, out, 0,
+                   hd=int(bool(relu)), aux1=rn, tile=choose_tile_f32(N * H * W, cout), stats=st,
+                   stats_per_sample=ps, nscale=scale)
+        return out.permute(0, 3, 1, 2)
+    Ho = (H + 2 * pad[0] - kh) // stride[0] + 1
+    Wo = (W + 2 * pad[1] - kw) // stride[1] + 1
+    out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.float32)
+    torch.ops.raft_stir.conv_geo([xn], [0], [cin], wp, b, kh, kw, pad[0], pad[1], stride[0], stride[1], Ho, Wo,
+                                 cout, out, 0, 1, 1, 0, 0, choose_tile_f32(N * Ho * Wo, cout), st, bool(ps), scale,
+                                 bool(relu))
+    return out.permute(0, 3, 1, 2)
+
+
 def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residual=None) -> torch.Tensor:
     """Inference (no autograd): ``[relu](conv_nobias(x) * scale + shift)``, then
     ``relu(. + residual)`` -- an eval-mode BatchNorm (scale / shift per output
     channel, the conv bias folded into shift: ops/norm.py) and the block's
     activations in the conv epilogue.  Stride-1 3x3 convs (:func:`eligible`) and
-    strided / 1x1 ones (:func:`eligible_geo`, no residual)."""
+    strided / 1x1 ones (:func:`eligible_geo`, no residual); fp32 inputs on the
+    F32 tiles (:func:`eligible_f32`)."""
+    if x.dtype == torch.float32:
+        return conv_f32(conv, x, scale=scale, shift=shift, relu=relu, residual=residual)
     xn = _nhwc(x)
     N, H, W, cin = xn.shape
     cout = conv.out_channels

@@ -199,9 +199,11 @@ def _eval_fused_ok(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, residual) 
                                     or norm.bias.requires_grad
                                     or (residual is not None and residual.requires_grad)):
         return False
-    if residual is not None and (residual.shape[0] != x.shape[0] or residual.dtype != torch.bfloat16
+    if residual is not None and (residual.shape != x.shape[:1] + residual.shape[1:] or residual.dtype != x.dtype
                                  or not residual.is_contiguous(memory_format=_CL)):
         return False
+    if x.dtype == torch.float32:
+        return enc_conv.eligible_f32(conv, x, residual)
     if enc_conv.eligible(conv, x):
         return True
     return residual is None and enc_conv.eligible_geo(conv, x)
@@ -294,6 +296,10 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
     if _eval_fused_ok(conv, norm, x, residual):  # eval BatchNorm: everything in the conv epilogue
         sc, sh = _eval_affine(norm, conv.bias)
         return enc_conv.conv_norm(conv, x, sc, sh, relu, residual)
+    if enc_conv.eligible_f32(conv, x):  # fp32 inference on the split-bf16 F32 tiles
+        st = _stats_request(norm, x, conv.out_channels)
+        return norm_act(norm, enc_conv.conv_f32(conv, x, bias=False, stats=st), relu, residual, bias=conv.bias,
+                        stats=st)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
         st = _stats_request(norm, x, conv.out_channels)
         return norm_act(norm, enc_conv.conv3x3(conv, x, st), relu, residual, bias=conv.bias, stats=st)
@@ -313,6 +319,8 @@ def conv_pair_norm_act(conv1: nn.Conv2d, norm1: nn.Module, down: nn.Conv2d, norm
     3x3's (0, 0) phase) instead of two dgrads and an add."""
     fold = (conv1.bias is not None and down.bias is not None and _FOLD_BIAS and _ext.use_hip(x)
             and _norm_kind_ok(norm1) and _norm_kind_ok(norm_d))
+    if fold and x.dtype == torch.float32 and enc_conv.eligible_f32(conv1, x) and enc_conv.eligible_f32(down, x):
+        return conv_norm_act(conv1, norm1, x), conv_norm_act(down, norm_d, x, relu=False)
     if fold and enc_conv.pair_eligible(conv1, down, x):
         if _eval_fused_ok(conv1, norm1, x, None) and _eval_fused_ok(down, norm_d, x, None):
             sc1, sh1 = _eval_affine(norm1, conv1.bias)

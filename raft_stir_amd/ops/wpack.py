@@ -53,7 +53,8 @@ class _Entry:
         return all(r() is not None for r in self.refs)
 
 
-_MAX_SRC = 127          # source rows per arena (code = src << 24 | index)
+_MAX_SRC = 63           # source rows per arena (code = lo << 30 | src << 24 | index)
+_LOF = 1 << 40          # index-map flag: the element is lo = bf16(w - bf16(w)) (split layouts)
 _ARENA_MIN = 1 << 23    # packed elements per arena (bf16 flat + int32 codes: 48 MiB)
 
 
@@ -96,10 +97,12 @@ class _Arena:
                 trans.append((lo, lo + w.numel(), self.sid[id(w)]))
                 lo += w.numel()
             lm = e.local_map
+            lo = lm >= _LOF
+            base = torch.where(lo, lm - _LOF, lm)
             c = torch.full_like(lm, -1)
             for a, b, row in trans:
-                sel = (lm >= a) & (lm < b)
-                c[sel] = (lm[sel] - a) | (row << 24)
+                sel = (base >= a) & (base < b)
+                c[sel] = (base[sel] - a) | (row << 24) | (lo[sel].long() << 30)
             codes.append(c)
         code = torch.cat(codes).to(torch.int32)
         off = self.used
@@ -141,14 +144,18 @@ class _Arena:
                 offs.append(o)
                 o += n
             code = self.code[:self.used].long().cpu()
-            row, li = code >> 24, code & 0xffffff
+            row, li = (code >> 24) & 63, code & 0xffffff
             g = torch.full_like(code, o)
             ok = code >= 0
             g[ok] = torch.tensor(offs, dtype=torch.long)[row[ok]] + li[ok]
-            self.gmap = (g.to(self.dev), numels)
+            lo = ok & ((code >> 30) & 1).bool()
+            self.gmap = (g.to(self.dev), numels, lo.to(self.dev) if lo.any() else None)
         parts = [w.detach().reshape(-1).float() for w in ws if w is not None]
         src = torch.cat(parts + [torch.zeros(1, device=self.dev)])
-        self.flat[:self.used].copy_(src.index_select(0, self.gmap[0]))
+        v = src.index_select(0, self.gmap[0])
+        if self.gmap[2] is not None:
+            v = torch.where(self.gmap[2], v - v.to(torch.bfloat16).float(), v)
+        self.flat[:self.used].copy_(v)
 
 
 class _Chunk:
@@ -220,10 +227,10 @@ class _Registry:
             c.mark_packed()
         self.gen = _wgen.generation()
 
-    def get(self, key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
+    def get(self, key, weights: Sequence[torch.Tensor], layout: Callable, split: bool = False) -> torch.Tensor:
         e = self.entries.get(key)
         if e is None or len(e.refs) != len(weights) or any(r() is not w for r, w in zip(e.refs, weights)):
-            e = self._register(key, weights, layout)
+            e = self._register(key, weights, layout, split)
         if _wgen.force_repack() and e.view is not None:  # captured training step: the body repacks explicitly
             return e.view
         vers = tuple((w.data_ptr(), w._version) for w in weights)
@@ -232,7 +239,7 @@ class _Registry:
         return e.view
 
     @torch.no_grad()
-    def _register(self, key, weights, layout):
+    def _register(self, key, weights, layout, split=False):
         # index map: the layout evaluated on (local index + 1) so that the
         # layout's zero padding maps to -1
         n, idx = 0, []
@@ -241,6 +248,11 @@ class _Registry:
             n += w.numel()
         assert n < (1 << 24), "index map must be exact in fp32"
         lm = layout([t.float() for t in idx]).round().long() - 1
+        if split:  # [.., K] -> [.., 2K]: per 32-wide K chunk [w_hi 32 | w_lo 32] (ops/conv.py split_weight)
+            *lead, k = lm.shape
+            assert k % 32 == 0
+            m = lm.reshape(*lead, k // 32, 1, 32)
+            lm = torch.cat([m, torch.where(m >= 0, m + _LOF, m)], -2).reshape(*lead, 2 * k)
         e = _Entry(tuple(weakref.ref(w) for w in weights), layout, lm.reshape(-1).cpu(), tuple(lm.shape))
         self.entries[key] = e
         self.pending.append(e)
@@ -265,6 +277,16 @@ def packed(key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tens
     if reg is None:
         reg = _REGS[dev] = _Registry(dev)
     return reg.get(key, list(weights), layout)
+
+
+def packed_split(key, weights: Sequence[torch.Tensor], layout: Callable) -> torch.Tensor:
+    """:func:`packed` of an fp32-style layout in the split [wh | wl] form of
+    the F32 conv tiles (per 32-wide K chunk, wl = bf16(w - bf16(w)))."""
+    dev = weights[0].device
+    reg = _REGS.get(dev)
+    if reg is None:
+        reg = _REGS[dev] = _Registry(dev)
+    return reg.get(("split",) + tuple(key), list(weights), layout, True)
 
 
 def repack() -> None:

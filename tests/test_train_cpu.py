@@ -218,3 +218,17 @@ def test_wpack_batched_layouts_follow_updates():
         assert torch.equal(b, lay2([w1.detach(), w2.detach()]).to(torch.bfloat16))
         w1.grad, w2.grad = torch.randn_like(w1), torch.randn_like(w2)
         torch.optim.SGD([w1, w2], lr=0.5, foreach=True).step()
+
+
+def test_wpack_split_layout_matches_split_weight():
+    """wpack.packed_split (gathered [wh | wl] chunks) == ops/conv.py split_weight
+    of the fp32 packed layout, for a channels_last source."""
+    from raft_stir_amd.ops import wpack
+    from raft_stir_amd.ops.conv import pack_weight, pad_to, split_weight
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(40, 64, 3, 3).contiguous(memory_format=torch.channels_last))
+    lay = lambda ws: pack_weight(ws[0], [(64, [(0, 64, 0)])], pad_to(40, 128), torch.float32)  # noqa: E731
+    got = wpack.packed_split(("split_test", id(w)), [w], lay)
+    want = split_weight(lay([w.detach()]))
+    assert got.shape == want.shape and got.dtype == torch.bfloat16
+    assert torch.equal(got, want)
