@@ -81,6 +81,24 @@ bool deterministic();
 bool enc_halo_launch(const uint16_t* x, int xstr, const uint16_t* w, int Ktot, uint16_t* y, int ystr, int B, int H,
                      int W, int cin, int cout, int num_cus, const EncEpi& e, hipStream_t stream);
 bool enc_halo_supported(int cin, int cout);
+struct StemLaunch {  // must match stem.hip
+  const void* x;
+  int x_bf16, B, Hi, Wi, Ho, Wo;
+  const void* w;
+  const float* bias;
+  int Cout, epi, relu;
+  void* out;
+  int ostr, ooff;
+  const void* res;
+  int rstr;
+  const float* chs;
+  float* stats;
+  int stats_ps, f32;
+};
+void stem_launch(const StemLaunch& L, hipStream_t stream);
+int stem_wgrad_blocks(long P, int* px_per_block);
+void stem_wgrad_launch(const void* x, bool x_bf16, int B, int Hi, int Wi, int Ho, int Wo, const uint16_t* dy, int ystr,
+                       int Cout, float* part, int nblk, int px_per_block, float* dw, hipStream_t stream);
 }  // namespace rs
 
 namespace {
@@ -202,10 +220,11 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
       TORCH_CHECK(C > 0 && C % 32 == 0, "conv_fused: segment channels must be a positive multiple of 32");
       TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb,
                   "conv_fused: segment window out of bounds or misaligned");
-      L.seg_ptr[s] = static_cast<const at::BFloat16*>(segs[s].data_ptr()) + off;
+      L.seg_ptr[s] = static_cast<const char*>(segs[s].data_ptr()) + (size_t)off * segs[s].element_size();
       L.seg_C[s] = C;
       L.seg_stride[s] = Cb;
-      TORCH_CHECK(segs[s].numel() * 2 < (int64_t(1) << 31), "conv_fused: segment tensor must be < 2 GiB");
+      TORCH_CHECK(segs[s].numel() * segs[s].element_size() < (int64_t(1) << 31),
+                  "conv_fused: segment tensor must be < 2 GiB");
       L.seg_bytes[s] = (unsigned)((segs[s].numel() - off) * segs[s].element_size());
       Ktot += C;
     } else {
@@ -385,7 +404,7 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
       const int C = seg_C[s], off = seg_off[s], Cb = segs[s].size(3);
       TORCH_CHECK(C > 0 && C % bk == 0, "conv_geo: segment channels must be a multiple of ", bk, " for tile ", tile);
       TORCH_CHECK(off >= 0 && off % 8 == 0 && Cb % 8 == 0 && off + C <= Cb, "conv_geo: segment window");
-      L.seg_ptr[s] = static_cast<const at::BFloat16*>(segs[s].data_ptr()) + off;
+      L.seg_ptr[s] = static_cast<const char*>(segs[s].data_ptr()) + (size_t)off * segs[s].element_size();
       L.seg_C[s] = C;
       L.seg_stride[s] = Cb;
       Ktot += C;
@@ -731,9 +750,76 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
   RS_CHECK_LAUNCH();
 }
 
+// 7x7 / stride-2 / pad-3 stem conv, 3 -> Cout <= 64 (csrc/stem.hip).
+//   x: NHWC image [B, Hi, Wi, 3] fp32 or bf16; w: packed [64][7][32] bf16 (k = kx*3 + ci;
+//   fp32 output: the split [64][7][64] layout); out: NHWC [B, Ho, Wo, >= Cout] (bf16, or
+//   fp32 -> the split-bf16 MFMA path); epi 0 (+ bias, + stats) or EPI_NORM (nscale with
+//   bias = shift, relu).
+void stem_conv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const Tensor& out, int64_t Cout,
+               int64_t epi, const c10::optional<Tensor>& stats, bool stats_per_sample,
+               const c10::optional<Tensor>& nscale, bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3 &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "stem_conv: x must be a contiguous NHWC [B,H,W,3] fp32 / bf16 image");
+  const int B = x.size(0), Hi = x.size(1), Wi = x.size(2);
+  const int Ho = (Hi + 6 - 7) / 2 + 1, Wo = (Wi + 6 - 7) / 2 + 1;
+  const bool f32 = out.scalar_type() == at::kFloat;
+  check_nhwc(out, B, Ho, Wo, "stem_conv: out", f32 ? at::kFloat : at::kBFloat16);
+  TORCH_CHECK(Cout >= 1 && Cout <= 64 && Cout % 4 == 0 && out.size(3) >= Cout && out.size(3) % 4 == 0,
+              "stem_conv: Cout must be a multiple of 4 in [4, 64]");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3 &&
+                  w.size(0) == 64 && w.size(1) == 7 && w.size(2) == (f32 ? 64 : 32),
+              "stem_conv: packed weight must be bf16 [64][7][", f32 ? 64 : 32, "]");
+  TORCH_CHECK(epi == 0 || epi == EPI_NORM, "stem_conv: epilogue 0 (bias) or EPI_NORM");
+  if (bias)
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() >= Cout, "stem_conv: bias fp32 (Cout,)");
+  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, B, Cout, "stem_conv");
+  TORCH_CHECK(!relu || epi == EPI_NORM, "stem_conv: relu goes with EPI_NORM");
+  TORCH_CHECK((uintptr_t)out.data_ptr() % 16 == 0, "stem_conv: out alignment");
+  TORCH_CHECK(out.numel() < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 31), "stem_conv: size");
+  rs::StemLaunch L{};
+  L.x = x.data_ptr(); L.x_bf16 = x.scalar_type() == at::kBFloat16;
+  L.B = B; L.Hi = Hi; L.Wi = Wi; L.Ho = Ho; L.Wo = Wo;
+  L.w = w.data_ptr(); L.bias = bias ? bias->data_ptr<float>() : nullptr;
+  L.Cout = Cout; L.epi = epi; L.relu = relu ? 1 : 0;
+  L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = 0;
+  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps; L.f32 = f32 ? 1 : 0;
+  const c10::DeviceGuard guard(x.device());
+  rs::stem_launch(L, stream());
+  RS_CHECK_LAUNCH();
+}
+
+// dW (fp32 [Cout][3][7][7]) of the stem conv from dy (NHWC bf16 [B, Ho, Wo, >= Cout],
+// contiguous) and the image x: deterministic (per-block partials, ordered sum).
+void stem_wgrad(const Tensor& x, const Tensor& dy, int64_t Cout, const Tensor& dw) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3 &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "stem_wgrad: x must be a contiguous NHWC [B,H,W,3] image");
+  const int B = x.size(0), Hi = x.size(1), Wi = x.size(2);
+  const int Ho = (Hi + 6 - 7) / 2 + 1, Wo = (Wi + 6 - 7) / 2 + 1;
+  check_nhwc(dy, B, Ho, Wo, "stem_wgrad: dy");
+  TORCH_CHECK(Cout >= 1 && Cout <= 64 && dy.size(3) >= Cout && dy.size(3) % 8 == 0 &&
+                  (uintptr_t)dy.data_ptr() % 16 == 0, "stem_wgrad: dy channels / alignment");
+  TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.scalar_type() == at::kFloat && dw.numel() == Cout * 147,
+              "stem_wgrad: dw must be fp32 [Cout][3][7][7]");
+  const long P = (long)B * Ho * Wo;
+  int per = 0;
+  const int nblk = rs::stem_wgrad_blocks(P, &per);
+  const c10::DeviceGuard guard(x.device());
+  Tensor part = at::empty({(int64_t)nblk * 64 * 224}, dw.options());
+  rs::stem_wgrad_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, B, Hi, Wi, Ho, Wo,
+                        static_cast<const uint16_t*>(dy.data_ptr()), dy.size(3), Cout, part.data_ptr<float>(), nblk,
+                        per, dw.data_ptr<float>(), stream());
+  RS_CHECK_LAUNCH();
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("stem_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) out, int Cout, int epi, Tensor(b!)? stats=None, "
+        "bool stats_per_sample=False, Tensor? nscale=None, bool relu=False) -> ()");
+  m.def("stem_wgrad(Tensor x, Tensor dy, int Cout, Tensor(a!) dw) -> ()");
   m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout, Tensor(b!)? stats=None, "
         "bool stats_per_sample=False, Tensor? nscale=None, Tensor? nshift=None, Tensor? res=None, "
         "bool relu=False) -> ()");
@@ -766,6 +852,8 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("conv_ws", &conv_ws);
   m.impl("conv3x3_halo", &conv3x3_halo);
+  m.impl("stem_conv", &stem_conv);
+  m.impl("stem_wgrad", &stem_wgrad);
   m.impl("conv_geo", &conv_geo);
   m.impl("flow_encode", &flow_encode);
   m.impl("flow_head", &flow_head);

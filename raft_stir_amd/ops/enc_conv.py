@@ -238,6 +238,93 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
     return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats)
 
 
+# ------------------------------------------------------------------- 7x7 stem
+# The encoders' 7x7 / stride-2 stem (3 -> 64 / 32 channels) on csrc/stem.hip:
+# forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
+# conv epilogues (normalisation statistics, eval-BN scale / shift + ReLU) and a
+# deterministic MFMA weight gradient; the image needs no input gradient.
+_STEM = os.environ.get("RS_STEM", "1") != "0"
+
+
+def _stem_layout(ws):
+    w = ws[0]
+    cout = w.shape[0]
+    t = w.permute(0, 2, 3, 1).reshape(cout, 7, 21)  # [co][ky][kx * 3 + ci]
+    out = torch.zeros(64, 7, 32, dtype=t.dtype, device=t.device)
+    out[:cout, :, :21] = t
+    return out
+
+
+def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (_ENABLED and _STEM) or not _ext.use_hip(x) or x.dim() != 4:
+        return False
+    if conv.kernel_size != (7, 7) or conv.stride != (2, 2) or conv.padding != (3, 3) or conv.in_channels != 3:
+        return False
+    if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    if conv.out_channels > 64 or conv.out_channels % 8 or x.requires_grad:
+        return False
+    if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous(memory_format=_CL):
+        return False
+    f32 = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32
+    if f32 and torch.is_grad_enabled() and conv.weight.requires_grad:
+        return False  # fp32 training: the module graph
+    return x.numel() * 4 < (1 << 31)
+
+
+def _stem_out(conv, x):
+    N, _, H, W = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    f32 = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32
+    out = torch.empty(N, Ho, Wo, conv.out_channels, device=x.device,
+                      dtype=torch.float32 if f32 else torch.bfloat16)
+    w = (wpack.packed_split if f32 else wpack.packed)(("stem", id(conv.weight)), [conv.weight], _stem_layout)
+    return out, w
+
+
+class _Stem(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, hold, wstream, stats):
+        conv = hold.p
+        out, wp = _stem_out(conv, x)
+        st, ps = stats if stats is not None else (None, False)
+        torch.ops.raft_stir.stem_conv(_nhwc(x), wp, None, out, conv.out_channels, 0, st, ps)
+        ctx.save_for_backward(x)
+        ctx.param, ctx.wstream = conv.weight, wstream
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        weight = ctx.param
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dyn = _nhwc(dy.to(torch.bfloat16))
+
+            def wgrad():
+                g = torch.empty(weight.shape, device=dy.device, dtype=torch.float32)
+                torch.ops.raft_stir.stem_wgrad(_nhwc(x), dyn, weight.shape[0], g)
+                return (g.to(weight.dtype),)
+            dw, = _wgrad_on(ctx.wstream, wgrad, [dyn, x])
+        return None, dw, None, None, None
+
+
+def stem(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
+    """conv(x) without its bias (:func:`stem_eligible`); ``stats``: see
+    :func:`_conv3x3_into`."""
+    w, st = _weight_in(conv.weight)
+    return _Stem.apply(x, w, _Hold(conv), st, stats)
+
+
+@torch.no_grad()
+def stem_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool) -> torch.Tensor:
+    """Inference: ``[relu](conv_nobias(x) * scale + shift)`` (eval BatchNorm in the epilogue)."""
+    out, wp = _stem_out(conv, x)
+    torch.ops.raft_stir.stem_conv(_nhwc(x), wp, shift, out, conv.out_channels, EPI_NORM, None, False, scale,
+                                  bool(relu))
+    return out.permute(0, 3, 1, 2)
+
+
 # ------------------------------------------------------------- fp32 inference
 # fp32 (the reference's default inference precision) on the split-bf16 F32
 # tiles of csrc/conv.hip: every stride-1 / stride-2 3x3 and 1x1 encoder conv,

@@ -293,6 +293,14 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
     forward and no bias-gradient reduction over it backward."""
     if conv.bias is None or not _FOLD_BIAS or not _ext.use_hip(x) or not _norm_kind_ok(norm):
         return norm_act(norm, conv(x), relu, residual)
+    if residual is None and enc_conv.stem_eligible(conv, x):  # the 7x7 / stride-2 stem (csrc/stem.hip)
+        if isinstance(norm, nn.BatchNorm2d) and not norm.training and not (
+                torch.is_grad_enabled() and (conv.weight.requires_grad or norm.weight.requires_grad
+                                             or norm.bias.requires_grad)):
+            sc, sh = _eval_affine(norm, conv.bias)
+            return enc_conv.stem_norm(conv, x, sc, sh, relu)
+        st = _stats_request(norm, x, conv.out_channels)
+        return norm_act(norm, enc_conv.stem(conv, x, st), relu, residual, bias=conv.bias, stats=st)
     if _eval_fused_ok(conv, norm, x, residual):  # eval BatchNorm: everything in the conv epilogue
         sc, sh = _eval_affine(norm, conv.bias)
         return enc_conv.conv_norm(conv, x, sc, sh, relu, residual)

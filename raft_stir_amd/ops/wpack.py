@@ -72,6 +72,7 @@ class _Arena:
         self.code = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         self.used = 0
         self.srcs = []      # weakrefs, row order of the source table
+        self.numels = []    # element counts of the sources (dead ones pack as zeros)
         self.sid = {}       # id(param) -> row
         self.tab = None     # device int64 [rows][10]
         self.tab_key = None
@@ -94,6 +95,7 @@ class _Arena:
                 if row is None or self.srcs[row]() is not w:  # new source (or a dead one's reused id)
                     self.sid[id(w)] = len(self.srcs)
                     self.srcs.append(r)
+                    self.numels.append(w.numel())
                 trans.append((lo, lo + w.numel(), self.sid[id(w)]))
                 lo += w.numel()
             lm = e.local_map
@@ -137,7 +139,7 @@ class _Arena:
             return
         # reference path (CPU): cat(sources) + zero, gathered by the decoded codes
         ws = [r() for r in self.srcs]
-        numels = [(w.numel() if w is not None else 0) for w in ws]
+        numels = list(self.numels)
         if self.gmap is None or self.gmap[1] != numels:
             offs, o = [], 0
             for n in numels:
@@ -150,7 +152,8 @@ class _Arena:
             g[ok] = torch.tensor(offs, dtype=torch.long)[row[ok]] + li[ok]
             lo = ok & ((code >> 30) & 1).bool()
             self.gmap = (g.to(self.dev), numels, lo.to(self.dev) if lo.any() else None)
-        parts = [w.detach().reshape(-1).float() for w in ws if w is not None]
+        parts = [w.detach().reshape(-1).float() if w is not None else torch.zeros(n, device=self.dev)
+                 for w, n in zip(ws, numels)]
         src = torch.cat(parts + [torch.zeros(1, device=self.dev)])
         v = src.index_select(0, self.gmap[0])
         if self.gmap[2] is not None:

@@ -148,7 +148,7 @@ def test_graphed_inference_sees_weight_updates(cuda):
     i1 = torch.rand(1, 3, 128, 192, device=cuda) * 255
     i2 = torch.rand(1, 3, 128, 192, device=cuda) * 255
     gi = GraphedInference(m, i1.shape, iters=4)
-    gi(i1, i2)
+    before = gi(i1, i2)[1].clone()
     opt = torch.optim.AdamW(m.parameters(), lr=5e-3, fused=True)
     for p in m.parameters():
         p.grad = torch.randn_like(p)
@@ -156,4 +156,8 @@ def test_graphed_inference_sees_weight_updates(cuda):
     got = gi(i1, i2)[1].clone()
     with torch.no_grad():
         want = m(i1, i2, iters=4, test_mode=True)[1]
-    _close(got, want, 1e-3, "graphed flow after the update")
+    # stale weights would leave the replay at ~the pre-update flow; graph vs eager
+    # differ only by the order of the fp32 atomic statistics sums (bf16 flips)
+    moved = ((before - want).norm() / want.norm()).item()
+    assert moved > 1e-2, moved
+    _close(got, want, min(3e-3, 0.1 * moved), "graphed flow after the update")
