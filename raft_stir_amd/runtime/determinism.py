@@ -10,6 +10,9 @@ partials -- and makes the third refuse to run (train with the all-pairs
 correlation).  It also asks MIOpen for deterministic convolution algorithms
 (the encoder's strided / 1x1 convs) via ``torch.backends.cudnn``.
 
+The encoder norm statistics accumulated in the conv epilogues (fp32 atomics)
+are also switched off: deterministic mode keeps the two-level reduction.
+
 Everything else on the training path is deterministic by construction:
 norm statistics (per-block partials, fp64 finalize), the loss, the convex
 upsampling backward (gather), the pyramid lookup backward (row-owned
