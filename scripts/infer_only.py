@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Inference-only driver for profiling: RAFT full, bf16, 12 iterations,
-1088x436 (padded to 1088x440), batch 1, random-init weights, synthetic pair.
+1088x436 (padded to 1088x440), batch 1, random-init weights, synthetic pair;
+the pyramid dtype follows bench.py (--corr-dtype auto: bf16 under bf16).
 
     python scripts/infer_only.py [--reps 10] [--graph] [--small] [--size H W] [--alt]
 """
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--alt", action="store_true", help="on-the-fly correlation")
     ap.add_argument("--fp32", action="store_true")
+    ap.add_argument("--corr-dtype", default="auto", choices=["auto", "float32", "bfloat16"],
+                    help="pyramid storage, as bench.py (auto = bf16 under bf16 autocast)")
     a = ap.parse_args()
     from raft_stir_amd.config import make_args
     from raft_stir_amd.models import RAFT
@@ -31,7 +34,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = RAFT(make_args(small=a.small, mixed_precision=not a.fp32, alternate_corr=a.alt))
+    model = RAFT(make_args(small=a.small, mixed_precision=not a.fp32, alternate_corr=a.alt,
+                            corr_dtype=a.corr_dtype))
     model = model.to(dev).to(memory_format=torch.channels_last).eval()
     h, w = a.size
     i1 = torch.rand(1, 3, h, w, device=dev) * 255
