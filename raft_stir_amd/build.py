@@ -80,11 +80,6 @@ def _digest(path: str, flags) -> str:
 
 
 def _compile(src: str, flags, verbose: bool):
-    # kernel experiments: extra hipcc flags for the weight-stationary conv units
-    # only (e.g. RAFT_STIR_WS_FLAGS="-DRS_WS_STAMPS -DRS_WS_LIST=RS_WS(1,5,6)")
-    extra = os.environ.get("RAFT_STIR_WS_FLAGS", "")
-    if extra and os.path.basename(src).startswith("conv_ws"):
-        flags = list(flags) + extra.split()
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
     stamp = obj + ".sha1"
     dig = _digest(src, flags)

@@ -911,10 +911,6 @@ struct ConvLaunch {
   unsigned w_bytes;
   int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
   int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
-  // tile 48: weight-stationary kernel (conv_ws.hip)
-  const void* wf;
-  int ws_G, ws_NB, ws_ncs, ws_ncb, ws_rpc, ws_nstrips, ws_nrch, ws_rsp, ws_blocks;
-  void* ws_stamps;
   // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
   const float* chs;
   float* stats;
@@ -969,15 +965,6 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
       default: RS_GEO(128, 64, 2, 2, 32); break;  // 4
     }
 #undef RS_GEO
-    return;
-  }
-  if (L.tile == 48) {  // weight-stationary kernel (host-checked geometry: ops_conv.cpp ws_setup)
-    a.wf = static_cast<const bf16_t*>(L.wf);
-    a.ws_ncs = L.ws_ncs; a.ws_ncb = L.ws_ncb; a.ws_nstrips = L.ws_nstrips; a.ws_nrch = L.ws_nrch;
-    a.ws_rpc = L.ws_rpc; a.ws_rsp = L.ws_rsp; a.ws_kg = L.Ktot / 16;
-    a.ws_stamps = static_cast<unsigned long long*>(L.ws_stamps);
-    if (!conv_ws_launch(a, L.ws_G, L.ws_NB, L.ws_blocks, stream))
-      fprintf(stderr, "conv_ws: (KH=%d, KW=%d, G=%d, NB=%d) not instantiated\n", L.KH, L.KW, L.ws_G, L.ws_NB), abort();
     return;
   }
   if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8 (host-checked)

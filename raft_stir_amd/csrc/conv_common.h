@@ -1,4 +1,4 @@
-// Shared pieces of the implicit-GEMM convolution kernels (conv.hip, conv_v2.hip, conv_ws.h):
+// Shared pieces of the implicit-GEMM convolution kernels (conv.hip, conv_v2.hip):
 // epilogue kinds, the launch-argument block, the fused epilogues and the
 // staging helpers (buffer / global LDS-DMA, counted vmcnt waits, XCD remap).
 #pragma once
@@ -63,12 +63,6 @@ struct Args {
   // output pixel ((b*oH + y*OSY + OOY)*oW + x*OSX + OOX)
   int Hi, Wi, SY, SX;
   int oH, oW, OSY, OSX, OOY, OOX;
-  // weight-stationary kernel (conv_ws.hip): fragment-packed weights
-  // [Cout_pad/32][taps][Ktot/16][64 lanes][8], channel slices / co-blocks per
-  // block, 16-column strips, row chunks of ws_rpc rows, ring-row slots, Ktot/16
-  const bf16_t* wf;
-  int ws_ncs, ws_ncb, ws_nstrips, ws_nrch, ws_rpc, ws_rsp, ws_kg;
-  unsigned long long* ws_stamps;  // RS_WS_STAMPS builds only: per-wave s_memtime stamps
   // EPI_NORM per-channel scale; normalisation statistics of the stored output
   // (bf16-rounded acc + bias): stats[(g * Cout + co) * 2 + {0, 1}] += {sum, sum of
   // squares} with g = image (stats_ps) or 0 (vector atomics; the buffer is
@@ -707,6 +701,4 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint4* lds_base
 
 // conv_v2.hip: tiles 42-45 (3x3 / 1x5 / 5x1 only); false if the kernel size is not instantiated
 bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream);
-// conv_ws.hip: weight-stationary kernel; false if (KH, KW, G, NB) is not instantiated
-bool conv_ws_launch(const conv::Args& a, int G, int NB, int nblocks, hipStream_t stream);
 }  // namespace rs

@@ -31,19 +31,13 @@ struct ConvLaunch {
   unsigned w_bytes;
   int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
   int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
-  // tile kWsTile: weight-stationary kernel (conv_ws.hip)
-  const void* wf;
-  int ws_G, ws_NB, ws_ncs, ws_ncb, ws_rpc, ws_nstrips, ws_nrch, ws_rsp, ws_blocks;
-  void* ws_stamps;
   // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
   const float* chs;
   float* stats;
   int stats_ps;
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
-constexpr int kWsTile = 48;
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
-bool conv_ws_instantiated(int KH, int KW, int G, int NB, int epi);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
                      int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff, bool f32,
                      hipStream_t stream);
@@ -152,52 +146,13 @@ NormX norm_extras(const c10::optional<Tensor>& stats, bool per_sample, const c10
   return x;
 }
 
-// Weight-stationary kernel geometry (csrc/conv_ws.hip), checked against what
-// the kernel assumes: Ktot = ncs * 16 * G, ring + partials within 160 KiB,
-// <= 4 halo DMA pieces per wave per tile, <= 8 waves.
-void ws_setup(rs::ConvLaunch& L, const Tensor& wf, at::IntArrayRef cfg, int Ktot) {
-  TORCH_CHECK(cfg.size() == 5 || cfg.size() == 6,
-              "conv_ws: cfg = [G, NB, ncs, ncb, rows_per_chunk] (+ stamp buffer address, diagnostic builds)");
-  // diagnostic: device address of a [blocks * 8 * 66] int64 stamp buffer (RS_WS_STAMPS builds)
-  L.ws_stamps = cfg.size() == 6 ? reinterpret_cast<void*>(cfg[5]) : nullptr;
-  const int G = cfg[0], NB = cfg[1], ncs = cfg[2], ncb = cfg[3], rpc = cfg[4];
-  TORCH_CHECK(rs::conv_ws_instantiated(L.KH, L.KW, G, NB, L.epi), "conv_ws: (KH=", L.KH, ", KW=", L.KW, ", G=", G,
-              ", NB=", NB, ", epi=", L.epi, ") is not instantiated (csrc/conv_ws_*.hip)");
-  TORCH_CHECK(ncs == 4 && ncb == 1, "conv_ws: 4 channel slices x 1 output block per workgroup");
-  TORCH_CHECK(G >= 1 && ncs * 16 * G == Ktot, "conv_ws: Ktot (", Ktot, ") must equal 64 * G");
-  TORCH_CHECK(L.KH * L.KW * G <= 40, "conv_ws: too many weight fragments per wave");
-  TORCH_CHECK(rpc >= 1, "conv_ws: rows per chunk");
-  const int TH = 2 * NB, HWD = 16 + L.KW - 1, CS = 2 * G + 1;
-  const int rsp = (ncs * HWD * CS + 63) / 64 * 64;
-  const int RR = 2 * TH + L.KH - 1;
-  const int slots = RR * rsp + 2 * ncs * 4 * 64;  // halo ring + double-buffered partial sums
-  TORCH_CHECK(slots <= 10240, "conv_ws: LDS ring + partials exceed 160 KiB (", slots * 16, " B)");
-  const int pieces = TH * rsp / 64;
-  TORCH_CHECK((pieces + ncs - 1) / ncs <= 10, "conv_ws: more than 10 halo pieces per MFMA wave");
-  const int ncob = (L.Cout + 31) / 32, ncog = (ncob + ncb - 1) / ncb;
-  TORCH_CHECK(wf.is_cuda() && wf.is_contiguous() && wf.scalar_type() == at::kBFloat16 && wf.dim() == 3 &&
-                  wf.size(1) == L.KH * L.KW && wf.size(2) == Ktot && wf.size(0) % 32 == 0 &&
-                  wf.size(0) >= ncog * ncb * 32,
-              "conv_ws: fragment-packed weight must be bf16 [>= ", ncog * ncb * 32, "][taps][Ktot]");
-  L.wf = wf.data_ptr();
-  L.ws_G = G; L.ws_NB = NB; L.ws_ncs = ncs; L.ws_ncb = ncb; L.ws_rpc = rpc;
-  L.ws_nstrips = (L.W + 15) / 16;
-  L.ws_nrch = (L.H + rpc - 1) / rpc;
-  L.ws_rsp = rsp;
-  const int64_t blocks = int64_t(ncog) * L.B * L.ws_nstrips * L.ws_nrch;
-  TORCH_CHECK(blocks < (int64_t(1) << 31), "conv_ws: grid too large");
-  L.ws_blocks = (int)blocks;
-  L.tile = rs::kWsTile;
-}
-
 void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C,
                const Tensor& w, const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t Cout,
                int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
                const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
                int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
-               const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile, at::IntArrayRef ws_cfg,
+               const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile,
                const NormX& nx = NormX()) {
-  const bool ws = tile == rs::kWsTile;
   TORCH_CHECK(!segs.empty() && segs.size() <= 3, "conv_fused: 1..3 input segments");
   TORCH_CHECK(seg_off.size() == segs.size() && seg_C.size() == segs.size(), "conv_fused: segment spec");
   const int B = segs[0].size(0), H = segs[0].size(1), W = segs[0].size(2);
@@ -236,7 +191,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= rs::kWsTile, "conv_fused: tile must be in [0,48]");
+  TORCH_CHECK(tile >= 0 && tile <= 47, "conv_fused: tile must be in [0,47]");
   if (tile >= 42 && tile <= 47)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
@@ -254,17 +209,15 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
                     : (bm128 || bm128w) ? 128 : (tile == 5 ? 16 : 64);
-  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && !ws && !f32)  // 64-deep K steps
+  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && !f32)  // 64-deep K steps
     for (size_t s = 0; s < segs.size(); ++s)
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: 64-deep-K tiles need segment channels % 64 == 0");
-  if (!ws) {
-    TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
-                "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
-    TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == (f32 ? 2 : 1) * Ktot,
-                "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
-    TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
-                "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
-  }
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
+              "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
+  TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == (f32 ? 2 : 1) * Ktot,
+              "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
+  TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
+              "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
   if (bias) {
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() >= Cout &&
                     bias->is_contiguous(),
@@ -274,7 +227,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   L.w_bytes = (unsigned)(w.numel() * 2);
   L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.B = B; L.H = H; L.W = W; L.KH = KH; L.KW = KW; L.PH = KH / 2; L.PW = KW / 2;
-  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = ws ? Ktot : w.size(2);  // weight row length
+  L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = w.size(2);  // weight row length
   L.epi = epi; L.scale = scale; L.hd = hd; L.tile = tile;
   if (epi == EPI_FLOW) {
     TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kFloat && out.dim() == 4 &&
@@ -326,23 +279,9 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
   if (nx.stats || nx.chs)
-    TORCH_CHECK(!ws && !(tile >= 42 && tile <= 47),
-                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-48)");
+    TORCH_CHECK(!(tile >= 42 && tile <= 47),
+                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-47)");
   L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
-  if (ws) {
-    ws_setup(L, w, ws_cfg, Ktot);
-    // the weight-stationary epilogues use vector accesses only (conv_ws.h ws_pre / ws_fin)
-    TORCH_CHECK(epi != EPI_FLOW, "conv_ws: EPI_FLOW is not supported");
-    TORCH_CHECK(!(bias && (epi == EPI_ACC_F32 || epi == EPI_GRU_QBWD)), "conv_ws: accumulating epilogues take no bias");
-    TORCH_CHECK(!bias || bias->numel() >= (Cout + 3) / 4 * 4, "conv_ws: bias must hold round_up(Cout, 4) values");
-    TORCH_CHECK(Cout % 4 == 0 || epi == 0 || epi == 1 || epi == 2,
-                "conv_ws: Cout % 4 == 0 required except for the bias / ReLU / scale epilogues");
-    const int offs = L.ooff | L.ostr | L.o2off | L.o2str | L.o3off | L.o3str | L.a1off | L.a1str | L.a2off | L.a2str;
-    const uintptr_t ptrs = (uintptr_t)L.out | (uintptr_t)L.out2 | (uintptr_t)L.out3 | (uintptr_t)L.aux1 |
-                           (uintptr_t)L.aux2 | (uintptr_t)L.bias;
-    TORCH_CHECK((offs & 3) == 0 && (ptrs & 15) == 0,
-                "conv_ws: epilogue tensors need 16-B aligned bases and channel offsets / strides % 4 == 0");
-  }
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();
 }
@@ -354,23 +293,9 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
                 int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
                 const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile,
                 const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale) {
-  TORCH_CHECK(tile != rs::kWsTile, "conv_fused: the weight-stationary kernel is conv_ws");
   const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, segs.at(0).size(0), Cout, "conv_fused");
   conv_impl(segs, seg_off, seg_C, w, bias, KH, KW, Cout, epi, scale, hd, out, ooff, out2, o2off, out3, o3off,
-            aux1, a1off, aux2, a2off, tile, {}, nx);
-}
-
-// torch.ops.raft_stir.conv_ws: the same convolution + epilogue contract as
-// conv_fused, on the weight-stationary kernel; wf = fragment-packed weights
-// (ops/conv.py frag_layout), cfg = [G, NB, ncs, ncb, rows_per_chunk].
-void conv_ws(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C,
-             const Tensor& wf, const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t Cout,
-             int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
-             const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
-             int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
-             const c10::optional<Tensor>& aux2, int64_t a2off, at::IntArrayRef cfg) {
-  conv_impl(segs, seg_off, seg_C, wf, bias, KH, KW, Cout, epi, scale, hd, out, ooff, out2, o2off, out3, o3off,
-            aux1, a1off, aux2, a2off, rs::kWsTile, cfg);
+            aux1, a1off, aux2, a2off, tile, nx);
 }
 
 // convf1 of the motion encoder from coords1 (flow = coords1 - grid), ReLU, bf16
@@ -837,9 +762,6 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
         "Tensor(d!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None) -> ()");
-  m.def("conv_ws(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor wf, Tensor? bias, int KH, int KW, "
-        "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
-        "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int[] cfg) -> ()");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
         "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
         "int OOX, int tile, Tensor(b!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None, "
@@ -850,7 +772,6 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
-  m.impl("conv_ws", &conv_ws);
   m.impl("conv3x3_halo", &conv3x3_halo);
   m.impl("stem_conv", &stem_conv);
   m.impl("stem_wgrad", &stem_wgrad);

@@ -137,132 +137,20 @@ def tuned_tiles() -> dict:
     return _TUNED
 
 
-# ---------------------------------------------------------------- weight-stationary kernel
-# csrc/conv_ws.hip: the weights of a wave's 32 output channels x (taps x Ktot /
-# ncs) input channels stay in VGPRs for the whole launch; the block walks a
-# 16-column strip down the image through an LDS ring of halo rows.
-WS_TILE = 48
-_G1, _G3, _GS = (4, 6, 8, 12, 16, 18, 24), (1, 2, 3, 4), (2, 4, 6)
-# instantiated (KH, KW) -> G per epilogue class (csrc/conv_ws_<class>.hip)
-WS_INST = {
-    "plain": {(1, 1): _G1, (3, 3): _G3},
-    "zr": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
-    "q": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
-    "relubwd": {(1, 1): _G1, (3, 3): _G3},
-    "acc": {(1, 1): _G1, (3, 3): _G3, (1, 5): _GS, (5, 1): _GS},
-    "qbwd": {(1, 5): _GS, (5, 1): _GS, (3, 3): _G3},
-}
-
-
-def ws_class(epi: int):
-    return {EPI_GRU_ZR: "zr", EPI_GRU_Q: "q", EPI_RELU_BWD: "relubwd", EPI_ACC_F32: "acc",
-            EPI_GRU_QBWD: "qbwd", EPI_FLOW: None, EPI_NORM: None}.get(epi, "plain")
-
-
-WS_G = {k: v for d in WS_INST.values() for k, v in d.items()}  # union (tests)
-_WS = os.environ.get("RS_CONV_WS", "1") != "0"
-_NUM_CUS = 256
-
-
-def frag_layout(w: torch.Tensor) -> torch.Tensor:
-    """[Cout_pad][taps][Ktot] packed weights (or index maps) -> the
-    weight-stationary kernel's fragment order, same shape: element
-    (cob, tap, kg, lane, j) = W[32 cob + lane % 32][tap][16 kg + 8 (lane // 32) + j],
-    i.e. one v_mfma_f32_32x32x16_bf16 A fragment = 1 KiB contiguous."""
-    cp, taps, k = w.shape
-    assert cp % 32 == 0 and k % 16 == 0, (cp, k)
-    return w.reshape(cp // 32, 32, taps, k // 16, 2, 8).permute(0, 2, 3, 4, 1, 5).reshape(cp, taps, k).contiguous()
-
-
-def ws_geometry(kh: int, kw: int, G: int, ncs: int = 4, ncb: int = 1, NB: int = 1):
-    """(ring-row slots, LDS slots, halo pieces per MFMA wave per tile) -- the
-    checks of ops_conv.cpp ws_setup; None if the configuration does not fit."""
-    TH, hwd, cs = 2 * NB, 16 + kw - 1, 2 * G + 1
-    rsp = (ncs * hwd * cs + 63) // 64 * 64
-    slots = (2 * TH + kh - 1) * rsp + 2 * ncs * 4 * 64
-    ppw = -(-(TH * rsp // 64) // ncs)
-    if slots > 10240 or ppw > 10 or ncs != 4 or ncb != 1 or NB != 1 or kh * kw * G > 40:
-        return None
-    return rsp, slots, ppw
-
-
-def ws_rows_per_chunk(B: int, H: int, W: int, cout: int, target: int = _NUM_CUS) -> int:
-    """Rows per block so that the grid is ~one block per CU (blocks =
-    ceil(cout/32) x B x ceil(W/16) x ceil(H/rpc)); even (2-row tiles)."""
-    base = -(-cout // 32) * B * (-(-W // 16))
-    nrch = max(1, target // base)
-    rpc = -(-H // nrch)
-    return rpc + (rpc & 1)
-
-
-_WS_CFG: dict = {}
-
-
-def ws_config(B: int, H: int, W: int, cout: int, ktot: int, kh: int, kw: int, cout_pad: int, epi: int = EPI_BIAS):
-    """[G, NB, ncs, ncb, rows_per_chunk] for conv_ws, or None (no instantiated fit)."""
-    cls = ws_class(epi)
-    if cls is None or ktot % 64:
-        return None
-    key = (B, H, W, cout, ktot, kh, kw, cout_pad, cls)
-    if key in _WS_CFG:
-        return _WS_CFG[key]
-    G = ktot // 64
-    cfg = None
-    if G in WS_INST[cls].get((kh, kw), ()) and ws_geometry(kh, kw, G) is not None and -(-cout // 32) * 32 <= cout_pad:
-        tuned = tuned_ws().get(f"{B}x{H}x{W}|{cout}|{ktot}|{kh}x{kw}")
-        rpc = int(tuned[4]) if tuned is not None else ws_rows_per_chunk(B, H, W, cout)
-        cfg = [G, 1, 4, 1, rpc]
-    _WS_CFG[key] = cfg
-    return cfg
-
-
-_TUNED_WS: dict | None = None
-
-
-def tuned_ws() -> dict:
-    global _TUNED_WS
-    if _TUNED_WS is None:
-        _TUNED_WS = {}
-        if os.environ.get("RS_CONV_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
-            import json
-            with open(_TUNED_PATH) as f:
-                _TUNED_WS = {k: list(v) for k, v in json.load(f).get("ws", {}).items()}
-    return _TUNED_WS
-
-
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=None, wf=None, ws_cfg=None, stats=None, stats_per_sample=False,
-               nscale=None):
+               aux2=None, a2off=0, tile=None, stats=None, stats_per_sample=False, nscale=None):
     """segs: list of (NHWC bf16 buffer, channel offset, channels read).
-    ``wf``: the same weights in frag_layout -- the weight-stationary kernel runs
-    when it has an instantiated configuration for the shape (unless ``tile``
-    forces a tile kernel or RS_CONV_WS=0).
     ``stats`` (fp32 [G][cout][2]): the epilogue adds each channel's (sum, sum of
     squares) of the output (ops/norm.py); ``nscale`` with ``epi=EPI_NORM``:
-    out = [relu if hd](acc * nscale + bias) [then relu(. + aux1)].  Both run on
-    the tile kernels only."""
+    out = [relu if hd](acc * nscale + bias) [then relu(. + aux1)]."""
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
     if _RECORD is not None:
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
-                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, wf=wf, ws_cfg=ws_cfg))
-    if wf is not None and stats is None and nscale is None and (tile == WS_TILE or (tile is None and _WS)):
-        t0 = tensors[0]
-        cfg = ws_cfg if ws_cfg is not None else ws_config(t0.shape[0], t0.shape[1], t0.shape[2], cout, sum(chans),
-                                                          kh, kw, wf.shape[0], epi)
-        if cfg is not None:
-            if bias is not None and (bias.numel() % 4 or bias.data_ptr() % 16):
-                # the kernel reads the bias in aligned 4-channel vectors (the engines
-                # hand it padded, aligned biases; this copy is the slow path)
-                bias = pack_bias(bias, pad_to(bias.numel(), 4)).clone()
-            torch.ops.raft_stir.conv_ws(tensors, offs, chans, wf, bias, kh, kw, cout, epi, float(scale), hd,
-                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, list(cfg))
-            return
-        if tile == WS_TILE:
-            raise ValueError(f"conv_ws: no configuration for {tuple(t0.shape)} cout={cout} K={sum(chans)} {kh}x{kw}")
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile))
     if tile is None:
         t0 = tensors[0]
         tile = tuned_tiles().get(tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi))

@@ -104,7 +104,12 @@ def _hip_ok(norm, x, residual):
 # and zeroes the buffer again (torch.ops.raft_stir.norm_finalize): no
 # separate reduction pass over the activation.  The fp32 atomics make the
 # sums order-dependent, so deterministic mode keeps the two-level reduction.
-_FUSED_STATS = os.environ.get("RS_NORM_FUSED_STATS", "1") != "0"
+# Opt-in (RS_NORM_FUSED_STATS=1): measured SLOWER in situ -- the statistics
+# epilogue raises the halo / tile kernels' register use and contends on the
+# per-channel atomics (enc_halo 64->64: 115 -> 209 us per training call);
+# paired bench, round 3: 381 vs 368 pairs/s, 279 vs 269 FPS
+# (profiles/r3/README.md).  The two-level reduction is the default.
+_FUSED_STATS = os.environ.get("RS_NORM_FUSED_STATS", "0") == "1"
 
 
 def _deterministic() -> bool:

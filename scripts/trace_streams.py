@@ -10,6 +10,8 @@ import csv
 import gzip
 import sys
 
+TOP = 25
+
 
 def main(path):
     op = gzip.open if path.endswith(".gz") else open
@@ -54,6 +56,18 @@ def main(path):
     print(f"main-queue gaps > 100 us: {len(gaps)}, {sum(g[1] for g in gaps):.3f} ms")
     for g in gaps:
         print(f"  at {g[0]:7.3f} ms: {g[1]:6.3f} ms idle, then {g[2]}")
+    # per-queue kernel families (template arguments kept: tiles differ)
+    for q in sorted(byq, key=byq.get, reverse=True):
+        fam, n = collections.defaultdict(float), collections.Counter()
+        for r in step:
+            if r["Queue_Id"] == q:
+                s, e = T(r)
+                k = r["Kernel_Name"].replace("void ", "").split("(")[0][:70]
+                fam[k] += (e - s) / 1e6
+                n[k] += 1
+        print(f"queue {q} top kernels:")
+        for k in sorted(fam, key=fam.get, reverse=True)[:TOP]:
+            print(f"  {fam[k]:7.3f} ms {n[k]:4d}x  {k}")
 
 
 if __name__ == "__main__":

@@ -142,7 +142,7 @@ def _encoder(norm_fn, cuda, seed=7):
 
 
 def _run(enc, x, fused, train, bf16=True):
-    N._FUSED_STATS = fused
+    prev, N._FUSED_STATS = N._FUSED_STATS, fused
     try:
         enc.zero_grad(set_to_none=True)
         enc.train(train)
@@ -150,7 +150,7 @@ def _run(enc, x, fused, train, bf16=True):
             y = enc(x)
         y.float().square().mean().backward()
     finally:
-        N._FUSED_STATS = True
+        N._FUSED_STATS = prev
     return y.detach().float(), {n: p.grad.detach().clone() for n, p in enc.named_parameters() if p.grad is not None}
 
 
