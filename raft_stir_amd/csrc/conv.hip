@@ -430,10 +430,20 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(Args a) {
 // thread count, the last B staging instruction of the surplus waves is a
 // zero-fill of a 1 KiB pad (every wave issues the same number of loads, so
 // the vmcnt bookkeeping stays uniform).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N;
+//
+// KG > 1: intra-block split-K for small grids (batch-1 inference: 7480 pixels,
+// ~470 64x64 tiles for 256 CUs, < 2 waves per SIMD, every K step waits on
+// L2 latency).  The block holds KG groups of WAVES_M x WAVES_N waves over the
+// SAME output tile; group g stages and multiplies K steps g, g + KG, ... into
+// its own slice of each stage buffer, so KG x as many waves and loads are in
+// flight per tile and the serial K loop is KG x shorter.  At the end groups
+// 1..KG-1 park their accumulators in LDS and group 0 sums them (fixed order)
+// and runs the epilogue.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int STAGES, int KG = 1>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N * KG) void conv_buf_kernel(Args a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;  // threads per K group
   static_assert(NT == 256 || NT == 512, "4 or 8 waves");
+  static_assert(KG == 1 || KG == 2 || KG == 4, "KG");
   static_assert(STAGES >= 2 && STAGES <= 4, "STAGES");
   constexpr int BK = 64, CPR = 8, RB = 128;
   static_assert(BM % (WAVES_M * 16) == 0 && BN % (WAVES_N * 16) == 0, "wave tiles");
@@ -445,9 +455,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
   constexpr int PAD = BPART ? 64 : 0;
   constexpr int NLD = NA + NB;
   constexpr int kFar = 0x7ffffff0;  // past every buffer: reads as zero
-  __shared__ uint4 lds[STAGES][(BM + BN) * CPR + PAD];
+  constexpr int GSLOT = (BM + BN) * CPR + PAD;  // uint4 slots of one K group's slice of a stage
+  __shared__ uint4 lds[STAGES][KG * GSLOT];
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int kg = KG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT);
+  const int t = threadIdx.x - kg * NT, lane = t & 63, wave = t >> 6;  // within the K group
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
   const int nct = cdiv(a.Cout, BM);
   const int lid = a.xcd_remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -498,32 +510,43 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
   const int e1 = taps * (s0.C >> 6);
   const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> 6) : 0);
   const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> 6) : 0);
+  const int nst = (nsteps + KG - 1) / KG;  // stages; stage s holds K steps s * KG + (0 .. KG-1)
 
-  // scalar walk of the K steps: segment si, tap (ty, tx), channel chunk c0
-  int si = 0, tap = 0, ty = 0, tx = 0, c0 = 0, kseg = 0;
-  // (a macro, not a lambda: capturing the staging arrays by reference would
-  // take their address and move them to scratch)
-#define RS_BISSUE(BUF)                                                                          \
+  // scalar walk of this group's K steps: segment si, tap (ty, tx), channel chunk c0
+  int si = 0, tap = 0, ty = 0, tx = 0, c0 = 0, kseg = 0, kstep = 0;
+#define RS_BADV()                                                                               \
   do {                                                                                          \
-    const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                    \
-    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
-    const __amdgpu_buffer_rsrc_t rb = si == 0 ? rs0 : (si == 1 ? rs1 : rs2);                    \
-    uint4* dst = lds[BUF];                                                                      \
-    const int asoff = (tap * Ktot + kseg + c0) * 2;                                             \
-    _Pragma("unroll") for (int i = 0; i < NA; ++i) bdma16(rw, dst + wbase + NT * i, aoff[i], asoff); \
-    const int tsh = ty * W + tx;                                                                \
-    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
-      const int v = ((bmask[i] >> tap) & 1u) ? ((bpix[i] + tsh) * sst + c0 + bch[i]) * 2 : kFar; \
-      const bool pad = BPART && i == NB - 1 && wbase + NT * i >= NBC;                           \
-      bdma16(rb, dst + BM * CPR + (pad ? NBC : wbase + NT * i), v, 0);                          \
-    }                                                                                           \
-    c0 += BK; /* advance to the next K step */                                                  \
-    if (c0 == sC) {                                                                             \
+    const int sC_ = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                   \
+    ++kstep;                                                                                    \
+    c0 += BK;                                                                                   \
+    if (c0 == sC_) {                                                                            \
       c0 = 0;                                                                                   \
       ++tap;                                                                                    \
       if (++tx == KW) { tx = 0; ++ty; }                                                         \
-      if (tap == taps) { tap = 0; ty = 0; kseg += sC; ++si; }                                   \
+      if (tap == taps) { tap = 0; ty = 0; kseg += sC_; ++si; }                                  \
     }                                                                                           \
+  } while (0)
+  for (int g = 0; g < kg; ++g) RS_BADV();
+  // (a macro, not a lambda: capturing the staging arrays by reference would
+  // take their address and move them to scratch).  A K step past the end
+  // (the last stage of a split walk) stages zeros: every wave still issues
+  // NLD loads per stage, so the vmcnt bookkeeping stays uniform.
+#define RS_BISSUE(BUF)                                                                          \
+  do {                                                                                          \
+    const bool live_ = kstep < nsteps;                                                          \
+    const int sst = si == 0 ? s0.stride : (si == 1 ? s1.stride : s2.stride);                    \
+    const __amdgpu_buffer_rsrc_t rb = si == 0 ? rs0 : (si == 1 ? rs1 : rs2);                    \
+    uint4* dst = lds[BUF] + kg * GSLOT;                                                         \
+    const int asoff = live_ ? (tap * Ktot + kseg + c0) * 2 : 0;                                 \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                              \
+      bdma16(rw, dst + wbase + NT * i, live_ ? aoff[i] : kFar, asoff);                          \
+    const int tsh = ty * W + tx;                                                                \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int v = (live_ && ((bmask[i] >> tap) & 1u)) ? ((bpix[i] + tsh) * sst + c0 + bch[i]) * 2 : kFar; \
+      const bool pad = BPART && i == NB - 1 && wbase + NT * i >= NBC;                           \
+      bdma16(rb, dst + BM * CPR + (pad ? NBC : wbase + NT * i), v, 0);                          \
+    }                                                                                           \
+    _Pragma("unroll") for (int g_ = 0; g_ < KG; ++g_) RS_BADV(); /* this group's next K step */ \
   } while (0)
 
 
@@ -534,8 +557,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lc = lane >> 4;
-  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
-  constexpr uint32_t kStage = (BM + BN) * RB + PAD * 16;
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0][0] + kg * GSLOT * 16;
+  constexpr uint32_t kStage = KG * GSLOT * 16;
   uint32_t abase[2], bbase[2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
@@ -544,11 +567,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
   }
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nsteps) RS_BISSUE(s);
+    if (s < nst) RS_BISSUE(s);
   int buf = 0;
-  for (int step = 0; step < nsteps; ++step) {
+  for (int step = 0; step < nst; ++step) {
     // retire this step's copies; keep up to STAGES-2 later steps in flight
-    const int ahead = min(STAGES - 2, nsteps - 1 - step);
+    const int ahead = min(STAGES - 2, nst - 1 - step);
     if (STAGES >= 4 && ahead >= 2) wait_vmcnt<2 * NLD>();
     else if (STAGES >= 3 && ahead >= 1) wait_vmcnt<NLD>();
     else wait_vmcnt<0>();
@@ -566,7 +589,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[kk][nt]) : "v"(bbase[kk] + so), "i"(nt * 16 * RB)
                      : "memory");
     }
-    if (step + STAGES - 1 < nsteps) RS_BISSUE(buf == 0 ? STAGES - 1 : buf - 1);
+    if (step + STAGES - 1 < nst) RS_BISSUE(buf == 0 ? STAGES - 1 : buf - 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -588,6 +611,34 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void conv_buf_kernel(Args a
   }
 
 #undef RS_BISSUE
+#undef RS_BADV
+  if constexpr (KG > 1) {
+    // groups 1.. park their partial tiles in the (now free) stage buffers,
+    // lane-linear per accumulator element; group 0 adds them in group order
+    constexpr int NE = WM * WN * 4;  // accumulator floats per lane
+    static_assert((KG - 1) * NE * NT * 4 <= STAGES * KG * GSLOT * 16, "split-K reduction buffer");
+    float* red = reinterpret_cast<float*>(&lds[0][0]);
+    __syncthreads();  // every wave is done with the stage buffers
+    if (kg > 0) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            red[((size_t)((kg - 1) * NE + (mt * WN + nt) * 4 + j) * NT) + t] = acc[mt][nt][j];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+#pragma unroll
+    for (int g = 0; g < KG - 1; ++g)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt][nt][j] += red[((size_t)(g * NE + (mt * WN + nt) * 4 + j) * NT) + t];
+  }
 
   int pb[WN], py[WN], px[WN];
 #pragma unroll
@@ -1043,7 +1094,16 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
         case 30: RS_BUF8(256, 96, 2); break;
         case 31: RS_BUF8(128, 96, 2); break;
         case 32: RS_BUF8(256, 192, 2); break;
-        default: RS_BUF8(128, 192, 2); break;  // 33
+        case 33: RS_BUF8(128, 192, 2); break;
+#define RS_BUFK(BM_, BN_, ST_, KG_)                                                                  \
+  hipLaunchKernelGGL((conv::conv_buf_kernel<BM_, BN_, 2, 2, ST_, KG_>),                                \
+                     dim3(cdiv(a.P, BN_) * cdiv(L.Cout, BM_)), dim3(256 * KG_), 0, stream, a)
+        // intra-block split-K tiles for small grids (batch-1 inference)
+        case 34: RS_BUFK(64, 64, 2, 2); break;
+        case 35: RS_BUFK(64, 64, 3, 2); break;
+        case 36: RS_BUFK(128, 64, 2, 2); break;
+        default: RS_BUFK(64, 64, 2, 4); break;  // 37
+#undef RS_BUFK
 #undef RS_BUF8
 #undef RS_BUF
       }

@@ -38,6 +38,18 @@ struct ConvLaunch {
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
+struct EncWgradLaunch {
+  const void* x;
+  const void* dy;
+  int xstr, ystr;
+  long x_bytes, dy_bytes;
+  int B, H, W, Cin, Cout;
+  float* part;
+  float* dw;
+  int nsplit, tpb;
+};
+int enc_wgrad_splits(int B, int H, int W, int Cin, int Cout, int* tpb);
+void enc_wgrad_launch(const EncWgradLaunch& L, hipStream_t stream);
 void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, const float* bias,
                      int Cout, void* out, int ostr, int ooff, void* fout, int fstr, int foff, bool f32,
                      hipStream_t stream);
@@ -195,14 +207,15 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   if (tile >= 42 && tile <= 47)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
-  TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-33) support at most 32 taps");
+  TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
+  TORCH_CHECK(!(tile >= 38 && tile <= 41), "conv_fused: tiles 38-41 do not exist");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
   if (tile >= 24 && tile <= 26) {  // halo tiles: the (TH+KH-1) x (16+KW-1) halo must fit the LDS buffer
     const int TH = tile == 26 ? 4 : 8, HCAP = tile == 26 ? 128 : 192;
     TORCH_CHECK((TH + KH - 1) * (16 + KW - 1) <= HCAP, "conv_fused: kernel too large for halo tile ", tile);
   }
   const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13) || tile == 16 ||
-                     tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26;
+                     tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26 || tile == 36;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
   const int tileM = (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
                     : tile == 0 ? 32
@@ -551,6 +564,46 @@ void conv_wgrad_strided(const Tensor& dy, int64_t Cout, const std::vector<Tensor
   conv_wgrad_impl(dy, 0, Cout, segs, seg_off, seg_C, per, KH, KW, dw, db, 0, SY, SX);
 }
 
+// Weight gradient of a stride-1 / pad-1 3x3 convolution on csrc/enc_wgrad.hip
+// (halo tiles, all nine taps per block, deterministic partial reduction).
+//   dy : NHWC bf16 [B, H, W, Cout] view (channels contiguous, pixels dense)
+//   x  : NHWC bf16 [B, H, W, Cin] view
+// returns dW fp32 [Cout, Cin, 3, 3] (the parameter layout)
+static void check_nhwc_view(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.scalar_type() == at::kBFloat16, n, ": bf16 NHWC GPU tensor");
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) >= t.size(3) && t.stride(2) % 8 == 0 &&
+                  t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1),
+              n, ": dense NHWC pixels with a channel stride % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, ": 16-B aligned base");
+  TORCH_CHECK(t.numel() / t.size(3) * t.stride(2) * 2 < (int64_t(1) << 31), n, ": too large for 32-bit offsets");
+}
+
+Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
+  check_nhwc_view(dy, "enc_wgrad dy");
+  check_nhwc_view(x, "enc_wgrad x");
+  const int B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = dy.size(3);
+  TORCH_CHECK(dy.size(0) == B && dy.size(1) == H && dy.size(2) == W, "enc_wgrad: dy / x shapes");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Cin <= 512 && Cout <= 512,
+              "enc_wgrad: channel counts must be multiples of 64");
+  const c10::DeviceGuard guard(x.device());
+  rs::EncWgradLaunch L{};
+  L.x = x.data_ptr();
+  L.dy = dy.data_ptr();
+  L.xstr = x.stride(2);
+  L.ystr = dy.stride(2);
+  L.x_bytes = (long)B * H * W * L.xstr * 2;
+  L.dy_bytes = (long)B * H * W * L.ystr * 2;
+  L.B = B; L.H = H; L.W = W; L.Cin = Cin; L.Cout = Cout;
+  L.nsplit = rs::enc_wgrad_splits(B, H, W, Cin, Cout, &L.tpb);
+  Tensor part = at::empty({int64_t(L.nsplit) * Cout * 9 * Cin}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(at::kFloat));
+  L.part = part.data_ptr<float>();
+  L.dw = dw.data_ptr<float>();
+  rs::enc_wgrad_launch(L, stream());
+  RS_CHECK_LAUNCH();
+  return dw;
+}
+
 void colsum(const Tensor& dy, int64_t yoff, int64_t C, const Tensor& db) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.scalar_type() == at::kBFloat16, "colsum: bf16 dy");
   TORCH_CHECK(yoff >= 0 && yoff + C <= dy.size(-1), "colsum: channel window");
@@ -762,6 +815,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
         "Tensor(d!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None) -> ()");
+  m.def("enc_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
         "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
         "int OOX, int tile, Tensor(b!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None, "
@@ -773,6 +827,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("conv3x3_halo", &conv3x3_halo);
+  m.impl("enc_wgrad", &enc_wgrad);
   m.impl("stem_conv", &stem_conv);
   m.impl("stem_wgrad", &stem_wgrad);
   m.impl("conv_geo", &conv_geo);

@@ -211,7 +211,18 @@ class _Conv3x3(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+# csrc/enc_wgrad.hip: all nine taps of a 64 x 64 channel slice per block over
+# halo tiles (deterministic); 64 / 128-channel convs (layer1, layer3)
+_ENC_WGRAD = os.environ.get("RS_ENC_WGRAD", "1") != "0"
+
+
+def _enc_wgrad_op(dy, x):
+    return torch.ops.raft_stir.enc_wgrad(dy, x)
+
+
 def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
+    if _ENC_WGRAD and cin % 64 == 0 and cout % 64 == 0:
+        return _enc_wgrad_op(dyn, xn).to(weight.dtype)
     if _wgrad_covers(cin, cout):
         # the kernel tiles input channels in 64-wide segments: an odd
         # multiple of 32 (96) is covered by two OVERLAPPING segments,

@@ -8,6 +8,8 @@ repeated here.
   4  KITTI 1242x375, on-the-fly correlation (alt_cuda_corr path), bf16
   5  STIR point tracker (RAFT-small, 12 iters, 1x3x512x640, 32 query points):
      graphed serving latency, plus TorchScript export + parity check
+  6  config 2 in fp32 (the reference's default eval / export precision)
+  7  config 5's served latency in bf16 (mixed precision)
 
     python scripts/bench_configs.py [--only 2 4] [--out profiles/bench_configs.jsonl]
 """
@@ -50,11 +52,11 @@ def cfg1():
             "threads": torch.get_num_threads()}
 
 
-def _infer(size, alt, iters, reps):
+def _infer(size, alt, iters, reps, bf16=True):
     from raft_stir_amd.runtime.graph import GraphedInference
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    m = RAFT(make_args(mixed_precision=True, alternate_corr=alt)).to(dev)
+    m = RAFT(make_args(mixed_precision=bf16, alternate_corr=alt)).to(dev)
     m = m.to(memory_format=torch.channels_last).eval()
     h, w = size
     i1 = torch.rand(1, 3, h, w, device=dev) * 255
@@ -79,6 +81,26 @@ def cfg4():
         out["on_the_fly" if alt else "all_pairs"] = {"fps": round(1 / dt, 2), "ms_per_pair": round(dt * 1e3, 3),
                                                      "peak_mem_mib": round(mem), "padded": padded}
     return out
+
+
+def cfg6():
+    dt, mem, padded = _infer((436, 1088), False, 12, 30, bf16=False)
+    return {"config": "raft full 12-iter inference 1088x436, fp32, hipGraph", "fps": round(1 / dt, 2),
+            "ms_per_pair": round(dt * 1e3, 3), "padded": padded, "peak_mem_mib": round(mem)}
+
+
+def cfg7():
+    from raft_stir_amd.export.pointtrack import PointTrackServer
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m = RAFT(make_args(small=True, mixed_precision=True)).to(dev).eval()
+    i1 = torch.rand(1, 3, 512, 640, device=dev) * 255
+    i2 = torch.rand(1, 3, 512, 640, device=dev) * 255
+    pts = torch.rand(1, 32, 2, device=dev) * 500
+    srv = PointTrackServer(m, iters=12)
+    dt = _time(lambda: srv(pts, i1, i2), 50, torch.cuda.synchronize)
+    return {"config": "STIR point tracker raft-small 12 iters 1x3x512x640, 32 points, bf16",
+            "served_ms": round(dt * 1e3, 3), "served_fps": round(1 / dt, 1)}
 
 
 def cfg5():
@@ -109,10 +131,10 @@ def cfg5():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", type=int, nargs="+", default=[1, 2, 4, 5])
+    ap.add_argument("--only", type=int, nargs="+", default=[1, 2, 4, 5, 6, 7])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    fns = {1: cfg1, 2: cfg2, 4: cfg4, 5: cfg5}
+    fns = {1: cfg1, 2: cfg2, 4: cfg4, 5: cfg5, 6: cfg6, 7: cfg7}
     lines = []
     for k in a.only:
         r = {"id": k, **fns[k]()}

@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 42, 43, 44, 45, 46]
+CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 42, 43,
+              44, 45, 46]
 
 
 def record_calls(args):
