@@ -28,7 +28,10 @@
 //    per K step against 4 + 18 transposed reads, two waves per SIMD.
 // Each block writes its partial dW tile (plain stores); enc_wgrad_reduce sums
 // the partials in block order into the weight's own [Cout][Cin][3][3] layout:
-// deterministic, no atomics.
+// deterministic, no atomics.  Channel counts that are an odd multiple of 32
+// (layer2's 96) are covered by two OVERLAPPING 64-channel blocks, [0, 64) and
+// [C - 64, C); the reduction takes each channel from the first block that
+// holds it.
 #include "common.h"
 
 namespace rs {
@@ -54,8 +57,8 @@ struct WArgs {
   unsigned x_bytes, dy_bytes;
   int B, H, W, Cin, Cout;
   int tiles_w, tiles_img, ntiles, tpb;  // tiles per block (contiguous range)
-  int ncb, nib;                         // output / input channel blocks (64 each)
-  float* part;                          // [nsplit][Cout][9][Cin]
+  int ncb, nib;                         // output / input channel blocks (64 each, last one at C - 64)
+  float* part;                          // [nsplit][ncb][nib][64 co][9][64 ci]
 };
 
 __device__ __forceinline__ int swz(int row) { return ((row & 3) ^ ((row >> 3) & 1)) << 1; }
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(NT) void enc_wgrad_kernel(WArgs a) {
   const int nw = wave & 3, mh = wave >> 2;
   const int bid = blockIdx.x;
   const int cb = bid % a.ncb, ib = (bid / a.ncb) % a.nib, split = bid / (a.ncb * a.nib);
-  const int co0 = cb * 64, ci0 = ib * 64;
+  const int co0 = min(cb * 64, a.Cout - 64), ci0 = min(ib * 64, a.Cin - 64);
   int tile = split * a.tpb;
   const int tend = min(a.ntiles, tile + a.tpb);  // host: every split has >= 1 tile
 
@@ -209,28 +212,32 @@ __global__ __launch_bounds__(NT) void enc_wgrad_kernel(WArgs a) {
   }
 
   // partial tile: C[co][ci] of tap k, co = co0 + 16 (2 mh + m) + 4 g + j, ci = ci0 + 16 nw + (lane & 15)
-  float* o = a.part + (size_t)split * a.Cout * 9 * a.Cin;
-  const int ci = ci0 + 16 * nw + (lane & 15);
+  float* o = a.part + (size_t)((split * a.ncb + cb) * a.nib + ib) * (64 * 9 * 64);
+  const int ci = 16 * nw + (lane & 15);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int co = co0 + 16 * (2 * mh + m) + 4 * g + j;
+      const int co = 16 * (2 * mh + m) + 4 * g + j;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) o[((size_t)co * 9 + k) * a.Cin + ci] = acc[m][k][j];
+      for (int k = 0; k < 9; ++k) o[(co * 9 + k) * 64 + ci] = acc[m][k][j];
     }
 }
 
-// dw[co][ci][ky][kx] = sum over splits (in order) of part[s][co][ky*3+kx][ci];
-// threads walk the partial layout (ci fastest: coalesced reads)
+// dw[co][ci][ky][kx] = sum over splits (in order) of the partial of the block
+// holding (co, ci); threads walk (co, tap, ci), ci fastest (coalesced reads)
 __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit, int Cout,
                                                                int Cin, float* __restrict__ dw) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n = Cout * 9 * Cin;
-  if (i >= n) return;
+  if (i >= Cout * 9 * Cin) return;
   const int ci = i % Cin, r = i / Cin, k = r % 9, co = r / 9;
+  const int ncb = (Cout + 63) / 64, nib = (Cin + 63) / 64;
+  const int cb = min(co / 64, ncb - 1), ib = min(ci / 64, nib - 1);
+  const int col = co - min(cb * 64, Cout - 64), cil = ci - min(ib * 64, Cin - 64);
+  const size_t blk = (size_t)ncb * nib * (64 * 9 * 64);
+  const float* p = part + (size_t)(cb * nib + ib) * (64 * 9 * 64) + (col * 9 + k) * 64 + cil;
   float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += part[(size_t)sp * n + i];
+  for (int sp = 0; sp < nsplit; ++sp) s += p[sp * blk];
   dw[((size_t)co * Cin + ci) * 9 + k] = s;
 }
 
@@ -250,7 +257,7 @@ struct EncWgradLaunch {
 
 int enc_wgrad_splits(int B, int H, int W, int Cin, int Cout, int* tpb) {
   const int ntiles = B * cdiv(H, encw::TH) * cdiv(W, encw::TW);
-  const int chan = (Cout / 64) * (Cin / 64);
+  const int chan = cdiv(Cout, 64) * cdiv(Cin, 64);
   int want = 256 / chan;  // ~one block per CU
   if (want < 1) want = 1;
   *tpb = cdiv(ntiles, want);
@@ -270,8 +277,8 @@ void enc_wgrad_launch(const EncWgradLaunch& L, hipStream_t stream) {
   a.tiles_img = a.tiles_w * cdiv(L.H, encw::TH);
   a.ntiles = L.B * a.tiles_img;
   a.tpb = L.tpb;
-  a.ncb = L.Cout / 64;
-  a.nib = L.Cin / 64;
+  a.ncb = cdiv(L.Cout, 64);
+  a.nib = cdiv(L.Cin, 64);
   a.part = L.part;
   hipLaunchKernelGGL(encw::enc_wgrad_kernel, dim3(L.nsplit * a.ncb * a.nib), dim3(encw::NT), 0, stream, a);
   const int n = L.Cout * 9 * L.Cin;

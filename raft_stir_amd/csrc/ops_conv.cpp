@@ -583,8 +583,8 @@ Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
   check_nhwc_view(x, "enc_wgrad x");
   const int B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = dy.size(3);
   TORCH_CHECK(dy.size(0) == B && dy.size(1) == H && dy.size(2) == W, "enc_wgrad: dy / x shapes");
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && Cin <= 512 && Cout <= 512,
-              "enc_wgrad: channel counts must be multiples of 64");
+  TORCH_CHECK(Cin % 32 == 0 && Cout % 32 == 0 && Cin >= 64 && Cout >= 64 && Cin <= 512 && Cout <= 512,
+              "enc_wgrad: channel counts must be multiples of 32, >= 64");
   const c10::DeviceGuard guard(x.device());
   rs::EncWgradLaunch L{};
   L.x = x.data_ptr();
@@ -595,7 +595,8 @@ Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
   L.dy_bytes = (long)B * H * W * L.ystr * 2;
   L.B = B; L.H = H; L.W = W; L.Cin = Cin; L.Cout = Cout;
   L.nsplit = rs::enc_wgrad_splits(B, H, W, Cin, Cout, &L.tpb);
-  Tensor part = at::empty({int64_t(L.nsplit) * Cout * 9 * Cin}, x.options().dtype(at::kFloat));
+  const int64_t nblk = int64_t(L.nsplit) * ((Cout + 63) / 64) * ((Cin + 63) / 64);
+  Tensor part = at::empty({nblk * 64 * 9 * 64}, x.options().dtype(at::kFloat));
   Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(at::kFloat));
   L.part = part.data_ptr<float>();
   L.dw = dw.data_ptr<float>();

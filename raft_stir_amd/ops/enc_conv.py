@@ -212,7 +212,8 @@ class _Conv3x3(torch.autograd.Function):
 
 
 # csrc/enc_wgrad.hip: all nine taps of a 64 x 64 channel slice per block over
-# halo tiles (deterministic); 64 / 128-channel convs (layer1, layer3)
+# halo tiles (deterministic); every encoder 3x3 stride-1 conv (64 / 96 / 128
+# channels; 96 as two overlapping 64-channel blocks)
 _ENC_WGRAD = os.environ.get("RS_ENC_WGRAD", "1") != "0"
 
 
@@ -221,7 +222,7 @@ def _enc_wgrad_op(dy, x):
 
 
 def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
-    if _ENC_WGRAD and cin % 64 == 0 and cout % 64 == 0:
+    if _ENC_WGRAD and cin % 32 == 0 and cout % 32 == 0 and min(cin, cout) >= 64:
         return _enc_wgrad_op(dyn, xn).to(weight.dtype)
     if _wgrad_covers(cin, cout):
         # the kernel tiles input channels in 64-wide segments: an odd

@@ -25,7 +25,8 @@ def _ref(dy, x):
 
 
 @pytest.mark.parametrize("shape", [(2, 19, 45, 64, 64), (3, 13, 70, 128, 64), (1, 8, 32, 64, 128),
-                                   (2, 46, 62, 128, 128), (1, 5, 7, 64, 64)])
+                                   (2, 46, 62, 128, 128), (1, 5, 7, 64, 64), (2, 23, 31, 96, 96),
+                                   (1, 17, 40, 96, 64), (1, 9, 33, 64, 160)])
 def test_enc_wgrad_vs_fp32(cuda, shape):
     B, H, W, cin, cout = shape
     torch.manual_seed(0)
