@@ -59,18 +59,28 @@ __device__ __forceinline__ int swz(int r, int c) {
 // staging), the packed A row [wh 32 | wl 32] (ops/conv.py pack_weight_split),
 // and the three products are three MFMAs over the same LDS rows -- 3x the
 // MFMA work of bf16, no extra passes over the activations.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool GEO = false, bool F32 = false>
-__global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
+//
+// KG > 1: intra-block split-K (as conv_buf_kernel): KG groups of 4 waves over
+// the same output tile, group g staging and multiplying K steps g, g + KG, ...
+// through its own double buffer, partial tiles summed in LDS by group 0.  The
+// register-staged K loop exposes one global-load latency per step; at the
+// batch-1 shapes (STIR 1x64x80: 160 blocks, 72 K steps of the ConvGRU) that
+// latency, not the MFMAs, set the kernel time.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int BK, bool GEO = false, bool F32 = false, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv_lds_kernel(Args a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(KG == 1 || KG == 2 || KG == 4, "KG");
   static_assert(BK == 32 || BK == 64, "BK");
   static_assert(!F32 || BK == 64, "F32: 64-wide staged rows ([hi 32 | lo 32])");
   constexpr int CPR = BK / 8;  // 16-byte chunks per staged row
   constexpr int WM = BM / WAVES_M / 16, WN = BN / WAVES_N / 16;
   constexpr int NA = BM * CPR / 256, NB = F32 ? BN * 4 / 256 : BN * CPR / 256;  // F32: 8-channel units
   static_assert(NA >= 1 && NB >= 1, "BM, BN must be multiples of 64");
-  __shared__ uint4 lds[2][(BM + BN) * CPR];
+  __shared__ uint4 lds_[KG * 2][(BM + BN) * CPR];
 
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int kg = KG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
+  uint4 (*lds)[(BM + BN) * CPR] = lds_ + kg * 2;  // this K group's double buffer
+  const int t = threadIdx.x & 255, lane = t & 63, wave = t >> 6;
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
   const int bm0 = blockIdx.y * BM, bn0 = blockIdx.x * BN;
   const int m0 = bm0 + wm * WM * 16, n0 = bn0 + wn * WN * 16;
@@ -113,12 +123,18 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   const int e1 = taps * (s0.C >> SH);
   const int e2 = e1 + (a.nseg > 1 ? taps * (s1.C >> SH) : 0);
   const int nsteps = e2 + (a.nseg > 2 ? taps * (s2.C >> SH) : 0);
+  const int nst = (nsteps + KG - 1) / KG;  // block-uniform trip count; a group's steps past the end stage zeros
   const uint4 zero = make_uint4(0, 0, 0, 0);
 
   uint4 ra[NA], rb[NB], rl[F32 ? NB : 1];
 #define RS_GLOAD(STEP)                                                                          \
   do {                                                                                          \
-    const int step_ = (STEP);                                                                   \
+    const int step_ = (STEP) * KG + kg;                                                         \
+    if (KG > 1 && step_ >= nsteps) {                                                            \
+      _Pragma("unroll") for (int i = 0; i < NA; ++i) ra[i] = zero;                              \
+      _Pragma("unroll") for (int i = 0; i < NB; ++i) { rb[i] = zero; if constexpr (F32) rl[i] = zero; } \
+      break;                                                                                    \
+    }                                                                                           \
     const int si = (step_ >= e1) + (step_ >= e2);                                               \
     const bf16_t* sp = si == 0 ? s0.ptr : (si == 1 ? s1.ptr : s2.ptr);                          \
     const int sC = si == 0 ? s0.C : (si == 1 ? s1.C : s2.C);                                    \
@@ -175,9 +191,9 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
   RS_GLOAD(0);
   RS_LSTORE(0);
   __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
+  for (int step = 0; step < nst; ++step) {
     const int buf = step & 1;
-    if (step + 1 < nsteps) RS_GLOAD(step + 1);
+    if (step + 1 < nst) RS_GLOAD(step + 1);
     // (A half, B half) per MFMA pass: bf16 -> the two 32-deep halves of the
     // 64-deep step; F32 -> (wh, xh), (wh, xl), (wl, xh)
     constexpr int NPASS = F32 ? 3 : BK / 32;
@@ -198,11 +214,36 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(Args a) {
                                                                 __builtin_bit_cast(bf16x8_t, fb[nt]),
                                                                 acc[mt][nt], 0, 0, 0);
     }
-    if (step + 1 < nsteps) RS_LSTORE(buf ^ 1);
+    if (step + 1 < nst) RS_LSTORE(buf ^ 1);
     __syncthreads();
   }
 #undef RS_GLOAD
 #undef RS_LSTORE
+  if constexpr (KG > 1) {
+    // groups 1.. park their partial tiles in LDS (free after the loop's last
+    // barrier), group 0 adds them in group order
+    constexpr int NE = WM * WN * 4;
+    static_assert((KG - 1) * NE * 256 * 4 <= KG * 2 * (BM + BN) * CPR * 16, "split-K reduction buffer");
+    float* red = reinterpret_cast<float*>(&lds_[0][0]);
+    if (kg > 0) {
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) red[((kg - 1) * NE + (mt * WN + nt) * 4 + j) * 256 + t] = acc[mt][nt][j];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+#pragma unroll
+    for (int g = 0; g < KG - 1; ++g)
+#pragma unroll
+      for (int mt = 0; mt < WM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < WN; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt][nt][j] += red[(g * NE + (mt * WN + nt) * 4 + j) * 256 + t];
+  }
 
   int pb[WN], py[WN], px[WN];
 #pragma unroll
@@ -1018,14 +1059,22 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
 #undef RS_GEO
     return;
   }
-  if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8 (host-checked)
-#define RS_F32(BM_, BN_)                                                                            \
-  hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, 2, 2, 64, false, true>),                     \
-                     dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256), 0, stream, a)
-    if (L.tile == 6) RS_F32(64, 64);
-    else if (L.tile == 8) RS_F32(128, 128);
-    else RS_F32(128, 64);
+  if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8, split-K 38-40 (host-checked)
+#define RS_F32(BM_, BN_, KG_)                                                                       \
+  hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, 2, 2, 64, false, true, KG_>),                \
+                     dim3(cdiv(a.P, BN_), cdiv(L.Cout, BM_)), dim3(256 * KG_), 0, stream, a)
+    if (L.tile == 6) RS_F32(64, 64, 1);
+    else if (L.tile == 8) RS_F32(128, 128, 1);
+    else if (L.tile == 38) RS_F32(64, 64, 4);
+    else if (L.tile == 39) RS_F32(128, 64, 2);
+    else if (L.tile == 40) RS_F32(64, 64, 2);
+    else RS_F32(128, 64, 1);
 #undef RS_F32
+    return;
+  }
+  if (L.tile == 41) {  // tile 3 (64x64, 32-deep K, register-staged) with 4-way intra-block split-K
+    dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 64));
+    hipLaunchKernelGGL((conv::conv_lds_kernel<64, 64, 2, 2, 32, false, false, 4>), grid, dim3(1024), 0, stream, a);
     return;
   }
   if (L.tile >= 24 && L.tile <= 26) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)

@@ -224,21 +224,36 @@ __global__ __launch_bounds__(NT) void enc_wgrad_kernel(WArgs a) {
     }
 }
 
-// dw[co][ci][ky][kx] = sum over splits (in order) of the partial of the block
-// holding (co, ci); threads walk (co, tap, ci), ci fastest (coalesced reads)
+// dw[co][ci][ky][kx] = sum over splits of the partial of the block holding
+// (co, ci).  A block = 64 consecutive outputs (walked as (co, tap, ci), ci
+// fastest: coalesced partial rows) x 4 split slices; slice s sums splits
+// s, s + 4, ... and the four slice sums are added in slice order through
+// LDS: a fixed order (deterministic) with 4x the loads in flight of one
+// thread per output (the split count is ~256).
 __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit, int Cout,
                                                                int Cin, float* __restrict__ dw) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= Cout * 9 * Cin) return;
-  const int ci = i % Cin, r = i / Cin, k = r % 9, co = r / 9;
-  const int ncb = (Cout + 63) / 64, nib = (Cin + 63) / 64;
-  const int cb = min(co / 64, ncb - 1), ib = min(ci / 64, nib - 1);
-  const int col = co - min(cb * 64, Cout - 64), cil = ci - min(ib * 64, Cin - 64);
-  const size_t blk = (size_t)ncb * nib * (64 * 9 * 64);
-  const float* p = part + (size_t)(cb * nib + ib) * (64 * 9 * 64) + (col * 9 + k) * 64 + cil;
+  __shared__ float red[4][64];
+  const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + o;
+  const bool live = i < Cout * 9 * Cin;
   float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += p[sp * blk];
-  dw[((size_t)co * Cin + ci) * 9 + k] = s;
+  int co = 0, ci = 0, k = 0;
+  if (live) {
+    ci = i % Cin;
+    const int r = i / Cin;
+    k = r % 9;
+    co = r / 9;
+    const int ncb = (Cout + 63) / 64, nib = (Cin + 63) / 64;
+    const int cb = min(co / 64, ncb - 1), ib = min(ci / 64, nib - 1);
+    const int col = co - min(cb * 64, Cout - 64), cil = ci - min(ib * 64, Cin - 64);
+    const size_t blk = (size_t)ncb * nib * (64 * 9 * 64);
+    const float* p = part + (size_t)(cb * nib + ib) * (64 * 9 * 64) + (col * 9 + k) * 64 + cil;
+#pragma unroll 8
+    for (int sp = sl; sp < nsplit; sp += 4) s += p[sp * blk];
+  }
+  red[sl][o] = s;
+  __syncthreads();
+  if (sl == 0 && live) dw[((size_t)co * Cin + ci) * 9 + k] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
 }
 
 }  // namespace encw
@@ -282,7 +297,7 @@ void enc_wgrad_launch(const EncWgradLaunch& L, hipStream_t stream) {
   a.part = L.part;
   hipLaunchKernelGGL(encw::enc_wgrad_kernel, dim3(L.nsplit * a.ncb * a.nib), dim3(encw::NT), 0, stream, a);
   const int n = L.Cout * 9 * L.Cin;
-  hipLaunchKernelGGL(encw::enc_wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, stream, L.part, L.nsplit,
+  hipLaunchKernelGGL(encw::enc_wgrad_reduce_kernel, dim3(cdiv(n, 64)), dim3(256), 0, stream, L.part, L.nsplit,
                      L.Cout, L.Cin, L.dw);
 }
 

@@ -174,7 +174,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   const bool f32 = segs[0].scalar_type() == at::kFloat;
   const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
   if (f32) {
-    TORCH_CHECK(tile == 6 || tile == 7 || tile == 8, "conv_fused: fp32 activations run on tiles 6, 7, 8 only");
+    TORCH_CHECK(tile == 6 || tile == 7 || tile == 8 || (tile >= 38 && tile <= 40),
+                "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40 only");
     TORCH_CHECK(epi == 0 || epi == 1 || epi == 2 || epi == EPI_GRU_ZR || epi == EPI_GRU_Q || epi == EPI_NORM,
                 "conv_fused: fp32 activations support the forward epilogues (bias, relu, scale, gru_zr, gru_q, norm)");
   }
@@ -208,21 +209,22 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
-  TORCH_CHECK(!(tile >= 38 && tile <= 41), "conv_fused: tiles 38-41 do not exist");
+  TORCH_CHECK(!(tile >= 38 && tile <= 40) || f32, "conv_fused: tiles 38-40 are the fp32 split-K tiles");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
   if (tile >= 24 && tile <= 26) {  // halo tiles: the (TH+KH-1) x (16+KW-1) halo must fit the LDS buffer
     const int TH = tile == 26 ? 4 : 8, HCAP = tile == 26 ? 128 : 192;
     TORCH_CHECK((TH + KH - 1) * (16 + KW - 1) <= HCAP, "conv_fused: kernel too large for halo tile ", tile);
   }
   const bool bm128 = tile == 4 || tile == 7 || tile == 8 || (tile >= 10 && tile <= 13) || tile == 16 ||
-                     tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26 || tile == 36;
+                     tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26 || tile == 36 ||
+                     tile == 39;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
   const int tileM = (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
                     : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
                     : (bm128 || bm128w) ? 128 : (tile == 5 ? 16 : 64);
-  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && !f32)  // 64-deep K steps
+  if (tile >= 6 && tile != 12 && tile != 13 && tile != 14 && tile != 41 && !f32)  // 64-deep K steps
     for (size_t s = 0; s < segs.size(); ++s)
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: 64-deep-K tiles need segment channels % 64 == 0");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,

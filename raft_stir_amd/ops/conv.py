@@ -67,9 +67,17 @@ def pack_weight_split(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: i
 F32_TILES = (6, 7, 8)
 
 
-def choose_tile_f32(P: int, cout: int) -> int:
+def choose_tile_f32(P: int, cout: int, geo: bool = False) -> int:
     """Split-bf16 fp32 tile: 64x64 for narrow outputs / small grids, else
-    128x64 (128x128 at large pixel counts)."""
+    128x64 (128x128 at large pixel counts).  Batch-1 grids (<= 768 64x64
+    tiles: STIR 1x64x80, Sintel 1x55x136) take the intra-block split-K
+    variants, 4 K groups (38) when the grid has at most one tile per CU, else
+    2 (40): their register-staged K loop is load-latency bound there."""
+    nb64 = -(-P // 64) * -(-cout // 64)
+    if nb64 <= 256 and not geo:  # (conv_geo's strided tiles have no split-K variant)
+        return 38
+    if nb64 <= 768 and not geo:
+        return 40
     if cout <= 64:
         return 6
     return 8 if (P >= 16384 and cout >= 256) else 7
@@ -109,6 +117,8 @@ def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
             if 128 < cout <= 192 and k >= 1024 and _WIDE & 4:
                 return 29
         return 16 if (P >= 16384 and cout >= 192 and k >= 384) else 17
+    if -(-P // 64) * -(-cout // 64) <= 256:
+        return 41  # tile 3 with 4-way intra-block split-K: batch-1 grids (RAFT-small / STIR ConvGRU)
     big = cout >= 192 or (cout >= 126 and P >= 16384)
     return 4 if big else 3
 

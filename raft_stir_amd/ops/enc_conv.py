@@ -407,7 +407,7 @@ def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None, sc
     Wo = (W + 2 * pad[1] - kw) // stride[1] + 1
     out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.float32)
     torch.ops.raft_stir.conv_geo([xn], [0], [cin], wp, b, kh, kw, pad[0], pad[1], stride[0], stride[1], Ho, Wo,
-                                 cout, out, 0, 1, 1, 0, 0, choose_tile_f32(N * Ho * Wo, cout), st, bool(ps), scale,
+                                 cout, out, 0, 1, 1, 0, 0, choose_tile_f32(N * Ho * Wo, cout, geo=True), st, bool(ps), scale,
                                  bool(relu))
     return out.permute(0, 3, 1, 2)
 

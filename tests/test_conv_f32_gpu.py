@@ -18,7 +18,7 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("tile", [6, 7, 8])
+@pytest.mark.parametrize("tile", [6, 7, 8, 38, 39, 40])
 @pytest.mark.parametrize("k", [(3, 3), (1, 5), (5, 1), (1, 1)])
 @pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
 def test_conv_f32_plain(cuda, tile, k, epi):

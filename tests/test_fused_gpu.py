@@ -24,7 +24,7 @@ def _bf(x):
 
 @pytest.mark.parametrize("k", [(1, 1), (3, 3), (1, 5), (5, 1)])
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 6, 7, 11, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26,
-                                  27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37])
+                                  27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 41])
 @pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE])
 def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     torch.manual_seed(0)
