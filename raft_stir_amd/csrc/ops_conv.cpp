@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace rs {
 struct ConvLaunch {
   const void* seg_ptr[3];
@@ -38,6 +40,19 @@ struct ConvLaunch {
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
+struct SconvLaunch {
+  const void* x;
+  int xstr, Cin, B, Hi, Wi;
+  const float* w;
+  const float* bias;
+  void* y;
+  int ystr, yoff, Cout, Ho, Wo, KH, KW, S, P, relu;
+  const void* res;
+  int rstr;
+  bool f32;
+};
+int sconv_max_weights();
+void sconv_launch(const SconvLaunch& L, hipStream_t stream);
 struct EncWgradLaunch {
   const void* x;
   const void* dy;
@@ -580,6 +595,47 @@ static void check_nhwc_view(const Tensor& t, const char* n) {
   TORCH_CHECK(t.numel() / t.size(3) * t.stride(2) * 2 < (int64_t(1) << 31), n, ": too large for 32-bit offsets");
 }
 
+// Narrow-channel NHWC conv (csrc/sconv.hip; RAFT-small encoder inference):
+//   x   : [B, Hi, Wi, Cin] bf16 / fp32 view (dense pixels, channel stride % 8 == 0)
+//   w   : fp32 [Cout, KH, KW, Cin] contiguous;  bias: fp32 [Cout] or None
+//   out : [B, Ho, Wo, >= yoff + Cout] same dtype as x, contiguous; out[..., yoff:yoff+Cout] =
+//         [relu](conv(x) + bias) [then relu(. + res)]
+void sconv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, int64_t stride, int64_t pad,
+           bool relu, const Tensor& out, int64_t yoff, const c10::optional<Tensor>& res) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "sconv: x bf16 / fp32 NHWC");
+  const int B = x.size(0), Hi = x.size(1), Wi = x.size(2), Cin = x.size(3);
+  TORCH_CHECK(x.stride(3) == 1 && x.stride(2) % 8 == 0 && x.stride(1) == Wi * x.stride(2) &&
+                  x.stride(0) == Hi * x.stride(1) && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "sconv: x must be dense NHWC pixels with a channel stride % 8 == 0, 16-B aligned");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(3) == Cin,
+              "sconv: w fp32 [Cout, KH, KW, Cin]");
+  const int Cout = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "sconv: channel counts must be multiples of 8");
+  TORCH_CHECK(std::min(4, Cout / 8) * 8 * KH * KW * Cin <= rs::sconv_max_weights(), "sconv: weight tile too large");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "sconv: geometry");
+  const int Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.scalar_type() == x.scalar_type() &&
+                  out.size(0) == B && out.size(1) == Ho && out.size(2) == Wo && yoff >= 0 && yoff % 8 == 0 &&
+                  yoff + Cout <= out.size(3) && out.size(3) % 8 == 0,
+              "sconv: out must be contiguous [B, Ho, Wo, C] with the window [yoff, yoff + Cout)");
+  if (bias) TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() == Cout, "sconv: bias");
+  if (res)
+    TORCH_CHECK(res->is_cuda() && res->is_contiguous() && res->scalar_type() == x.scalar_type() && res->dim() == 4 &&
+                    res->size(0) == B && res->size(1) == Ho && res->size(2) == Wo && res->size(3) == Cout,
+                "sconv: residual must be contiguous [B, Ho, Wo, Cout]");
+  const c10::DeviceGuard guard(x.device());
+  rs::SconvLaunch L{};
+  L.x = x.data_ptr(); L.xstr = x.stride(2); L.Cin = Cin; L.B = B; L.Hi = Hi; L.Wi = Wi;
+  L.w = w.data_ptr<float>(); L.bias = bias ? bias->data_ptr<float>() : nullptr;
+  L.y = out.data_ptr(); L.ystr = out.size(3); L.yoff = yoff; L.Cout = Cout;
+  L.Ho = Ho; L.Wo = Wo; L.KH = KH; L.KW = KW; L.S = stride; L.P = pad; L.relu = relu ? 1 : 0;
+  L.res = res ? res->data_ptr() : nullptr; L.rstr = Cout;
+  L.f32 = x.scalar_type() == at::kFloat;
+  rs::sconv_launch(L, stream());
+  RS_CHECK_LAUNCH();
+}
+
 Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
   check_nhwc_view(dy, "enc_wgrad dy");
   check_nhwc_view(x, "enc_wgrad x");
@@ -819,6 +875,8 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
         "Tensor(d!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None) -> ()");
   m.def("enc_wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("sconv(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool relu, Tensor(a!) out, int yoff, "
+        "Tensor? res) -> ()");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
         "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
         "int OOX, int tile, Tensor(b!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None, "
@@ -831,6 +889,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("conv3x3_halo", &conv3x3_halo);
   m.impl("enc_wgrad", &enc_wgrad);
+  m.impl("sconv", &sconv);
   m.impl("stem_conv", &stem_conv);
   m.impl("stem_wgrad", &stem_wgrad);
   m.impl("conv_geo", &conv_geo);

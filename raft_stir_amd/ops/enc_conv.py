@@ -723,3 +723,72 @@ def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor, stats=None):
     w1, st = _weight_in(conv1.weight)
     wd, _ = _weight_in(down.weight)
     return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st, stats)
+
+
+# ------------------------------------------------------- narrow-channel convs
+# RAFT-small's encoders (reference core/extractor.py:60-116, :195-267) run
+# 1x1 / 3x3 convs of 8-96 channels; at inference they go to csrc/sconv.hip
+# (VALU, fp32 accumulation, bias / ReLU / residual in the epilogue, bf16 or
+# fp32 NHWC) instead of MIOpen + a bias kernel + an autocast weight cast.
+_SCONV = os.environ.get("RS_SCONV", "1") != "0"
+
+
+def sconv_eligible(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:
+    """Inside RAFT-small's encoder only (the scope where geo_scope(False) keeps
+    the MFMA strided paths off): full RAFT's 64-128-channel convs stay on the
+    MFMA kernels."""
+    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x):
+        return False
+    if x.dtype not in (torch.bfloat16, torch.float32) or not x.is_contiguous(memory_format=_CL):
+        return False
+    if x.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):
+        return False  # autocast would have run this conv in bf16
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad
+                                    or (conv.bias is not None and conv.bias.requires_grad)
+                                    or (residual is not None and residual.requires_grad)):
+        return False  # inference only (no backward kernels)
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if k not in ((1, 1), (3, 3)) or isinstance(p, str) or p != (k[0] // 2, k[1] // 2):
+        return False
+    if s not in ((1, 1), (2, 2)) or conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    cin, cout = conv.in_channels, conv.out_channels
+    if cin % 8 or cout % 8 or min(4, cout // 8) * 8 * k[0] * k[1] * cin > 16384:
+        return False
+    if residual is not None and (residual.dtype != x.dtype or not residual.is_contiguous(memory_format=_CL)):
+        return False
+    return x.numel() * x.element_size() < (1 << 31)
+
+
+def _sconv_weight(conv: nn.Conv2d) -> torch.Tensor:
+    """fp32 [Cout, KH, KW, Cin], cached per weight version (runtime/weights.py
+    generation + the parameter's version counter)."""
+    from ..runtime import weights
+    w = conv.weight
+    key = (weights.generation(), w.data_ptr(), w._version)
+    hit = conv.__dict__.get("_rs_sconv_w")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        t = w.detach().float().permute(0, 2, 3, 1).contiguous()
+        if hit is not None and hit[1].shape == t.shape:
+            hit[1].copy_(t)  # in place: hipGraphs captured with the old tensor stay valid
+            t = hit[1]
+    conv.__dict__["_rs_sconv_w"] = (key, t)
+    return t
+
+
+def sconv(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, relu: bool = False, residual=None) -> torch.Tensor:
+    """[relu](conv(x) [+ bias]) [then relu(. + residual)] on csrc/sconv.hip;
+    channels_last in and out (see :func:`sconv_eligible`)."""
+    xn = _nhwc(x)
+    N, H, W, _ = xn.shape
+    kh, kw = conv.kernel_size
+    s, p = conv.stride[0], conv.padding[0]
+    Ho, Wo = (H + 2 * p - kh) // s + 1, (W + 2 * p - kw) // s + 1
+    cout = conv.out_channels
+    out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=x.dtype)
+    b = conv.bias.detach().float().contiguous() if (bias and conv.bias is not None) else None
+    rn = _nhwc(residual).contiguous() if residual is not None else None
+    torch.ops.raft_stir.sconv(xn, _sconv_weight(conv), b, s, p, bool(relu), out, 0, rn)
+    return out.permute(0, 3, 1, 2)

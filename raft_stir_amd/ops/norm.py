@@ -296,6 +296,12 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
     (instance / train-mode batch norm remove it exactly; eval-mode batch norm
     shifts its running mean by it): no bias-add pass over the conv output
     forward and no bias-gradient reduction over it backward."""
+    if enc_conv.sconv_eligible(conv, x, residual):  # narrow channels (RAFT-small encoders), inference
+        if isinstance(norm, nn.Sequential) and len(norm) == 0:  # norm_fn 'none': all in the conv epilogue
+            return enc_conv.sconv(conv, x, True, relu, residual)
+        if _norm_kind_ok(norm) and _FOLD_BIAS:
+            return norm_act(norm, enc_conv.sconv(conv, x, False), relu, residual, bias=conv.bias)
+        return norm_act(norm, enc_conv.sconv(conv, x, True), relu, residual)
     if conv.bias is None or not _FOLD_BIAS or not _ext.use_hip(x) or not _norm_kind_ok(norm):
         return norm_act(norm, conv(x), relu, residual)
     if residual is None and enc_conv.stem_eligible(conv, x):  # the 7x7 / stride-2 stem (csrc/stem.hip)
