@@ -205,7 +205,7 @@ class FusedUpdate:
             P = B * H * W
 
             def cf(segs, w, b, kh, kw, cout, epi, out, ooff=0, **kw_):
-                conv_fused(segs, w, b, kh, kw, cout, epi, out, ooff, tile=choose_tile_f32(P, cout), **kw_)
+                conv_fused(segs, w, b, kh, kw, cout, epi, out, ooff, tile=None, **kw_)  # tuned F32 table / heuristic
         else:
             cf = conv_fused
         hx[..., :hd].copy_(net.permute(0, 2, 3, 1))

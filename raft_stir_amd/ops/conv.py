@@ -147,6 +147,21 @@ def tuned_tiles() -> dict:
     return _TUNED
 
 
+_TUNED_F32: dict | None = None
+
+
+def tuned_tiles_f32() -> dict:
+    """Measured F32-tile table (scripts/tune_conv.py --f32), keyed by tune_key."""
+    global _TUNED_F32
+    if _TUNED_F32 is None:
+        _TUNED_F32 = {}
+        if os.environ.get("RS_CONV_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+            import json
+            with open(_TUNED_PATH) as f:
+                _TUNED_F32 = {k: int(v) for k, v in json.load(f).get("tiles_f32", {}).items()}
+    return _TUNED_F32
+
+
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
                aux2=None, a2off=0, tile=None, stats=None, stats_per_sample=False, nscale=None):
@@ -160,12 +175,18 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
     if _RECORD is not None:
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
-                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile))
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, stats=stats,
+                            stats_per_sample=stats_per_sample, nscale=nscale))
     if tile is None:
         t0 = tensors[0]
-        tile = tuned_tiles().get(tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi))
-        if tile is None:
-            tile = choose_tile(t0.shape[0] * t0.shape[1] * t0.shape[2], cout, chans, kh * kw)
+        key = tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi)
+        P = t0.shape[0] * t0.shape[1] * t0.shape[2]
+        if t0.dtype == torch.float32:  # split-bf16 F32 tiles: measured table, else the heuristic
+            tile = tuned_tiles_f32().get(key) or choose_tile_f32(P, cout)
+        else:
+            tile = tuned_tiles().get(key)
+            if tile is None:
+                tile = choose_tile(P, cout, chans, kh * kw)
     if stats is None and nscale is None:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

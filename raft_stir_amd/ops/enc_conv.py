@@ -400,7 +400,7 @@ def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None, sc
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.float32)
         rn = _nhwc(residual) if residual is not None else None
         conv_fused([(xn, 0, cin)], wp, b, 3, 3, cout, EPI_NORM if norm else EPI_BIAS, out, 0,
-                   hd=int(bool(relu)), aux1=rn, tile=choose_tile_f32(N * H * W, cout), stats=st,
+                   hd=int(bool(relu)), aux1=rn, tile=None, stats=st,
                    stats_per_sample=ps, nscale=scale)
         return out.permute(0, 3, 1, 2)
     Ho = (H + 2 * pad[0] - kh) // stride[0] + 1

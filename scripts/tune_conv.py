@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+F32_CANDIDATES = [6, 7, 8, 38, 39, 40]
 CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 42, 43,
               44, 45, 46]
 
@@ -35,7 +36,7 @@ def record_calls(args):
     from raft_stir_amd.utils.padder import InputPadder
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = RAFT(make_args(mixed_precision=True, small=args.small)).to(dev).to(memory_format=torch.channels_last)
+    model = RAFT(make_args(mixed_precision=not args.f32, small=args.small)).to(dev).to(memory_format=torch.channels_last)
     calls = {}
 
     def grab(tag, fn):
@@ -50,15 +51,16 @@ def record_calls(args):
                 calls[key] = (tag, c)
         C._RECORD = None
 
-    model.train()
-    i1, i2, flow, valid = make_batch(args.batch, *args.size, seed=0, device=dev)
+    if not args.f32:
+        model.train()
+        i1, i2, flow, valid = make_batch(args.batch, *args.size, seed=0, device=dev)
 
-    def train_step():
-        preds = model(i1, i2, iters=args.iters)
-        loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
-        loss.backward()
-    train_step()  # warm (engine buffers)
-    grab("train", train_step)
+        def train_step():
+            preds = model(i1, i2, iters=args.iters)
+            loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+            loss.backward()
+        train_step()  # warm (engine buffers)
+        grab("train", train_step)
     model.eval()
     h, w = args.infer_size
     j1 = torch.rand(1, 3, h, w, device=dev) * 255
@@ -107,6 +109,8 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--small", action="store_true", help="tune RAFT-small's calls")
     ap.add_argument("--merge", action="store_true", help="update the existing table instead of replacing it")
+    ap.add_argument("--f32", action="store_true",
+                    help="fp32 inference calls on the split-bf16 F32 tiles -> the 'tiles_f32' table")
     args = ap.parse_args()
     os.environ["RS_CONV_TUNED"] = "0"  # record with the heuristic, compare against it
     from raft_stir_amd.ops import _ext
@@ -123,28 +127,42 @@ def main():
             if kw[k] is not None:
                 kw[k] = kw[k].clone()
         t_in = kw["segs"][0][0]
-        heur = C.choose_tile(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"],
-                             [s[2] for s in kw["segs"]], kw["kh"] * kw["kw"])
+        if args.f32:
+            heur = C.choose_tile_f32(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"])
+            cands = F32_CANDIDATES
+        else:
+            heur = C.choose_tile(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"],
+                                 [s[2] for s in kw["segs"]], kw["kh"] * kw["kw"])
+            cands = CANDIDATES
         res = {}
-        for t in sorted(set(CANDIDATES + [heur])):
+        for t in sorted(set(cands + [heur])):
             try:
                 res[t] = gtime(lambda: C.conv_fused(**kw, tile=t), args.reps)
-            except RuntimeError:
+            except RuntimeError as e:
+                if t == heur:
+                    print("  heuristic tile failed:", str(e).splitlines()[0], flush=True)
                 continue
+        if not res:
+            print(f"{tag:5s} {key:42s} no applicable tile, skipped", flush=True)
+            continue
         best = min(res, key=res.get)
         table[key] = best
-        report.append(dict(key=key, phase=tag, heuristic=heur, us_heuristic=round(res[heur], 2), best=best,
+        report.append(dict(key=key, phase=tag, heuristic=heur, us_heuristic=round(res.get(heur, res[best]), 2), best=best,
                            us_best=round(res[best], 2)))
-        print(f"{tag:5s} {key:42s} heur t{heur} {res[heur]:7.1f}us  best t{best} {res[best]:7.1f}us", flush=True)
-    if args.merge and os.path.exists(args.out):
+        print(f"{tag:5s} {key:42s} heur t{heur} {res.get(heur, float('nan')):7.1f}us  best t{best} {res[best]:7.1f}us", flush=True)
+    section, rsection = ("tiles_f32", "report_f32") if args.f32 else ("tiles", "report")
+    old = {}
+    if os.path.exists(args.out):
         with open(args.out) as f:
             old = json.load(f)
+    if args.merge:
         keys = set(table)
-        table = {**old.get("tiles", {}), **table}
-        report = [r for r in old.get("report", []) if r["key"] not in keys] + report
+        table = {**old.get(section, {}), **table}
+        report = [r for r in old.get(rsection, []) if r["key"] not in keys] + report
+    old.update({"device": torch.cuda.get_device_name(0), "note": "scripts/tune_conv.py", section: table,
+                rsection: report})
     with open(args.out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(0), "note": "scripts/tune_conv.py", "tiles": table,
-                   "report": report}, f, indent=1)
+        json.dump(old, f, indent=1)
     tot_h = sum(r["us_heuristic"] for r in report)
     tot_b = sum(r["us_best"] for r in report)
     print(f"sum over distinct calls: heuristic {tot_h:.1f}us -> tuned {tot_b:.1f}us; wrote {args.out}")
