@@ -61,17 +61,41 @@ __device__ __forceinline__ void im2col_row(const SArgs& s, int b, int iy, int ix
 // Forward.  Block = 64 output pixels (b, oy, ox0 .. ox0+63) x 64 channels;
 // waves 2 x 2, wave tile 32 channels x 32 pixels (2 x 2 16x16 MFMA tiles).
 // w: packed [64][7][32] bf16 ([64][7][64] = [wh 32 | wl 32] for F32).
+// Staging: the 7 input rows the block reads are each ONE contiguous run of
+// the NHWC image (134 pixels x 3 channels = 402 values from pixel 2*ox0 - 3),
+// loaded coalesced and stored as bf16 (hi / lo) rows of XR elements; the
+// im2col row of output pixel n and kernel row ky is then elements
+// [6n, 6n + 21) of LDS row ky -- no per-(pixel, tap) gathers.  K lanes
+// 21..31 read the next pixel's values; the packed weights are zero there.
+constexpr int XR = 416;  // LDS row (elements): 402 live + the K-lane overhang of pixel 63 (6 * 63 + 32 = 410)
+
 template <bool F32>
 __global__ __launch_bounds__(256) void stem_fwd_kernel(SArgs s, conv::Args a) {
-  __shared__ __attribute__((aligned(16))) bf16_t xs[(F32 ? 2 : 1) * PXB * 7 * RS_];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[(F32 ? 2 : 1) * 7 * XR];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int segs = cdiv(s.Wo, PXB);
   const int row = blockIdx.x / segs, ox0 = (blockIdx.x - row * segs) * PXB;
   const int b = row / s.Ho, oy = row - b * s.Ho;
-  for (int r = t; r < PXB * 7; r += 256) {  // (pixel, ky) im2col rows
-    const int n = r / 7, ky = r - n * 7;
-    bf16_t* hi = xs + (size_t)(n * 7 + ky) * RS_;
-    im2col_row<F32>(s, b, 2 * oy - 3 + ky, 2 * (ox0 + n) - 3, hi, hi + PXB * 7 * RS_);
+  const int ix0 = 2 * ox0 - 3;
+  // value pairs (2 consecutive elements of one row): 7 rows x 208 pairs
+  for (int q = t; q < 7 * (XR / 2); q += 256) {
+    const int ky = q / (XR / 2), e = (q - ky * (XR / 2)) * 2;
+    const int iy = 2 * oy - 3 + ky;
+    float v[2] = {0.f, 0.f};
+    if (iy >= 0 && iy < s.Hi) {
+      const size_t rbase = ((size_t)b * s.Hi + iy) * s.Wi * 3;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ee = e + u, ix = ix0 + ee / 3;
+        if (ee < 402 && ix >= 0 && ix < s.Wi) v[u] = ldx(s, rbase + (size_t)ix * 3 + ee % 3);
+      }
+    }
+    const bf16_t h0 = f2bf(v[0]), h1 = f2bf(v[1]);
+    *reinterpret_cast<uint32_t*>(xs + ky * XR + e) = uint32_t(h0) | (uint32_t(h1) << 16);
+    if constexpr (F32) {
+      const bf16_t l0 = f2bf(v[0] - bf2f(h0)), l1 = f2bf(v[1] - bf2f(h1));
+      *reinterpret_cast<uint32_t*>(xs + 7 * XR + ky * XR + e) = uint32_t(l0) | (uint32_t(l1) << 16);
+    }
   }
   __syncthreads();
   const int wm = wave & 1, wn = wave >> 1;
@@ -82,6 +106,11 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(SArgs s, conv::Args a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // B fragment: 8 bf16 at element 6n + 8lc of row ky (4-byte aligned: four 32-bit reads)
+  auto bfrag = [&](const bf16_t* base, int n, int ky) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(base + ky * XR + 6 * n + 8 * lc);
+    return make_uint4(p[0], p[1], p[2], p[3]);
+  };
 #pragma unroll
   for (int ky = 0; ky < 7; ++ky) {
     uint4 fa[2][F32 ? 2 : 1], fb[2][F32 ? 2 : 1];
@@ -93,9 +122,9 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(SArgs s, conv::Args a) {
     }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      const bf16_t* xr = xs + (size_t)((wn * 32 + nt * 16 + lr) * 7 + ky) * RS_ + lc * 8;
-      fb[nt][0] = *reinterpret_cast<const uint4*>(xr);
-      if constexpr (F32) fb[nt][1] = *reinterpret_cast<const uint4*>(xr + PXB * 7 * RS_);
+      const int n = wn * 32 + nt * 16 + lr;
+      fb[nt][0] = bfrag(xs, n, ky);
+      if constexpr (F32) fb[nt][1] = bfrag(xs + 7 * XR, n, ky);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)

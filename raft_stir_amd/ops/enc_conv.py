@@ -255,10 +255,13 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
 # forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
 # conv epilogues (normalisation statistics, eval-BN scale / shift + ReLU) and a
 # deterministic MFMA weight gradient; the image needs no input gradient.
-# RS_STEM: "f32" (default) runs the HIP stem for fp32 inference only -- under
-# bf16 the MIOpen implicit GEMM is faster (training 2 x 405 us HIP forward +
-# 500 us weight gradient vs 2 x 73 + 2 x 111 us; paired bench 347 -> 357
-# pairs/s with RS_STEM=0, profiles/r3/README.md); "1": always, "0": never.
+# RS_STEM: "infer" (default) runs the HIP stem for inference (bf16 and fp32;
+# the forward stages each input row as one coalesced run) and leaves bf16
+# training on MIOpen, whose forward + weight gradient measured faster than
+# the HIP pair (2 x 405 us forward + 500 us weight gradient vs 2 x 73 + 2 x 111
+# us with the first, gather-staged forward; paired bench 347 -> 357 pairs/s
+# with RS_STEM=0, profiles/r3/README.md); "f32": fp32 inference only; "1":
+# always; "0": never.
 _STEM_MODE = os.environ.get("RS_STEM", "f32")
 _STEM = _STEM_MODE != "0"
 
@@ -287,6 +290,8 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     if f32 and torch.is_grad_enabled() and conv.weight.requires_grad:
         return False  # fp32 training: the module graph
     if _STEM_MODE == "f32" and not f32:
+        return False
+    if _STEM_MODE == "infer" and torch.is_grad_enabled() and conv.weight.requires_grad:
         return False
     return x.numel() * 4 < (1 << 31)
 

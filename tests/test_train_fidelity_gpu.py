@@ -113,13 +113,17 @@ def test_fused_bf16_training_curve_tracks_fp32(cuda):
     def batches(s):
         return make_batch(2, 128, 192, seed=1000 + s, device=cuda, max_disp=16.0)
 
-    lbf = _train(mbf, steps, batches, 4e-4)
-    with _ext.reference_mode():
-        l32 = _train(m32, steps, batches, 4e-4)
-    # 200 steps of a chaotic recurrent model: run-to-run nondeterminism (fp32
-    # atomics in MIOpen / HIP weight gradients) moves the fp32 curve itself by
-    # ~+-20 % between processes (13.5 .. 17.7 at the end), so the bounds are on
-    # 50-step means and relative to each other.
+    from raft_stir_amd.runtime.determinism import deterministic
+    # 200 steps of a chaotic recurrent model: with the default (fp32-atomic)
+    # weight gradients the fp32 curve itself ends anywhere in ~10.8 .. 17.7
+    # between processes (profiles/r3/README.md), which made a 25 % bound on the
+    # bf16 - fp32 gap flaky.  Both runs are in deterministic mode (ordered
+    # reductions; MIOpen deterministic algorithms for the fp32 reference), so
+    # each curve is a fixed function of the code and the bound is exact.
+    with deterministic(True):
+        lbf = _train(mbf, steps, batches, 4e-4)
+        with _ext.reference_mode():
+            l32 = _train(m32, steps, batches, 4e-4)
     w = 50
     first_bf, last_bf = lbf[:w].mean().item(), lbf[-w:].mean().item()
     first_32, last_32 = l32[:w].mean().item(), l32[-w:].mean().item()
