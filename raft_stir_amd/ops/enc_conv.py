@@ -255,14 +255,15 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
 # forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
 # conv epilogues (normalisation statistics, eval-BN scale / shift + ReLU) and a
 # deterministic MFMA weight gradient; the image needs no input gradient.
-# RS_STEM: "infer" (default) runs the HIP stem for inference (bf16 and fp32;
-# the forward stages each input row as one coalesced run) and leaves bf16
-# training on MIOpen, whose forward + weight gradient measured faster than
-# the HIP pair (2 x 405 us forward + 500 us weight gradient vs 2 x 73 + 2 x 111
-# us with the first, gather-staged forward; paired bench 347 -> 357 pairs/s
-# with RS_STEM=0, profiles/r3/README.md); "f32": fp32 inference only; "1":
-# always; "0": never.
-_STEM_MODE = os.environ.get("RS_STEM", "f32")
+# RS_STEM: "auto" (default) runs the HIP stem for fp32 inference and for
+# full RAFT's bf16 inference (64 channels: 285.6 vs 283.3 FPS paired, the
+# forward staging each input row as one coalesced run), and leaves bf16
+# training and RAFT-small's 32-channel bf16 stem (2.27 vs 2.24 ms STIR) on
+# MIOpen, whose training forward + weight gradient measured faster than the
+# HIP pair (2 x 405 us forward + 500 us weight gradient vs 2 x 73 + 2 x 111 us
+# with the first, gather-staged forward; profiles/r3/README.md);
+# "infer": all inference; "f32": fp32 inference only; "1": always; "0": never.
+_STEM_MODE = os.environ.get("RS_STEM", "auto")
 _STEM = _STEM_MODE != "0"
 
 
@@ -291,7 +292,9 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
         return False  # fp32 training: the module graph
     if _STEM_MODE == "f32" and not f32:
         return False
-    if _STEM_MODE == "infer" and torch.is_grad_enabled() and conv.weight.requires_grad:
+    if _STEM_MODE in ("infer", "auto") and torch.is_grad_enabled() and conv.weight.requires_grad:
+        return False
+    if _STEM_MODE == "auto" and not f32 and conv.out_channels != 64:
         return False
     return x.numel() * 4 < (1 << 31)
 
