@@ -32,6 +32,10 @@
 // (layer2's 96) are covered by two OVERLAPPING 64-channel blocks, [0, 64) and
 // [C - 64, C); the reduction takes each channel from the first block that
 // holds it.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 
 namespace rs {
@@ -271,11 +275,17 @@ struct EncWgradLaunch {
 };
 
 int enc_wgrad_splits(int B, int H, int W, int Cin, int Cout, int* tpb) {
+  // RS_ENC_WGRAD_TPB: minimum tiles per block (fewer blocks, fewer partial
+  // tiles to write and reduce; A/B switch)
+  static const int tmin = [] {
+    const char* e = getenv("RS_ENC_WGRAD_TPB");
+    return e ? atoi(e) : 0;
+  }();
   const int ntiles = B * cdiv(H, encw::TH) * cdiv(W, encw::TW);
   const int chan = cdiv(Cout, 64) * cdiv(Cin, 64);
   int want = 256 / chan;  // ~one block per CU
   if (want < 1) want = 1;
-  *tpb = cdiv(ntiles, want);
+  *tpb = std::max(cdiv(ntiles, want), tmin);
   return cdiv(ntiles, *tpb);
 }
 
