@@ -51,7 +51,7 @@ def record_calls(args):
                 calls[key] = (tag, c)
         C._RECORD = None
 
-    if not args.f32:
+    if not args.f32 and not args.infer_only:
         model.train()
         i1, i2, flow, valid = make_batch(args.batch, *args.size, seed=0, device=dev)
 
@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--small", action="store_true", help="tune RAFT-small's calls")
     ap.add_argument("--merge", action="store_true", help="update the existing table instead of replacing it")
+    ap.add_argument("--infer-only", action="store_true", help="record only the inference forward's calls")
     ap.add_argument("--f32", action="store_true",
                     help="fp32 inference calls on the split-bf16 F32 tiles -> the 'tiles_f32' table")
     args = ap.parse_args()
