@@ -28,8 +28,6 @@
 // with zeros for padding channels, so the K loop needs no bounds checks.
 #include "conv_common.h"
 
-#include <stdio.h>
-
 namespace rs {
 namespace conv {
 

@@ -126,6 +126,34 @@ class MpiSintel(FlowDataset):
                 self.flow_list += sorted(glob(osp.join(flow_root, scene, "*.flo")))
 
 
+_CHAIRS_INDEX = osp.join(osp.dirname(osp.abspath(__file__)), "chairs_val_index.txt")
+
+
+def load_chairs_split(split_file="chairs_split.txt", root=None) -> np.ndarray:
+    """The FlyingChairs split (1 = training, 2 = validation per pair, reference
+    chairs_split.txt; /root/reference/core/datasets.py:124-127).  A user file is
+    looked up as given (CWD) and next to the data root; otherwise the packaged
+    table (``chairs_val_index.txt``: the 640 validation indices of the
+    22,872-pair release) is expanded."""
+    cands = [split_file]
+    if root is not None:
+        cands.append(osp.join(root, "..", osp.basename(split_file)))
+    for c in cands:
+        if c and osp.exists(c):
+            return np.loadtxt(c, dtype=np.int32).reshape(-1)
+    total, idx = None, []
+    with open(_CHAIRS_INDEX) as f:
+        for line in f:
+            if line.startswith("#"):
+                if line.startswith("# total"):
+                    total = int(line.split()[2])
+                continue
+            idx.extend(int(v) for v in line.split())
+    out = np.ones(total, dtype=np.int32)
+    out[np.asarray(idx, dtype=np.int64)] = 2
+    return out
+
+
 class FlyingChairs(FlowDataset):
     def __init__(self, aug_params=None, split="train", root="datasets/FlyingChairs_release/data",
                  split_file="chairs_split.txt"):
@@ -136,10 +164,7 @@ class FlyingChairs(FlowDataset):
         assert len(images) // 2 == len(flows)
         if not flows:
             return
-        if not osp.exists(split_file):
-            alt = osp.join(root, "..", osp.basename(split_file))
-            split_file = alt if osp.exists(alt) else split_file
-        split_list = np.loadtxt(split_file, dtype=np.int32)
+        split_list = load_chairs_split(split_file, root)
         want = {"training": 1, "validation": 2}.get(split)
         for i in range(len(flows)):
             if split_list[i] == want:

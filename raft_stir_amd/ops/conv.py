@@ -45,7 +45,6 @@ def pack_weight(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: int,
 
 
 @torch.no_grad()
-@torch.no_grad()
 def split_weight(packed: torch.Tensor) -> torch.Tensor:
     """A packed fp32 weight [Cout_pad][taps][Ktot] -> the F32 tiles' split
     layout [Cout_pad][taps][2 * Ktot] bf16: per 32-channel K chunk [wh 32 | wl 32]
@@ -83,6 +82,7 @@ def choose_tile_f32(P: int, cout: int, geo: bool = False) -> int:
     return 8 if (P >= 16384 and cout >= 256) else 7
 
 
+@torch.no_grad()
 def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
     b = bias.detach().float()
     if n is not None and n > b.numel():

@@ -21,6 +21,7 @@ convolutions have none.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -783,7 +784,30 @@ def _sconv_weight(conv: nn.Conv2d) -> torch.Tensor:
             hit[1].copy_(t)  # in place: hipGraphs captured with the old tensor stay valid
             t = hit[1]
     conv.__dict__["_rs_sconv_w"] = (key, t)
+    _SCONV_LIVE.add(conv)
     return t
+
+
+_SCONV_LIVE = weakref.WeakSet()
+
+
+def _refresh_sconv() -> None:
+    """runtime/weights.py refresh_all: rewrite every live permuted sconv weight
+    in place, so GraphedInference replays of RAFT-small's encoders see the
+    current parameters (the captured graph holds the cached tensor)."""
+    for conv in list(_SCONV_LIVE):
+        hit = conv.__dict__.get("_rs_sconv_w")
+        if hit is not None:
+            conv.__dict__["_rs_sconv_w"] = (None, hit[1])
+            _sconv_weight(conv)
+
+
+def _register_sconv_refresher():
+    from ..runtime import weights
+    weights.register_refresher(_refresh_sconv)
+
+
+_register_sconv_refresher()
 
 
 def sconv(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, relu: bool = False, residual=None) -> torch.Tensor:

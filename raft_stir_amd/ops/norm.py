@@ -254,6 +254,9 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
                 torch.ops.raft_stir.bn_running_update(
                     mean.reshape(-1), rstd.reshape(-1), None if bias is None else bias.detach().float().contiguous(),
                     rm, rv, norm.num_batches_tracked, norm.eps, norm.momentum, n)
+                # a custom mutable op does not bump the version counters: do it
+                # here so the eval-mode caches keyed on them (_cached) go stale
+                torch.autograd.graph.increment_version([rm, rv])
             else:
                 var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
                 unbiased = var * (n / max(n - 1, 1))

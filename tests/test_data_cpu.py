@@ -299,3 +299,17 @@ def test_flow_viz_wheel_and_image():
     assert tuple(img[1, 1]) == (255, 255, 255)  # zero flow -> white
     bgr = flow_viz.flow_to_image(fl, convert_to_bgr=True)
     assert np.array_equal(bgr[..., ::-1], img)
+
+
+def test_packaged_chairs_split(tmp_path, monkeypatch):
+    """Without a chairs_split.txt in the CWD or next to the data, FlyingChairs
+    falls back to the packaged table: 22,872 pairs, 22,232 train / 640 val
+    (SURVEY D3), identical to the reference file when it is present."""
+    import os
+    from raft_stir_amd.data.datasets import load_chairs_split
+    monkeypatch.chdir(tmp_path)
+    s = load_chairs_split("chairs_split.txt", str(tmp_path / "nodata"))
+    assert s.shape == (22872,) and (s == 1).sum() == 22232 and (s == 2).sum() == 640
+    ref = "/root/reference/chairs_split.txt"
+    if os.path.exists(ref):
+        assert np.array_equal(s, np.loadtxt(ref, dtype=np.int32))

@@ -13,7 +13,8 @@
    backward passes and accumulates them (the same per-sample launches, so
    only the fp32 reduction order differs: <= 1e-5 relative, deterministic
    mode), with BatchNorm frozen on both, and the two replicas must be bitwise
-   identical after the step.
+   identical after the step; and match ONE batch-2 single-process pass
+   within 3e-2 (batch equivalence; different launches and bf16 roundings).
 
 Reference semantics: /root/reference/train.py:138 (DataParallel over --gpus).
 """
@@ -117,6 +118,12 @@ if r == 0:
         l2, _ = sequence_loss(ref(i1[k:k+1], i2[k:k+1], iters=4), fl[k:k+1], v[k:k+1], 0.8, sync_metrics=False)
         l2.backward()
     torch.save((flat_grads(ref) / 2).cpu(), os.environ["OUT"] + "/single.pt")
+    # and ONE batch-2 pass of a fresh replica (batch equivalence: the mean loss
+    # over the global batch, as the reference's DataParallel computes it)
+    ref2 = new_model(dev, m.state_dict())
+    l3, _ = sequence_loss(ref2(i1, i2, iters=4), fl, v, 0.8, sync_metrics=False)
+    l3.backward()
+    torch.save(flat_grads(ref2).cpu(), os.environ["OUT"] + "/batched.pt")
     print("PACKED", m._train_engine().grad_group is not None)
 rd.shutdown()
 '''
@@ -175,3 +182,8 @@ def test_ddp_two_ranks_match_single_process(cuda, tmp_path):
     rel = ((a - s).norm() / s.norm()).item()
     # identical per-sample launches: only the order of the two-term fp32 sums differs
     assert rel < 1e-5, rel
+    # batch equivalence vs one batch-2 process: different launches (batch-2
+    # tiles, bf16 rounding of batched activations), same math
+    bt = torch.load(tmp_path / "batched.pt", weights_only=True)
+    relb = ((a - bt).norm() / bt.norm()).item()
+    assert relb < 3e-2, relb

@@ -111,3 +111,34 @@ def test_conv_norm_act_folds_bias(cuda, kind):
         assert conv.bias.grad.abs().max() == 0 and rconv.bias.grad.abs().max() < 1e-3
         if kind == "batch_train":
             torch.testing.assert_close(norm.running_mean, rnorm.running_mean, atol=1e-5, rtol=1e-5)
+
+
+def test_bn_recalibration_then_eval(cuda):
+    """Train-mode forwards under no_grad (BN recalibration) update the running
+    buffers through the custom bn_running_update op; a following eval()
+    forward must see the new buffers, not the eval-affine cache of the old ones
+    (ops/norm.py bumps the version counters the cache is keyed on)."""
+    from raft_stir_amd.ops.norm import conv_norm_act
+    torch.manual_seed(5)
+    C = 64
+    conv = nn.Conv2d(32, C, 3, padding=1).to(cuda)
+    norm = nn.BatchNorm2d(C).to(cuda)
+    rconv, rnorm = copy.deepcopy(conv), copy.deepcopy(norm)
+    x = torch.randn(2, 32, 24, 40, device=cuda).contiguous(memory_format=torch.channels_last)
+    x2 = (torch.randn(2, 32, 24, 40, device=cuda) * 3 + 1).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        norm.eval()
+        rnorm.eval()
+        conv_norm_act(conv, norm, x)  # populate the eval-mode cache
+        norm.train()
+        rnorm.train()
+        for _ in range(3):
+            conv_norm_act(conv, norm, x2)
+            F.relu(rnorm(rconv(x2)))
+        norm.eval()
+        rnorm.eval()
+        torch.testing.assert_close(norm.running_mean, rnorm.running_mean, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(norm.running_var, rnorm.running_var, atol=1e-4, rtol=1e-4)
+        y = conv_norm_act(conv, norm, x)
+        yr = F.relu(rnorm(rconv(x)))
+    torch.testing.assert_close(y, yr, atol=1e-4, rtol=1e-4)
