@@ -13,6 +13,8 @@
 //   color_jitter(img u8 HxWx3, b, c, s, h, order[4])
 //                                   torchvision ColorJitter-on-PIL semantics with
 //                                   the random factors drawn by the caller
+//   resize_crop(img, oh, ow, fy, fx, y0, x0, ch, cw, hflip, vflip, mul)
+//                                   crop(flip(resize(img))) * mul[c] without the full resize
 //   sparse_flow_resize(flow, valid, fx, fy)  scatter-resize of sparse KITTI flow
 //                                   (reference core/utils/augmentor.py:161-193)
 //
@@ -28,6 +30,8 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <xmmintrin.h>
 #include <vector>
 
 namespace {
@@ -250,10 +254,77 @@ at::Tensor resize_bilinear(const at::Tensor& img_in, int64_t OH, int64_t OW, dou
   return img_in.dim() == 2 ? out.squeeze(-1) : out;
 }
 
+// ------------------------------------------- fused resize + flip + crop
+// crop(flip(resize(img, OH x OW))) [* mul[c]] without materialising the
+// resized image: FlowAugmentor.spatial_transform draws the crop offset from the
+// resized size, then only the ch x cw window is interpolated (the resize was
+// up to 4x the crop's pixels).  Same taps and the same float operations as
+// resize_impl, so the window is bitwise equal to slicing the full resize.
+// Output row i reads resized row (vflip ? OH-1-(y0+i) : y0+i); likewise columns.
+template <typename T>
+void resize_crop_impl(const T* src, T* dst, int H, int W, int C, int OH, int OW, double sy, double sx, int y0,
+                      int x0, int ch, int cw, bool hflip, bool vflip, const float* mul) {
+  auto ty = taps(H, OH, sy), tx = taps(W, OW, sx);
+  std::vector<Tap> cx(cw);
+  for (int j = 0; j < cw; ++j) cx[j] = tx[hflip ? OW - 1 - (x0 + j) : x0 + j];
+  for (int i = 0; i < ch; ++i) {
+    const Tap& t = ty[vflip ? OH - 1 - (y0 + i) : y0 + i];
+    const T* r0 = src + size_t(t.i0) * W * C;
+    const T* r1 = src + size_t(t.i1) * W * C;
+    const float wy = t.w1;
+    T* d = dst + size_t(i) * cw * C;
+    for (int j = 0; j < cw; ++j) {
+      const Tap& u = cx[j];
+      for (int c = 0; c < C; ++c) {
+        const float a0 = float(r0[u.i0 * C + c]), a1 = float(r0[u.i1 * C + c]);
+        const float b0 = float(r1[u.i0 * C + c]), b1 = float(r1[u.i1 * C + c]);
+        const float h0 = a0 + u.w1 * (a1 - a0);
+        const float h1 = b0 + u.w1 * (b1 - b0);
+        const float v = h0 + wy * (h1 - h0);
+        if constexpr (std::is_same<T, uint8_t>::value)
+          d[j * C + c] = uint8_t(std::min(255.f, std::max(0.f, std::nearbyint(v))));
+        else
+          d[j * C + c] = T(mul ? v * mul[c] : v);
+      }
+    }
+  }
+}
+
+at::Tensor resize_crop(const at::Tensor& img_in, int64_t OH, int64_t OW, double fy, double fx, int64_t y0,
+                       int64_t x0, int64_t ch, int64_t cw, bool hflip, bool vflip, at::ArrayRef<double> mul) {
+  TORCH_CHECK(img_in.dim() == 3, "resize_crop: HxWxC");
+  auto img = img_in.contiguous();
+  const int H = int(img.size(0)), W = int(img.size(1)), C = int(img.size(2));
+  TORCH_CHECK(OH > 0 && OW > 0 && ch > 0 && cw > 0, "resize_crop: empty");
+  TORCH_CHECK(y0 >= 0 && x0 >= 0 && y0 + ch <= OH && x0 + cw <= OW, "resize_crop: window outside the resized image");
+  TORCH_CHECK(mul.empty() || int64_t(mul.size()) == C, "resize_crop: one multiplier per channel");
+  const double sy = fy > 0 ? 1.0 / fy : double(H) / OH;
+  const double sx = fx > 0 ? 1.0 / fx : double(W) / OW;
+  at::Tensor out;
+  if (img.scalar_type() == at::kByte) {
+    TORCH_CHECK(mul.empty(), "resize_crop: no multipliers on uint8 images");
+    out = at::empty({ch, cw, C}, at::kByte);
+    resize_crop_impl<uint8_t>(img.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), H, W, C, int(OH), int(OW), sy, sx,
+                              int(y0), int(x0), int(ch), int(cw), hflip, vflip, nullptr);
+  } else {
+    img = img.to(at::kFloat);
+    std::vector<float> m(mul.begin(), mul.end());
+    out = at::empty({ch, cw, C}, at::kFloat);
+    resize_crop_impl<float>(img.data_ptr<float>(), out.data_ptr<float>(), H, W, C, int(OH), int(OW), sy, sx,
+                            int(y0), int(x0), int(ch), int(cw), hflip, vflip, m.empty() ? nullptr : m.data());
+  }
+  return out;
+}
+
 // ---------------------------------------------------------- colour jitter
 // torchvision ColorJitter applied to a PIL RGB image: the four adjustments in
 // the order given (0 brightness, 1 contrast, 2 saturation, 3 hue), each a PIL
 // operation with uint8 rounding between steps.
+inline int rne(float x) { return _mm_cvtss_si32(_mm_set_ss(x)); }  // nearest, ties to even
+inline float ffloor(float x) {
+  const float t = float(int(x));
+  return t > x ? t - 1.f : t;
+}
 inline uint8_t clip8(float v) { return uint8_t(std::min(255.f, std::max(0.f, v))); }
 inline int luma(int r, int g, int b) { return (r * 19595 + g * 38470 + b * 7471 + 0x8000) >> 16; }
 
@@ -299,32 +370,68 @@ at::Tensor color_jitter(const at::Tensor& img_in, double bright, double contrast
   auto out = img_in.contiguous().clone();
   uint8_t* p = out.data_ptr<uint8_t>();
   const int64_t n = out.size(0) * out.size(1);
+  uint8_t lut[256];
   for (int64_t op : order) {
-    if (op == 0) {
+    if (op == 0) {  // per-value map: a 256-entry table
       const float f = float(bright);
-      for (int64_t i = 0; i < 3 * n; ++i) p[i] = clip8(p[i] * f);
+      for (int v = 0; v < 256; ++v) lut[v] = clip8(v * f);
+      for (int64_t i = 0; i < 3 * n; ++i) p[i] = lut[p[i]];
     } else if (op == 1) {
       // PIL ImageEnhance.Contrast: blend with the (rounded) mean grey level.
-      double acc = 0;
+      int64_t acc = 0;
       for (int64_t i = 0; i < n; ++i) acc += luma(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
-      const float mean = float(int(acc / n + 0.5));
+      const float mean = float(int(double(acc) / n + 0.5));
       const float f = float(contrast);
-      for (int64_t i = 0; i < 3 * n; ++i) p[i] = clip8(mean + f * (p[i] - mean));
+      for (int v = 0; v < 256; ++v) lut[v] = clip8(mean + f * (v - mean));
+      for (int64_t i = 0; i < 3 * n; ++i) p[i] = lut[p[i]];
     } else if (op == 2) {
       const float f = float(sat);
       for (int64_t i = 0; i < n; ++i) {
-        const float g = float(luma(p[3 * i], p[3 * i + 1], p[3 * i + 2]));
-        for (int c = 0; c < 3; ++c) p[3 * i + c] = clip8(g + f * (p[3 * i + c] - g));
+        uint8_t* q = p + 3 * i;
+        const float g = float(luma(q[0], q[1], q[2]));
+        q[0] = clip8(g + f * (q[0] - g));
+        q[1] = clip8(g + f * (q[1] - g));
+        q[2] = clip8(g + f * (q[2] - g));
       }
     } else if (op == 3) {
       if (hue == 0.0) continue;
       const int shift = int(hue * 255.0);
+      // rgb2hsv -> shift -> hsv2rgb with the divisions of the reference
+      // formulas kept (a one-step hue quantisation change moves a channel by
+      // up to ~6 levels), floor / round-to-nearest-even as inline SSE
+      // conversions instead of libm calls (baseline x86-64 has no roundss)
       for (int64_t i = 0; i < n; ++i) {
-        int h, s, v, r, g, b;
-        rgb2hsv(p[3 * i], p[3 * i + 1], p[3 * i + 2], h, s, v);
-        h = (h + shift) & 255;  // uint8 wrap, as torchvision does on the H plane
-        hsv2rgb(h, s, v, r, g, b);
-        p[3 * i] = uint8_t(r); p[3 * i + 1] = uint8_t(g); p[3 * i + 2] = uint8_t(b);
+        uint8_t* q = p + 3 * i;
+        const int r = q[0], g = q[1], b = q[2];
+        const int maxc = std::max(r, std::max(g, b)), minc = std::min(r, std::min(g, b));
+        if (maxc == minc) continue;  // grey: s = 0, the hue shift leaves it unchanged
+        const float cr = float(maxc - minc);
+        const int s_ = int(cr / maxc * 255.f);
+        const float rc = (maxc - r) / cr, gc = (maxc - g) / cr, bc = (maxc - b) / cr;
+        float hf;
+        if (r == maxc) hf = bc - gc;
+        else if (g == maxc) hf = 2.f + rc - bc;
+        else hf = 4.f + gc - rc;
+        hf = hf / 6.f;
+        hf = hf - ffloor(hf);
+        const int h = (int(hf * 255.f) + shift) & 255;  // uint8 wrap, as torchvision does on the H plane
+        // hsv2rgb (s > 0 here unless the quantised s is 0)
+        if (s_ == 0) { q[0] = q[1] = q[2] = uint8_t(maxc); continue; }
+        const float hh = h / 255.f, sf = s_ / 255.f;
+        const int k = int(hh * 6.f);  // hh >= 0: truncation is floor
+        const float f = hh * 6.f - k;
+        const int v = maxc;
+        const int pp = rne(v * (1.f - sf)), qq = rne(v * (1.f - sf * f)), tt = rne(v * (1.f - sf * (1.f - f)));
+        int ro, go, bo;
+        switch (k % 6) {
+          case 0: ro = v; go = tt; bo = pp; break;
+          case 1: ro = qq; go = v; bo = pp; break;
+          case 2: ro = pp; go = v; bo = tt; break;
+          case 3: ro = pp; go = qq; bo = v; break;
+          case 4: ro = tt; go = pp; bo = v; break;
+          default: ro = v; go = pp; bo = qq; break;
+        }
+        q[0] = uint8_t(ro); q[1] = uint8_t(go); q[2] = uint8_t(bo);
       }
     }
   }
@@ -367,5 +474,7 @@ TORCH_LIBRARY(raft_stir_host, m) {
   m.def("resize_bilinear(Tensor img, int oh, int ow, float fy=0., float fx=0.) -> Tensor", &resize_bilinear);
   m.def("color_jitter(Tensor img, float brightness, float contrast, float saturation, float hue, int[] order) -> Tensor",
         &color_jitter);
+  m.def("resize_crop(Tensor img, int oh, int ow, float fy, float fx, int y0, int x0, int ch, int cw, bool hflip, "
+        "bool vflip, float[] mul) -> Tensor", &resize_crop);
   m.def("sparse_flow_resize(Tensor flow, Tensor valid, float fx, float fy) -> Tensor[]", &sparse_flow_resize);
 }

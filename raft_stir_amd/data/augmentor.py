@@ -165,7 +165,7 @@ def _erase(img1, img2, prob, bounds=(50, 100)):
     ht, wd = img1.shape[:2]
     if np.random.rand() < prob:
         img2 = img2.copy()
-        mean_color = np.mean(img2.reshape(-1, 3), axis=0)
+        mean_color = img2.reshape(-1, 3).sum(0, dtype=np.int64) / (img2.size // 3)
         for _ in range(np.random.randint(1, 3)):
             x0 = np.random.randint(0, wd)
             y0 = np.random.randint(0, ht)
@@ -211,21 +211,37 @@ class FlowAugmentor:
             scale_y *= 2 ** np.random.uniform(-self.max_stretch, self.max_stretch)
         scale_x = float(np.clip(scale_x, min_scale, None))
         scale_y = float(np.clip(scale_y, min_scale, None))
-        if np.random.rand() < self.spatial_aug_prob:
+        # the draws in the reference's order (scale, stretch, resize?, flips,
+        # crop); the crop offsets depend only on the resized SIZE, so the
+        # native path resizes just the crop window (csrc_host resize_crop)
+        resize = np.random.rand() < self.spatial_aug_prob
+        hflip = vflip = False
+        if self.do_flip:
+            hflip = np.random.rand() < self.h_flip_prob
+            vflip = np.random.rand() < self.v_flip_prob
+        oh, ow = (int(round(ht * scale_y)), int(round(wd * scale_x))) if resize else (ht, wd)
+        y0 = np.random.randint(0, oh - self.crop_size[0])
+        x0 = np.random.randint(0, ow - self.crop_size[1])
+        ch, cw = self.crop_size
+        ops = _host_ops()
+        if resize and ops is not None and hasattr(ops, "resize_crop"):
+            sgn = (-1.0 if hflip else 1.0, -1.0 if vflip else 1.0)
+            rc = lambda a, mul: ops.resize_crop(torch.from_numpy(np.ascontiguousarray(a)), oh, ow, scale_y, scale_x,
+                                                int(y0), int(x0), ch, cw, hflip, vflip, mul).numpy()
+            return (rc(img1, []), rc(img2, []),
+                    rc(flow.astype(np.float32), [scale_x * sgn[0], scale_y * sgn[1]]))
+        if resize:
             img1 = _resize(img1, scale_x, scale_y)
             img2 = _resize(img2, scale_x, scale_y)
             flow = _resize(flow.astype(np.float32), scale_x, scale_y)
             flow = flow * np.array([scale_x, scale_y], np.float32)
-        if self.do_flip:
-            if np.random.rand() < self.h_flip_prob:
-                img1, img2 = img1[:, ::-1], img2[:, ::-1]
-                flow = flow[:, ::-1] * np.array([-1.0, 1.0], np.float32)
-            if np.random.rand() < self.v_flip_prob:
-                img1, img2 = img1[::-1, :], img2[::-1, :]
-                flow = flow[::-1, :] * np.array([1.0, -1.0], np.float32)
-        y0 = np.random.randint(0, img1.shape[0] - self.crop_size[0])
-        x0 = np.random.randint(0, img1.shape[1] - self.crop_size[1])
-        sl = (slice(y0, y0 + self.crop_size[0]), slice(x0, x0 + self.crop_size[1]))
+        if hflip:
+            img1, img2 = img1[:, ::-1], img2[:, ::-1]
+            flow = flow[:, ::-1] * np.array([-1.0, 1.0], np.float32)
+        if vflip:
+            img1, img2 = img1[::-1, :], img2[::-1, :]
+            flow = flow[::-1, :] * np.array([1.0, -1.0], np.float32)
+        sl = (slice(y0, y0 + ch), slice(x0, x0 + cw))
         return img1[sl], img2[sl], flow[sl]
 
     def __call__(self, img1, img2, flow):

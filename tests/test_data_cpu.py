@@ -313,3 +313,33 @@ def test_packaged_chairs_split(tmp_path, monkeypatch):
     ref = "/root/reference/chairs_split.txt"
     if os.path.exists(ref):
         assert np.array_equal(s, np.loadtxt(ref, dtype=np.int32))
+
+
+def test_fused_resize_crop_matches_resize_then_crop(monkeypatch):
+    """FlowAugmentor.spatial_transform's native crop-window resize
+    (csrc_host resize_crop) is bitwise the full resize + flips + crop."""
+    from raft_stir_amd.data import frame_utils
+    rs = np.random.RandomState(7)
+    img1 = rs.randint(0, 255, (96, 128, 3)).astype(np.uint8)
+    img2 = rs.randint(0, 255, (96, 128, 3)).astype(np.uint8)
+    flow = rs.randn(96, 128, 2).astype(np.float32) * 5
+    a = aug.FlowAugmentor((64, 80), min_scale=-0.2, max_scale=0.8, do_flip=True)
+    a.h_flip_prob = a.v_flip_prob = 0.5
+    ops = frame_utils._host_ops()
+    if ops is None or not hasattr(ops, "resize_crop"):
+        pytest.skip("native host ops not built")
+
+    class NoFused:  # the host ops minus resize_crop
+        def __getattr__(self, k):
+            if k == "resize_crop":
+                raise AttributeError(k)
+            return getattr(ops, k)
+    for seed in range(12):
+        np.random.seed(seed)
+        got = a.spatial_transform(img1, img2, flow)
+        monkeypatch.setattr(aug, "_host_ops", lambda: NoFused())
+        np.random.seed(seed)
+        want = a.spatial_transform(img1, img2, flow)
+        monkeypatch.undo()
+        for g, w in zip(got, want):
+            assert g.shape == w.shape and np.array_equal(np.ascontiguousarray(g), np.ascontiguousarray(w)), seed
