@@ -27,7 +27,7 @@ class RAFTConfig:
     fnet_dim: int = 256
     # engine knobs (not in the reference): kernel choices for the GPU path
     fused_gru: bool = True             # fused HIP gate kernels in the ConvGRU
-    fused_train: bool = True           # whole-loop fused training engine (RAFT / RAFT-small, bf16)
+    fused_train: bool = True           # whole-loop fused training engine (RAFT / RAFT-small, bf16 or fp32)
     overlap_encoders: bool = True      # context encoder on a second HIP stream (GPU)
     # storage dtype of the all-pairs pyramid: "float32" (reference, core/corr.py:58),
     # "bfloat16" (half the volume bytes; needs bf16 autocast features), or "auto"

@@ -942,28 +942,32 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(Args a) {
 //   dq_pre = dh' z (1 - q~^2)        -> dq (bf16, the q-conv dgrad/wgrad operand)
 //   dz_pre = dh' (q~ - h) z (1 - z)  -> dzr[:, 0:hd] (bf16)
 //   dh    <- dh' (1 - z)             (fp32, in place; the conv dgrads add to it)
-__global__ __launch_bounds__(256) void gru_gate_bwd_kernel(float* __restrict__ dh, int dhstr, const bf16_t* __restrict__ z,
-                                                           int zstr, const bf16_t* __restrict__ q, int qstr,
-                                                           const bf16_t* __restrict__ h, int hstr, int hoff,
-                                                           bf16_t* __restrict__ dq, int dqstr,
-                                                           bf16_t* __restrict__ dzr, int dzrstr, long P, int hd) {
+// T: the activations' type (bf16, or fp32 in the fp32 training engine).
+template <typename T>
+__global__ __launch_bounds__(256) void gru_gate_bwd_kernel(float* __restrict__ dh, int dhstr, const T* __restrict__ z,
+                                                           int zstr, const T* __restrict__ q, int qstr,
+                                                           const T* __restrict__ h, int hstr, int hoff,
+                                                           T* __restrict__ dq, int dqstr,
+                                                           T* __restrict__ dzr, int dzrstr, long P, int hd) {
   const long total = P * hd;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long p = i / hd;
     const int c = (int)(i - p * hd);
     const float g = dh[p * dhstr + c];
-    const float zv = bf2f(z[p * zstr + c]), qv = bf2f(q[p * qstr + c]), hv = bf2f(h[p * hstr + hoff + c]);
-    dq[p * dqstr + c] = f2bf(g * zv * (1.f - qv * qv));
-    dzr[p * dzrstr + c] = f2bf(g * (qv - hv) * zv * (1.f - zv));
+    const float zv = io<T>::ld(z + p * zstr + c), qv = io<T>::ld(q + p * qstr + c);
+    const float hv = io<T>::ld(h + p * hstr + hoff + c);
+    io<T>::st(dq + p * dqstr + c, g * zv * (1.f - qv * qv));
+    io<T>::st(dzr + p * dzrstr + c, g * (qv - hv) * zv * (1.f - zv));
     dh[p * dhstr + c] = g * (1.f - zv);
   }
 }
 
-// Motion-encoder output gradient: d = G[:, off:off+n] * (act > 0) -> out (bf16, width
+// Motion-encoder output gradient: d = G[:, off:off+n] * (act > 0) -> out (T, width
 // ostr, channels >= n zeroed), then G[:, off:off+nz] = 0 (consumed).
+template <typename T>
 __global__ __launch_bounds__(256) void relu_take_kernel(float* __restrict__ G, int gstr, int goff, int n, int nz,
-                                                        const bf16_t* __restrict__ act, int astr, int aoff,
-                                                        bf16_t* __restrict__ out, int ostr, long P) {
+                                                        const T* __restrict__ act, int astr, int aoff,
+                                                        T* __restrict__ out, int ostr, long P) {
   const long total = P * ostr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long p = i / ostr;
@@ -971,9 +975,9 @@ __global__ __launch_bounds__(256) void relu_take_kernel(float* __restrict__ G, i
     float v = 0.f;
     if (c < n) {
       const float g = G[p * gstr + goff + c];
-      v = bf2f(act[p * astr + aoff + c]) > 0.f ? g : 0.f;
+      v = io<T>::ld(act + p * astr + aoff + c) > 0.f ? g : 0.f;
     }
-    out[i] = f2bf(v);
+    io<T>::st(out + i, v);
     if (c < nz) G[p * gstr + goff + c] = 0.f;
   }
 }
@@ -1083,7 +1087,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     else hipLaunchKernelGGL((conv::conv_halo_kernel<128, 4, 128>), grid, dim3(256), 0, stream, a);
     return;
   }
-  if (L.tile >= 42 && L.tile <= 47) {  // lean unrolled-tap tiles (conv_v2.hip)
+  if (L.tile >= 42 && L.tile <= 50) {  // lean unrolled-tap tiles (conv_v2.hip)
     conv_v2_launch(a, L.tile, stream);
     return;
   }
@@ -1175,18 +1179,28 @@ static int egrid(long total) {
 }
 
 void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
-                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd,
+                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd, bool f32,
                          hipStream_t stream) {
-  hipLaunchKernelGGL(conv::gru_gate_bwd_kernel, dim3(egrid(P * hd)), dim3(256), 0, stream, dh, dhstr,
-                     static_cast<const bf16_t*>(z), zstr, static_cast<const bf16_t*>(q), qstr,
-                     static_cast<const bf16_t*>(h), hstr, hoff, static_cast<bf16_t*>(dq), dqstr,
-                     static_cast<bf16_t*>(dzr), dzrstr, P, hd);
+  if (f32)
+    hipLaunchKernelGGL(conv::gru_gate_bwd_kernel<float>, dim3(egrid(P * hd)), dim3(256), 0, stream, dh, dhstr,
+                       static_cast<const float*>(z), zstr, static_cast<const float*>(q), qstr,
+                       static_cast<const float*>(h), hstr, hoff, static_cast<float*>(dq), dqstr,
+                       static_cast<float*>(dzr), dzrstr, P, hd);
+  else
+    hipLaunchKernelGGL(conv::gru_gate_bwd_kernel<bf16_t>, dim3(egrid(P * hd)), dim3(256), 0, stream, dh, dhstr,
+                       static_cast<const bf16_t*>(z), zstr, static_cast<const bf16_t*>(q), qstr,
+                       static_cast<const bf16_t*>(h), hstr, hoff, static_cast<bf16_t*>(dq), dqstr,
+                       static_cast<bf16_t*>(dzr), dzrstr, P, hd);
 }
 
 void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* act, int astr, int aoff, void* out,
-                      int ostr, long P, hipStream_t stream) {
-  hipLaunchKernelGGL(conv::relu_take_kernel, dim3(egrid(P * ostr)), dim3(256), 0, stream, G, gstr, goff, n, nz,
-                     static_cast<const bf16_t*>(act), astr, aoff, static_cast<bf16_t*>(out), ostr, P);
+                      int ostr, long P, bool f32, hipStream_t stream) {
+  if (f32)
+    hipLaunchKernelGGL(conv::relu_take_kernel<float>, dim3(egrid(P * ostr)), dim3(256), 0, stream, G, gstr, goff, n,
+                       nz, static_cast<const float*>(act), astr, aoff, static_cast<float*>(out), ostr, P);
+  else
+    hipLaunchKernelGGL(conv::relu_take_kernel<bf16_t>, dim3(egrid(P * ostr)), dim3(256), 0, stream, G, gstr, goff, n,
+                       nz, static_cast<const bf16_t*>(act), astr, aoff, static_cast<bf16_t*>(out), ostr, P);
 }
 
 

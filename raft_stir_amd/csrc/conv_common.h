@@ -449,9 +449,10 @@ __device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)
 // ---------------------------------------------------------------- fp32 epilogues
 // The F32 tiles' epilogues: the forward kinds of the inference engine and
 // the encoders (bias / ReLU / scale, ConvGRU gates and update, eval-BN
-// EPI_NORM with residual) on fp32 NHWC outputs and aux inputs (every
-// "bf16_t*" of Args is read as float*), plus the normalisation statistics of
-// the unrounded output.
+// EPI_NORM with residual) and the dgrad kinds of the fp32 training engine
+// (ReLU backward, fp32 accumulation, the q-conv r-gate backward) on fp32 NHWC
+// outputs and aux inputs (every "bf16_t*" of Args is read as float*), plus
+// the normalisation statistics of the unrounded output.
 __device__ __forceinline__ void ld4f(const bf16_t* p, float (&f)[4]) {
   const float4 v = *reinterpret_cast<const float4*>(p);
   f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
@@ -494,6 +495,52 @@ __device__ __forceinline__ void epi_frag_f32(const Args& a, float (&v)[4], int c
       const float q = tanhf(v[j]);
       hn[j] = (1.f - z[j]) * h[j] + z[j] * q;
       if (qs) qs[j] = q;
+    }
+  } else if constexpr (E == EPI_RELU_BWD) {  // out = v * (act > 0)
+    const float* act = fi(a.aux1, a.a1str, a.a1off, p, cb);
+    float* o = fo(a.out, a.ostr, a.ooff, p, cb);
+    if (vec && full) {
+      const float4 av = *reinterpret_cast<const float4*>(act);
+      *reinterpret_cast<float4*>(o) = make_float4(av.x > 0.f ? v[0] : 0.f, av.y > 0.f ? v[1] : 0.f,
+                                                  av.z > 0.f ? v[2] : 0.f, av.w > 0.f ? v[3] : 0.f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] = act[j] > 0.f ? v[j] : 0.f;
+    }
+  } else if constexpr (E == EPI_ACC_F32) {  // out += v
+    float* o = fo(a.out, a.ostr, a.ooff, p, cb);
+    if (vec && full) {
+      acc4(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] += v[j];
+    }
+  } else if constexpr (E == EPI_GRU_QBWD) {  // as the bf16 form, fp32 dr_pre / h / r
+    float* o = fo(a.out, a.ostr, a.ooff, p, cb);
+    if (cb < a.hd) {
+      const float* h = fi(a.aux1, a.a1str, a.a1off, p, cb);
+      const float* r = fi(a.aux2, a.a2str, a.a2off, p, cb);
+      float* drp = fo(a.out2, a.o2str, a.o2off, p, cb);
+      float gv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        drp[j] = v[j] * h[j] * r[j] * (1.f - r[j]);
+        gv[j] = v[j] * r[j];
+      }
+      if (vec) {
+        acc4(o, gv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += gv[j];
+      }
+    } else if (vec && full) {
+      acc4(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (cb + j < a.Cout) o[j] += v[j];
     }
   } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE / EPI_NORM
 #pragma unroll
@@ -557,6 +604,9 @@ __device__ __forceinline__ void epilogue_pix_f32(const Args& a, const f32x4_t (&
   case E: epi_loop_f32<WM, WN, E>(a, acc, m0, lane, pp, pb); break
     RS_EPI32(EPI_GRU_ZR);
     RS_EPI32(EPI_GRU_Q);
+    RS_EPI32(EPI_RELU_BWD);
+    RS_EPI32(EPI_ACC_F32);
+    RS_EPI32(EPI_GRU_QBWD);
     RS_EPI32(EPI_RELU);
     RS_EPI32(EPI_SCALE);
     RS_EPI32(EPI_NORM);

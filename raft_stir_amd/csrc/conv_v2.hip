@@ -86,11 +86,11 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
   }
 }
 
-template <int KH, int KW, int NWM, int NWN, int S>
+template <int KH, int KW, int NWM, int NWN, int S, int MW = 1>
 struct V2 {
   static constexpr int T = KH * KW;
   static constexpr int NW = NWM * NWN, NT = 64 * NW;
-  static constexpr int BM = 32 * NWM;          // output channels per block
+  static constexpr int BM = 32 * NWM * MW;     // output channels per block (a wave: 32 MW)
   static constexpr int TH = 2 * NWN, TW = 32;  // pixel patch (a wave: 2 patch rows)
   static constexpr int HH = TH + KH - 1, HWD = TW + KW - 1;
   static constexpr int PPR = (HWD * 9 + 63) / 64;        // DMA pieces per halo row
@@ -127,9 +127,9 @@ struct V2 {
   }
 };
 
-template <int KH, int KW, int NWM, int NWN, int S>
+template <int KH, int KW, int NWM, int NWN, int S, int MW = 1>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
-  using C = V2<KH, KW, NWM, NWN, S>;
+  using C = V2<KH, KW, NWM, NWN, S, MW>;
   constexpr int T = C::T, NW = C::NW, NT = C::NT, BM = C::BM, TH = C::TH, TW = C::TW;
   constexpr int HWD = C::HWD, PPR = C::PPR, NHP = C::NHP, NHPW = C::NHPW, HSL = C::HSL;
   constexpr int ROWSL = C::ROWSL, ASL = C::ASL, NAPW = C::NAPW, NTH = C::NTH;
@@ -231,12 +231,14 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
   // ---- fragment read addresses (bytes, LDS)
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0];
   const int h = lane >> 5, l32 = lane & 31;
-  uint32_t aro[4];  // A row (wm*32 + l32), chunk 2ks+h, XOR-swizzled; + slot base at read time
+  uint32_t aro[MW][4];  // A row (wm*32*MW + mw*32 + l32), chunk 2ks+h, XOR-swizzled; + slot base at read time
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int r = wm * 32 + l32;
-    aro[ks] = lds0 + (uint32_t)(r * 128 + (((2 * ks + h) ^ ((r >> 1) & 7)) * 16));
-  }
+  for (int mw = 0; mw < MW; ++mw)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int r = (wm * MW + mw) * 32 + l32;
+      aro[mw][ks] = lds0 + (uint32_t)(r * 128 + (((2 * ks + h) ^ ((r >> 1) & 7)) * 16));
+    }
   uint32_t bro[2][2];  // [halo buffer][n-block]: halo pixel (patch row, column l32), chunk h
 #pragma unroll
   for (int hb = 0; hb < 2; ++hb)
@@ -244,31 +246,42 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
     for (int nb = 0; nb < 2; ++nb)
       bro[hb][nb] = lds0 + (uint32_t)((S * ASL + hb * HSL + (wn * 2 + nb) * ROWSL + l32 * 9 + h) * 16);
 
-  f32x16_t acc[2];
+  f32x16_t acc[MW][2];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
+  for (int mw = 0; mw < MW; ++mw)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[nb][j] = 0.f;
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[mw][nb][j] = 0.f;
 
-  u32x4_t F[2][3];  // [buffer][A, B0, B1]
+  u32x4_t F[2][MW + 2];  // [buffer][A_0 .. A_MW-1, B0, B1]
   // read the K=16 slice ks of tap TAP from weight slot SL and halo buffer HB into F[FB]
 #define RS_READ(FB, SL, HB, TAP, KS)                                                         \
   do {                                                                                       \
     constexpr int toff_ = (((TAP) / KW) * ROWSL + ((TAP) % KW) * 9 + 2 * (KS)) * 16;         \
-    asm volatile("ds_read_b128 %0, %1" : "=v"(F[FB][0]) : "v"(aro[KS] + (SL) * ASL * 16) : "memory"); \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(F[FB][1]) : "v"(bro[HB][0]), "i"(toff_) : "memory"); \
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(F[FB][2]) : "v"(bro[HB][1]), "i"(toff_) : "memory"); \
+    asm volatile("ds_read_b128 %0, %1" : "=v"(F[FB][0]) : "v"(aro[0][KS] + (SL) * ASL * 16) : "memory"); \
+    if constexpr (MW > 1)                                                                    \
+      asm volatile("ds_read_b128 %0, %1" : "=v"(F[FB][1]) : "v"(aro[1][KS] + (SL) * ASL * 16) : "memory"); \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(F[FB][MW]) : "v"(bro[HB][0]), "i"(toff_) : "memory"); \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(F[FB][MW + 1]) : "v"(bro[HB][1]), "i"(toff_) : "memory"); \
   } while (0)
+#define RS_MMA1(FB, MI, NB)                                                                  \
+  acc[MI][NB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, F[FB][MI]),  \
+                                                        __builtin_bit_cast(bf16x8_t, F[FB][MW + (NB)]), \
+                                                        acc[MI][NB], 0, 0, 0)
 #define RS_MMA(FB)                                                                           \
   do {                                                                                       \
-    acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, F[FB][0]),   \
-                                                     __builtin_bit_cast(bf16x8_t, F[FB][1]), acc[0], 0, 0, 0); \
-    acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, F[FB][0]),   \
-                                                     __builtin_bit_cast(bf16x8_t, F[FB][2]), acc[1], 0, 0, 0); \
+    RS_MMA1(FB, 0, 0);                                                                       \
+    RS_MMA1(FB, 0, 1);                                                                       \
+    if constexpr (MW > 1) {                                                                  \
+      RS_MMA1(FB, 1, 0);                                                                     \
+      RS_MMA1(FB, 1, 1);                                                                     \
+    }                                                                                        \
   } while (0)
 #define RS_FENCE(FB)                                                                         \
   do {                                                                                       \
-    asm volatile("" : "+v"(F[FB][0]), "+v"(F[FB][1]), "+v"(F[FB][2]));                       \
+    asm volatile("" : "+v"(F[FB][0]), "+v"(F[FB][MW]), "+v"(F[FB][MW + 1]));                 \
+    if constexpr (MW > 1) asm volatile("" : "+v"(F[FB][1]));                                  \
   } while (0)
 
   // ---- prologue: chunk-0 halo, groups 0 .. S-1 (all in chunk 0 since S <= T)
@@ -323,6 +336,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
     RS_KS(TT, 3);                                                                            \
   }
   static_assert(T <= 9, "taps");
+  static_assert(MW == 1 || MW == 2, "MW");
   int slot0 = 0;
   for (int c = 0; c < nchunks; ++c) {
     const int hb = c & 1;
@@ -333,6 +347,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
 #undef RS_KS
 #undef RS_FENCE
 #undef RS_MMA
+#undef RS_MMA1
 #undef RS_READ
 #undef RS_ISSUE_H
 #undef RS_ISSUE_A
@@ -353,7 +368,8 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
       py[nb] = px[nb] = pp[nb] = 0;
     }
   }
-  epilogue32<2>(a, acc, bm0 + wm * 32, lane, pp, pb, py, px);
+  epilogue32<2>(a, acc[0], bm0 + wm * MW * 32, lane, pp, pb, py, px);
+  if constexpr (MW > 1) epilogue32<2>(a, acc[1], bm0 + (wm * MW + 1) * 32, lane, pp, pb, py, px);
 }
 
 }  // namespace conv
@@ -361,9 +377,12 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_v2_kernel(Args a) {
 bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream) {
   // tile 42: 2x2 waves (64 Cout x 4x32 px, 4-slot ring); 43: 1x4 (32 x 8x32);
   // 44: 4x1 (128 x 2x32); 45 / 46 / 47: 2x2 with a 3 / 5 / 6-slot ring (47: 5 for 5 taps)
-  const int nwm = tile == 43 ? 1 : tile == 44 ? 4 : 2;
-  const int nwn = tile == 43 ? 4 : tile == 44 ? 1 : 2;
-  const int BM = 32 * nwm, TH = 2 * nwn;
+  // 48 / 49: 2x2 waves of 64 Cout x 2x32 px (two A fragments per wave, 128 Cout x 4x32 px
+  // per block; 3 / 2-slot ring); 50: 4x1 waves of 64 x 2x32 (256 Cout x 2x32 px, 3 slots)
+  const int mw = tile >= 48 ? 2 : 1;
+  const int nwm = tile == 43 ? 1 : (tile == 44 || tile == 50) ? 4 : 2;
+  const int nwn = tile == 43 ? 4 : (tile == 44 || tile == 50) ? 1 : 2;
+  const int BM = 32 * nwm * mw, TH = 2 * nwn;
   const dim3 grid(cdiv(a.Cout, BM) * a.B * cdiv(a.H, TH) * cdiv(a.W, 32));
   const dim3 block(64 * nwm * nwn);
 #define RS_V2(KH_, KW_)                                                                                  \
@@ -373,6 +392,9 @@ bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream) {
     case 44: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 4, 1, 4>), grid, block, 0, stream, a); break; \
     case 46: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, 5>), grid, block, 0, stream, a); break; \
     case 47: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, (KH_ * KW_ >= 6 ? 6 : 5)>), grid, block, 0, stream, a); break; \
+    case 48: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, 3, 2>), grid, block, 0, stream, a); break; \
+    case 49: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, 2, 2>), grid, block, 0, stream, a); break; \
+    case 50: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 4, 1, 3, 2>), grid, block, 0, stream, a); break; \
     default: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, 3>), grid, block, 0, stream, a); break; \
   }
   if (a.KH == 3 && a.KW == 3) {

@@ -526,8 +526,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 // row with a 7-wide sliding window in registers (1 LDS read + 1 dF read per
 // 7 FMAs) and keeps 49 tap accumulators; one atomic per output per block.
 constexpr int FROWS = 8;
+template <typename T>  // dF: bf16, or fp32 (the fp32 training engine)
 __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict__ coords, int Bp, int H, int W,
-                                                         const bf16_t* __restrict__ df, int fstr, int Cout,
+                                                         const T* __restrict__ df, int fstr, int Cout,
                                                          float* __restrict__ dw, float* __restrict__ db,
                                                          float* __restrict__ part) {
   extern __shared__ float fl[];  // [2][FROWS + 6][W + 6]
@@ -551,7 +552,7 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
     for (int i = 0; i < 49; ++i) acc[i] = 0.f;
     float bsum = 0.f;
     for (int r = 0; r < FROWS && y0 + r < H; ++r) {
-      const bf16_t* grow = df + ((size_t)b * HW + (size_t)(y0 + r) * W) * fstr + co;
+      const T* grow = df + ((size_t)b * HW + (size_t)(y0 + r) * W) * fstr + co;
       // x outer, taps inner: each dY value is loaded once and feeds 49 FMAs;
       // the 7 padded flow rows slide through registers (win[ky][kx] = flow
       // at (y0 + r + ky - 3, x + kx - 3))
@@ -561,7 +562,7 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
 #pragma unroll
         for (int kx = 0; kx < 6; ++kx) win[ky][kx] = F[(r + ky) * WP + kx];
       for (int x = 0; x < W; ++x) {
-        const float g = bf2f(grow[(size_t)x * fstr]);
+        const float g = io<T>::ld(grow + (size_t)x * fstr);
         bsum += g;
 #pragma unroll
         for (int ky = 0; ky < 7; ++ky) win[ky][6] = F[(r + ky) * WP + x + 6];
@@ -744,11 +745,15 @@ void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, 
 int flow_wgrad_blocks(int Bp, int H) { return Bp * cdiv(H, wgrad::FROWS); }
 
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
-                       float* db, float* part, hipStream_t stream) {
+                       float* db, float* part, bool f32, hipStream_t stream) {
   const int blocks = flow_wgrad_blocks(Bp, H);
   const size_t lds = sizeof(float) * 2 * (wgrad::FROWS + 6) * (W + 6);
-  hipLaunchKernelGGL(wgrad::flow_wgrad_kernel, dim3(blocks), dim3(256), lds, stream, coords, Bp, H, W,
-                     static_cast<const bf16_t*>(df), fstr, Cout, dw, db, part);
+  if (f32)
+    hipLaunchKernelGGL(wgrad::flow_wgrad_kernel<float>, dim3(blocks), dim3(256), lds, stream, coords, Bp, H, W,
+                       static_cast<const float*>(df), fstr, Cout, dw, db, part);
+  else
+    hipLaunchKernelGGL(wgrad::flow_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), lds, stream, coords, Bp, H, W,
+                       static_cast<const bf16_t*>(df), fstr, Cout, dw, db, part);
   if (part) {  // [blocks][98 * Cout | Cout] partials -> dw, db in block order
     const long st = 99L * Cout;
     hipLaunchKernelGGL(wgrad::det_reduce_kernel, dim3(cdiv(98 * Cout, 256)), dim3(256), 0, stream, part, blocks, st,

@@ -64,6 +64,14 @@ __device__ __forceinline__ void stc(bf16_t* p, const float (&f)[CPL]) {
   }
 }
 
+template <int CPL>
+__device__ __forceinline__ void stc(float* p, const float (&f)[CPL]) {
+  if constexpr (CPL == 4)
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  else
+    *reinterpret_cast<float2*>(p) = make_float2(f[0], f[1]);
+}
+
 // x: NHWC bf16 or fp32 (pixel stride xstr, channel offset xoff), w: fp32
 // [2][9][Cin], crd / src: (B, 2, H, W) fp32 (src may alias crd).
 template <int CPL, typename XT>
@@ -157,13 +165,14 @@ __global__ __launch_bounds__(256) void flowhead_fwd_kernel(const XT* __restrict_
   }
 }
 
-// dflow: (B, 2, H, W) fp32; w: fp32 [2][9][Cin]; act: NHWC bf16 hidden (ReLU output,
-// stride astr, offset aoff); out: NHWC bf16 (stride ostr, offset ooff), Cin channels.
-template <int CPL>
+// dflow: (B, 2, H, W) fp32; w: fp32 [2][9][Cin]; act: NHWC T hidden (ReLU output,
+// stride astr, offset aoff); out: NHWC T (stride ostr, offset ooff), Cin channels;
+// T = bf16, or fp32 (the fp32 training engine).
+template <int CPL, typename T>
 __global__ __launch_bounds__(256) void flowhead_dgrad_kernel(const float* __restrict__ dflow,
                                                              const float* __restrict__ w, int B, int H, int W,
-                                                             const bf16_t* __restrict__ act, int astr, int aoff,
-                                                             bf16_t* __restrict__ out, int ostr, int ooff) {
+                                                             const T* __restrict__ act, int astr, int aoff,
+                                                             T* __restrict__ out, int ostr, int ooff) {
   constexpr int CIN = 64 * CPL;
   const int lane = threadIdx.x & 63;
   const int segs_row = cdiv(W, PX);
@@ -249,17 +258,28 @@ void flowhead_fwd_launch(const void* x, int xstr, int xoff, int cin, const float
 }
 
 void flowhead_dgrad_launch(const float* dflow, const float* w, int cin, int B, int H, int W, const void* act,
-                           int astr, int aoff, void* out, int ostr, int ooff, hipStream_t s) {
+                           int astr, int aoff, void* out, int ostr, int ooff, bool f32, hipStream_t s) {
   const int segs = B * H * cdiv(W, fh::PX);
   const dim3 grid(cdiv(segs, 4));
+  if (f32) {
+    const float* ab = static_cast<const float*>(act);
+    float* ob = static_cast<float*>(out);
+    if (cin == 256)
+      hipLaunchKernelGGL((fh::flowhead_dgrad_kernel<4, float>), grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr,
+                         aoff, ob, ostr, ooff);
+    else
+      hipLaunchKernelGGL((fh::flowhead_dgrad_kernel<2, float>), grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr,
+                         aoff, ob, ostr, ooff);
+    return;
+  }
   const bf16_t* ab = static_cast<const bf16_t*>(act);
   bf16_t* ob = static_cast<bf16_t*>(out);
   if (cin == 256)
-    hipLaunchKernelGGL(fh::flowhead_dgrad_kernel<4>, grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr, aoff, ob,
-                       ostr, ooff);
+    hipLaunchKernelGGL((fh::flowhead_dgrad_kernel<4, bf16_t>), grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr,
+                       aoff, ob, ostr, ooff);
   else
-    hipLaunchKernelGGL(fh::flowhead_dgrad_kernel<2>, grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr, aoff, ob,
-                       ostr, ooff);
+    hipLaunchKernelGGL((fh::flowhead_dgrad_kernel<2, bf16_t>), grid, dim3(256), 0, s, dflow, w, B, H, W, ab, astr,
+                       aoff, ob, ostr, ooff);
 }
 
 }  // namespace rs

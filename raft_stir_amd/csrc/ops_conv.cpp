@@ -71,12 +71,12 @@ void flow_enc_launch(const float* coords, int B, int H, int W, const float* w, c
 void flowhead_fwd_launch(const void* x, int xstr, int xoff, int cin, const float* w, const float* bias, int B,
                          int H, int W, float* crd, const float* src, bool x_f32, hipStream_t s);
 void flowhead_dgrad_launch(const float* dflow, const float* w, int cin, int B, int H, int W, const void* act,
-                           int astr, int aoff, void* out, int ostr, int ooff, hipStream_t s);
+                           int astr, int aoff, void* out, int ostr, int ooff, bool f32, hipStream_t s);
 void gru_gate_bwd_launch(float* dh, int dhstr, const void* z, int zstr, const void* q, int qstr, const void* h,
-                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd,
+                         int hstr, int hoff, void* dq, int dqstr, void* dzr, int dzrstr, long P, int hd, bool f32,
                          hipStream_t stream);
 void relu_take_launch(float* G, int gstr, int goff, int n, int nz, const void* act, int astr, int aoff, void* out,
-                      int ostr, long P, hipStream_t stream);
+                      int ostr, long P, bool f32, hipStream_t stream);
 struct WgradLaunch {
   const void* dy;
   int ystr, yoff, Cout;
@@ -97,7 +97,7 @@ int colsum_blocks(int P);
 void colsum_launch(const void* dy, int ystr, int yoff, int C, int P, float* db, float* part, hipStream_t stream);
 int flow_wgrad_blocks(int Bp, int H);
 void flow_wgrad_launch(const float* coords, int Bp, int H, int W, const void* df, int fstr, int Cout, float* dw,
-                       float* db, float* part, hipStream_t stream);
+                       float* db, float* part, bool f32, hipStream_t stream);
 bool deterministic();
 bool enc_halo_launch(const uint16_t* x, int xstr, const uint16_t* w, int Ktot, uint16_t* y, int ystr, int B, int H,
                      int W, int cin, int cout, int num_cus, const EncEpi& e, hipStream_t stream);
@@ -191,8 +191,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   if (f32) {
     TORCH_CHECK(tile == 6 || tile == 7 || tile == 8 || (tile >= 38 && tile <= 40),
                 "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40 only");
-    TORCH_CHECK(epi == 0 || epi == 1 || epi == 2 || epi == EPI_GRU_ZR || epi == EPI_GRU_Q || epi == EPI_NORM,
-                "conv_fused: fp32 activations support the forward epilogues (bias, relu, scale, gru_zr, gru_q, norm)");
+    TORCH_CHECK(epi != EPI_FLOW, "conv_fused: fp32 activations: no flow epilogue (csrc/flowhead.hip serves it)");
   }
   L.f32 = f32 ? 1 : 0;
   int Ktot = 0;
@@ -219,10 +218,10 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 47, "conv_fused: tile must be in [0,47]");
-  if (tile >= 42 && tile <= 47)
+  TORCH_CHECK(tile >= 0 && tile <= 50, "conv_fused: tile must be in [0,50]");
+  if (tile >= 42 && tile <= 50)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
-                "conv_fused: tiles 42-45 are instantiated for 3x3, 1x5 and 5x1 kernels only");
+                "conv_fused: tiles 42-50 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
   TORCH_CHECK(!(tile >= 38 && tile <= 40) || f32, "conv_fused: tiles 38-40 are the fp32 split-K tiles");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
@@ -234,7 +233,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                      tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26 || tile == 36 ||
                      tile == 39;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
-  const int tileM = (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
+  const int tileM = (tile == 48 || tile == 49) ? 128 : tile == 50 ? 256
+                    : (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
                     : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
                     : tile == 29 ? 192
@@ -309,8 +309,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
   if (nx.stats || nx.chs)
-    TORCH_CHECK(!(tile >= 42 && tile <= 47),
-                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-47)");
+    TORCH_CHECK(!(tile >= 42 && tile <= 50),
+                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-50)");
   L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();
@@ -468,8 +468,9 @@ void flow_head_dgrad(const Tensor& dflow, const Tensor& w, int64_t cin, const Te
                   dflow.size(1) == 2,
               "flow_head_dgrad: dflow must be contiguous fp32 (B,2,H,W)");
   const int B = dflow.size(0), H = dflow.size(2), W = dflow.size(3);
-  check_nhwc(act, B, H, W, "act");
-  check_nhwc(out, B, H, W, "out");
+  const bool f32 = out.scalar_type() == at::kFloat;  // fp32 training engine
+  check_nhwc(act, B, H, W, "act", f32 ? at::kFloat : at::kBFloat16);
+  check_nhwc(out, B, H, W, "out", f32 ? at::kFloat : at::kBFloat16);
   const int vn = cin == 256 ? 4 : 2;
   TORCH_CHECK(aoff >= 0 && aoff + cin <= act.size(3) && aoff % vn == 0 && act.size(3) % vn == 0,
               "flow_head_dgrad: act channel window");
@@ -479,7 +480,7 @@ void flow_head_dgrad(const Tensor& dflow, const Tensor& w, int64_t cin, const Te
               "flow_head_dgrad: w must be fp32 [2][3][3][Cin]");
   const c10::DeviceGuard guard(dflow.device());
   rs::flowhead_dgrad_launch(dflow.data_ptr<float>(), w.data_ptr<float>(), cin, B, H, W, act.data_ptr(), act.size(3),
-                            aoff, out.data_ptr(), out.size(3), ooff, stream());
+                            aoff, out.data_ptr(), out.size(3), ooff, f32, stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -681,9 +682,10 @@ void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const 
                   coords.size(1) == 2,
               "flow_wgrad: coords fp32 (B',2,H,W)");
   const int Bp = coords.size(0), H = coords.size(2), W = coords.size(3);
-  TORCH_CHECK(df.is_cuda() && df.is_contiguous() && df.scalar_type() == at::kBFloat16 && df.dim() == 4 &&
+  const bool f32 = df.scalar_type() == at::kFloat;  // fp32 training engine
+  TORCH_CHECK(df.is_cuda() && df.is_contiguous() && (f32 || df.scalar_type() == at::kBFloat16) && df.dim() == 4 &&
                   df.size(0) == Bp && df.size(1) == H && df.size(2) == W,
-              "flow_wgrad: df bf16 (B',H,W,C)");
+              "flow_wgrad: df bf16 / fp32 (B',H,W,C)");
   const int Cout = db.numel();
   TORCH_CHECK(Cout <= df.size(3) && Cout <= 128 && dw.numel() == 98 * Cout && dw.scalar_type() == at::kFloat &&
                   db.scalar_type() == at::kFloat,
@@ -695,7 +697,7 @@ void flow_wgrad(const Tensor& coords, const Tensor& df, const Tensor& dw, const 
   if (rs::deterministic())
     part = at::empty({int64_t(rs::flow_wgrad_blocks(Bp, H)) * 99 * Cout}, coords.options());
   rs::flow_wgrad_launch(coords.data_ptr<float>(), Bp, H, W, df.data_ptr(), df.size(3), Cout, dw.data_ptr<float>(),
-                        db.data_ptr<float>(), part.defined() ? part.data_ptr<float>() : nullptr, stream());
+                        db.data_ptr<float>(), part.defined() ? part.data_ptr<float>() : nullptr, f32, stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -709,14 +711,18 @@ void gru_gate_bwd(const Tensor& dh, const Tensor& z, const Tensor& q, const Tens
                     t.size(-1) >= minc,
                 "gru_gate_bwd: ", n);
   };
+  const bool f32 = z.scalar_type() == at::kFloat;  // fp32 training engine
+  const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
   chk(dh, at::kFloat, hd, "dh (fp32)");
-  chk(q, at::kBFloat16, hd, "q");
-  chk(h, at::kBFloat16, hoff + hd, "h");
-  chk(dq, at::kBFloat16, hd, "dq");
-  chk(dzr, at::kBFloat16, hd, "dzr");
+  chk(z, adt, hd, "z");
+  chk(q, adt, hd, "q");
+  chk(h, adt, hoff + hd, "h");
+  chk(dq, adt, hd, "dq");
+  chk(dzr, adt, hd, "dzr");
   const c10::DeviceGuard guard(z.device());
   rs::gru_gate_bwd_launch(dh.data_ptr<float>(), dh.size(-1), z.data_ptr(), hd, q.data_ptr(), q.size(-1), h.data_ptr(),
-                          h.size(-1), hoff, dq.data_ptr(), dq.size(-1), dzr.data_ptr(), dzr.size(-1), P, hd, stream());
+                          h.size(-1), hoff, dq.data_ptr(), dq.size(-1), dzr.data_ptr(), dzr.size(-1), P, hd, f32,
+                          stream());
   RS_CHECK_LAUNCH();
 }
 
@@ -726,13 +732,15 @@ void relu_take(const Tensor& G, int64_t goff, int64_t n, int64_t nz, const Tenso
   TORCH_CHECK(G.is_cuda() && G.is_contiguous() && G.scalar_type() == at::kFloat && G.numel() / G.size(-1) == P &&
                   goff + std::max(n, nz) <= G.size(-1),
               "relu_take: G");
-  TORCH_CHECK(act.is_contiguous() && act.scalar_type() == at::kBFloat16 && act.numel() / act.size(-1) == P &&
+  const bool f32 = out.scalar_type() == at::kFloat;  // fp32 training engine
+  const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
+  TORCH_CHECK(act.is_contiguous() && act.scalar_type() == adt && act.numel() / act.size(-1) == P &&
                   aoff + n <= act.size(-1),
-              "relu_take: act");
-  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kBFloat16 && n <= out.size(-1), "relu_take: out");
+              "relu_take: act (the out dtype)");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == adt && n <= out.size(-1), "relu_take: out");
   const c10::DeviceGuard guard(out.device());
   rs::relu_take_launch(G.data_ptr<float>(), G.size(-1), goff, n, nz, act.data_ptr(), act.size(-1), aoff, out.data_ptr(),
-                       out.size(-1), P, stream());
+                       out.size(-1), P, f32, stream());
   RS_CHECK_LAUNCH();
 }
 

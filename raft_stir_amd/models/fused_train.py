@@ -1,4 +1,6 @@
-"""Fused TRAINING engine for the RAFT refinement loop (full RAFT, bf16).
+"""Fused TRAINING engine for the RAFT refinement loop (RAFT and RAFT-small; bf16
+under --mixed_precision, fp32 otherwise -- the reference's standard schedule,
+/root/reference/train_standard.sh:3-6).
 
 One ``torch.autograd.Function`` covers the whole 12-iteration refinement
 loop of reference core/raft.py:122-139 (update block of core/update.py).
@@ -42,6 +44,15 @@ and 12 accumulations, and every bias gradient one column sum.
 Numerics: bf16 operands, fp32 accumulation everywhere, fp32 gradient
 accumulators for the recurrent state -- the same contract as the reference's
 autocast training (which used fp16).
+
+fp32 (``cfg.mixed_precision`` off): every activation / gradient slot is fp32;
+the convolutions (forward and dgrad) run on the split-bf16 F32 tiles of
+csrc/conv.hip (x = xh + xl, w = wh + wl, x.w ~= xh.wh + xl.wh + xh.wl: relative
+error ~2^-17) with the packed weights in their [wh | wl] layout, and each
+weight gradient is the same bf16 MFMA GEMM run on the three split products
+(dYh.Xh + dYl.Xh + dYh.Xl, bias gradient from dYh + dYl).  The gate, ReLU,
+flow-head, flow-encoder, lookup and upsampling kernels run their fp32
+instantiations.
 """
 from __future__ import annotations
 
@@ -160,6 +171,9 @@ class FusedTrainEngine:
             self.convs = [self.c1, self.c2, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow, self.mask2]
         self.f1 = enc.convf1
         self.f1c = self.f1.weight.shape[0]
+        # fp32 training (the reference's default precision): fp32 slots, split-bf16 kernels
+        self.f32 = not bool(model.cfg.mixed_precision)
+        self.adt = torch.float32 if self.f32 else torch.bfloat16
         # parameter order handed to autograd (grads are returned in this order)
         self.params = []
         for pc in self.convs:
@@ -259,7 +273,8 @@ class FusedTrainEngine:
         code = code.to(torch.int32).to(dev)
         self._maps = dict(dev=dev, gather=gather.to(dev), nbf=nbf, layout=layout, scaled=scaled,
                           code_bf=code[:nbf], code_f32=code[nbf:], tab=None, tab_key=None,
-                          out_bf=torch.empty(nbf, dtype=torch.bfloat16, device=dev),
+                          # fp32 engine: the conv weights gathered in fp32, then split (pack)
+                          out_bf=torch.empty(nbf, dtype=torch.float32 if self.f32 else torch.bfloat16, device=dev),
                           out_f32=torch.empty(gather.numel() - nbf, dtype=torch.float32, device=dev),
                           glayout=glayout, gf1=gf1, gtotal=gtotal, ggather=torch.cat(gmaps).to(dev),
                           gscaled=gscaled, zero=torch.zeros(1, device=dev))
@@ -299,15 +314,23 @@ class FusedTrainEngine:
             v = src.index_select(0, M["gather"])
             for a, b, s in M["scaled"]:
                 v[a:b].mul_(s)
-            bf = v[:nbf].to(torch.bfloat16)
+            bf = v[:nbf] if self.f32 else v[:nbf].to(torch.bfloat16)
             vals = _Offset(v[nbf:], nbf)
+        k = 1
+        if self.f32:
+            # every packed layout's last dim is a multiple of 32: one split of the
+            # whole region into the F32 tiles' per-32-chunk [wh 32 | wl 32] rows
+            v32 = bf.view(-1, 1, 32)
+            hi = v32.to(torch.bfloat16)
+            bf = torch.cat([hi, (v32 - hi.float()).to(torch.bfloat16)], 1).view(-1)
+            k = 2
         ob, of = 0, nbf
         for pc, ws, wds, bs in M["layout"]:
             n = ws.numel()
-            pc.w = bf[ob:ob + n].view(ws)
+            pc.w = bf[k * ob:k * (ob + n)].view(ws[0], ws[1], k * ws[2])
             ob += n
             n = wds.numel()
-            pc.wd = bf[ob:ob + n].view(wds)
+            pc.wd = bf[k * ob:k * (ob + n)].view(wds[0], wds[1], k * wds[2])
             ob += n
             pc.b = vals[of:of + bs.numel()]
             of += bs.numel()
@@ -349,14 +372,15 @@ class FusedTrainEngine:
 
     @staticmethod
     def config_capable(cfg) -> bool:
-        """The configuration half of ``eligible`` (no tensors needed)."""
-        return bool(cfg.mixed_precision) and cfg.fused_gru and getattr(cfg, "fused_train", True)
+        """The configuration half of ``eligible`` (no tensors needed): bf16
+        (mixed precision) and fp32 training both run the fused engine."""
+        return bool(cfg.fused_gru) and getattr(cfg, "fused_train", True)
 
     @staticmethod
     def eligible(model, image, corr_fn) -> bool:
-        corr_ok = getattr(corr_fn, "state", None) is not None or (  # all-pairs pyramid, or on-the-fly
+        corr_ok = getattr(corr_fn, "state", None) is not None or (  # all-pairs pyramid, or on-the-fly (bf16)
             getattr(corr_fn, "f2s", None) is not None and corr_fn.radius == (3 if model.cfg.small else 4)
-            and len(corr_fn.f2s) == 4 and corr_fn.f1.dtype == torch.bfloat16)
+            and len(corr_fn.f2s) == 4 and corr_fn.f1.dtype == torch.bfloat16 and model.cfg.mixed_precision)
         return (image.device.type == "cuda" and torch.is_grad_enabled() and model.training
                 and FusedTrainEngine.config_capable(model.cfg)
                 and getattr(corr_fn, "hip", False) and corr_ok
@@ -374,10 +398,11 @@ class FusedTrainEngine:
     def buffers(self, B, H, W, iters, dev):
         key = (B, H, W, iters, dev)
         S = self._bufs.get(key)
+        adt = self.adt
         if S is None and self.small:
             n = iters * B
-            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=torch.bfloat16)
-            z = lambda b, c: torch.zeros(b, H, W, c, device=dev, dtype=torch.bfloat16)
+            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=adt)
+            z = lambda b, c: torch.zeros(b, H, W, c, device=dev, dtype=adt)
             S = dict(
                 corr=e(n, SCORR_PAD), f1=e(n, 64), mot=e(n, 128),
                 hx=z(n + B, 256),                 # channels 242:256 stay zero
@@ -385,7 +410,7 @@ class FusedTrainEngine:
                 rh=[z(n, 128)],                   # channels 96:128 stay zero (weight-gradient window)
                 head=e(n, 128), inp=e(B, 64),
                 C=torch.empty(n + B, 2, H, W, device=dev),
-                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
+                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=adt),  # 2 real
                 d_head=e(n, 128), d_zr=[e(n, 2 * SHD)], d_q=[e(n, SHD)], d_conv=e(n, 96), d_mot=e(n, 128),
                 d_f1=e(n, 64), d_corr=e(n, SCORR_PAD),
                 G=torch.empty(B, H, W, 256, device=dev),
@@ -393,21 +418,52 @@ class FusedTrainEngine:
             self._bufs = {key: S}
         elif S is None:
             n = iters * B
-            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=torch.bfloat16)
+            e = lambda b, c: torch.empty(b, H, W, c, device=dev, dtype=adt)
             S = dict(
                 corr=e(n, CORR_PAD), c1=e(n, 256), f1=e(n, 128), mot=e(n, 256), hx=e(n + B, 256), h1=e(n, HD),
                 z=[e(n, HD), e(n, HD)], r=[e(n, HD), e(n, HD)], q=[e(n, HD), e(n, HD)], rh=[e(n, HD), e(n, HD)],
                 head=e(n, 512), mask=e(n, 576), inp=e(B, 128),
                 C=torch.empty(n + B, 2, H, W, device=dev),  # coords before iteration i = slot i
                 # gradient (dY) slots (zero-initialised: only the leading channels are written)
-                d_mask=torch.zeros(n, H, W, 640, device=dev, dtype=torch.bfloat16),
-                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=torch.bfloat16),  # 2 real
+                d_mask=torch.zeros(n, H, W, 640, device=dev, dtype=adt),
+                d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=adt),  # 2 real
                 d_head=e(n, 512), d_zr=[e(n, 256), e(n, 256)], d_q=[e(n, HD), e(n, HD)], d_conv=e(n, 128),
                 d_c2f2=e(n, 256), d_c1=e(n, 256), d_f1=e(n, 128), d_corr=e(n, CORR_PAD),
                 G=torch.empty(B, H, W, 384, device=dev),
             )
             self._bufs = {key: S}  # one shape at a time (training crops are fixed)
         return S
+
+
+def _split_bf16(t: torch.Tensor):
+    """fp32 -> (hi, lo) bf16 with hi = bf16(t), lo = bf16(t - hi)."""
+    hi = t.to(torch.bfloat16)
+    return hi, (t - hi.float()).to(torch.bfloat16)
+
+
+def _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128=0):
+    """``pc.dw += dY^T X`` (+ ``pc.db += colsum dY``) over every iteration's
+    pixels on csrc/conv_wgrad.hip.  fp32 engine: the bf16 GEMM on the split
+    operands, dYh.Xh + dYl.Xh + dYh.Xl (the bias sums of the first two give
+    colsum(dYh + dYl))."""
+    per = [s[0].shape[0] * H * W for s in segs]
+    if not eng.f32:
+        R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
+                     per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
+        return
+    cache = eng.__dict__.setdefault("_split_cache", {})
+    def split(t):
+        key = (t.data_ptr(), tuple(t.shape))
+        v = cache.get(key)
+        if v is None:
+            v = cache[key] = _split_bf16(t)
+        return v
+    dyh, dyl = split(dy)
+    xs = [split(s[0]) for s in segs]
+    offs, chans = [s[1] for s in segs], [s[2] for s in segs]
+    R.conv_wgrad(dyh, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
+    R.conv_wgrad(dyl, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
+    R.conv_wgrad(dyh, yoff, pc.cout, [x[1] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, None, bn128)
 
 
 class DeferGrads(torch.autograd.Function):
@@ -630,6 +686,7 @@ class FusedTrainLoop(torch.autograd.Function):
             wstream = contextlib.nullcontext()
         with wstream:
             wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
+            eng.__dict__.pop("_split_cache", None)  # fp32 engine: the split operands of this step
             if eng.grad_group is not None:  # data parallel: one RCCL all-reduce of the packed buffer
                 eng.reduce_packed(gbuf)
             grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype)
@@ -650,8 +707,7 @@ class FusedTrainLoop(torch.autograd.Function):
             # --wgrad 12 at the training shape: 8-wave 256x64 for the 3x3
             # 256->192 conv 475 -> 397 us and GRU z|r 404 -> 374 us, 8-wave
             # 128x128 for the 128->512 head 472 -> 425 us)
-            R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
-                         [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db, bn128)
+            _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128)
 
         wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
         wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
@@ -840,8 +896,7 @@ def _small_wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):
     hxs = S["hx"][:n]
 
     def wg(pc, dy, yoff, segs, bn128=0):
-        R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
-                     [s[0].shape[0] * H * W for s in segs], pc.kh, pc.kw, pc.dw, pc.db, bn128)
+        _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128)
 
     wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 128)])
     wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, 128)])

@@ -205,8 +205,8 @@ class RAFT(nn.Module):
         side = None
         dparams = None
         enc_defer = contextlib.nullcontext()
-        if (gpu and self.cfg.overlap_encoders and OVERLAP["defer"] and self.training and torch.is_grad_enabled() and mixed
-                and self.cfg.fused_train and not test_mode):
+        if (gpu and self.cfg.overlap_encoders and OVERLAP["defer"] and self.training and torch.is_grad_enabled()
+                and FusedTrainEngine.config_capable(self.cfg) and not test_mode):
             # update-block weight gradients overlap the encoder backward, and the
             # encoder convs' weight gradients overlap their own dgrad chain
             # (see DeferGrads; ops/enc_conv.py defer_weights)

@@ -140,6 +140,54 @@ def test_fused_training_matches_module_graph(cuda, small):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("small", [False, True], ids=["raft", "raft_small"])
+def test_fused_fp32_training_matches_module_graph(cuda, small):
+    """fp32 training (the reference's standard schedule, no --mixed_precision)
+    through the fused engine -- split-bf16 F32 conv tiles forward and dgrad,
+    split-product weight gradients, fp32 gate / ReLU / flow-head kernels -- vs
+    the fp32 module graph (PyTorch convs): loss, predictions and every
+    parameter gradient within 1e-3 relative."""
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.models.fused_train import FusedTrainEngine
+    from raft_stir_amd.train.loss import sequence_loss
+    torch.manual_seed(0)
+    m = RAFT(make_args(mixed_precision=False, small=small)).to(cuda).to(memory_format=torch.channels_last).train()
+    m.freeze_bn()  # train-mode BN statistics differ in round-off between the two forward orders
+    ref = copy.deepcopy(m)
+    ref.cfg = ref.cfg.__class__(**{**ref.cfg.to_dict(), "fused_train": False})
+    i1, i2, flow, valid = make_batch(2, 192, 256, seed=2, device=cuda)
+    res = {}
+    calls = []
+    orig = FusedTrainEngine.eligible
+    FusedTrainEngine.eligible = staticmethod(lambda *a: calls.append(orig(*a)) or calls[-1])
+    try:
+        for name, net in (("fused", m), ("ref", ref)):
+            preds = net(i1, i2, iters=6)
+            loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
+            loss.backward()
+            res[name] = (loss.item(), [p.detach() for p in preds], _grads(net))
+    finally:
+        FusedTrainEngine.eligible = staticmethod(orig)
+    assert calls[0] and not calls[-1], calls  # fused engine used for m only
+    lf, pf, gf = res["fused"]
+    lr, pr, gr = res["ref"]
+    assert abs(lf - lr) <= 1e-4 * abs(lr), (lf, lr)
+    for a, b in zip(pf, pr):
+        assert ((a - b).norm() / b.norm()).item() < 1e-4
+    assert gf.keys() == gr.keys()
+    bad = []
+    for k in gr:
+        a, b = gf[k].flatten(), gr[k].flatten()
+        normed = k.split(".")[0] in ("fnet", "cnet") and k.endswith(".bias") and k not in (
+            "fnet.conv2.bias", "cnet.conv2.bias")
+        if b.norm() < 1e-8 or normed:
+            continue
+        rel = ((a - b).norm() / b.norm()).item()
+        if rel > 1e-3:
+            bad.append((k, rel))
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("small", [False, True], ids=["raft_r4", "raft_small_r3"])
 def test_fused_training_onthefly_corr_matches_module_graph(cuda, small):
     """--alternate_corr training through the fused engine (on-the-fly

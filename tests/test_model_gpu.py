@@ -142,7 +142,13 @@ def test_training_grads_match_cpu(cuda, small):
     gg = torch.cat([p.grad.flatten().cpu() for p in gpu.parameters()])
     cos = torch.nn.functional.cosine_similarity(gc, gg, dim=0).item()
     assert cos > 0.999, cos
-    assert (gc - gg).norm() / gc.norm() < 2e-2
+    # fp32 training on the GPU runs the fused engine (split-bf16 conv tiles,
+    # relative error ~2^-17 per product) and the encoders' fp32 convs
+    rel = ((gc - gg).norm() / gc.norm()).item()
+    names = [n for n, _ in cpu.named_parameters()]
+    worst = sorted(((((p.grad - q.grad.cpu()).norm() / p.grad.norm().clamp_min(1e-12)).item(), n)
+                    for n, p, q in zip(names, cpu.parameters(), gpu.parameters())), reverse=True)[:5]
+    assert rel < 1e-3, (rel, worst)
 
 
 @pytest.mark.parametrize("mixed,tol", [(False, 2e-3), (True, 3e-2)])
