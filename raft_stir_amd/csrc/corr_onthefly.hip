@@ -20,7 +20,12 @@
 // decomposition as corr_lookup's backward), then df1 accumulates in registers
 // (plain store once per pixel: every pixel owns its df1 row) and df2_l
 // receives g * f1 through float atomics (cells are shared between pixels).
+// Deterministic mode (DET): the df2 contributions are rounded to 32.32
+// fixed point and summed with 64-bit integer atomics -- integer addition is
+// associative, so the sums do not depend on the order the waves arrive in
+// (|df2| < 2^31, resolution 2^-32) -- then converted to fp32 by one pass.
 
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -136,7 +141,11 @@ __global__ __launch_bounds__(WAVES * 64) void otf_fwd_kernel(const T* __restrict
   }
 }
 
-template <typename T, typename GT, int CQ>
+__device__ __forceinline__ void fx_add(unsigned long long* p, float v) {
+  atomicAdd(p, (unsigned long long)__double2ll_rn((double)v * 4294967296.0));
+}
+
+template <typename T, typename GT, int CQ, bool DET>
 __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict__ f1, Lvl f2,
                                                              int levels,
                                                              const float* __restrict__ coords,
@@ -191,7 +200,7 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
     }
     __syncthreads();
     const T* f2b = static_cast<const T*>(f2.p[l]) + (size_t)b * H * W * C;
-    float* d2b = df2.p[l] + (size_t)b * H * W * C;
+    float* d2b = DET ? nullptr : df2.p[l] + (size_t)b * H * W * C;
     for (int base = 0; base < E2; base += 8) {
       const int cell = base + grp;
       const int X = (int)bx - r + cell / E, Y = (int)by - r + cell % E;
@@ -203,11 +212,20 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
           for (int q = 0; q < CQ; ++q) {
             const float4 v = ld4<T>(f2b + off + q * 32);
             da[q].x += gc * v.x; da[q].y += gc * v.y; da[q].z += gc * v.z; da[q].w += gc * v.w;
-            float* d = d2b + off + q * 32;
-            atomicAdd(d + 0, gc * a[q].x);
-            atomicAdd(d + 1, gc * a[q].y);
-            atomicAdd(d + 2, gc * a[q].z);
-            atomicAdd(d + 3, gc * a[q].w);
+            if constexpr (DET) {  // df2.p[l]: int64 32.32 fixed-point accumulators
+              unsigned long long* d = reinterpret_cast<unsigned long long*>(df2.p[l]) +
+                                      (size_t)b * H * W * C + off + q * 32;
+              fx_add(d + 0, gc * a[q].x);
+              fx_add(d + 1, gc * a[q].y);
+              fx_add(d + 2, gc * a[q].z);
+              fx_add(d + 3, gc * a[q].w);
+            } else {
+              float* d = d2b + off + q * 32;
+              atomicAdd(d + 0, gc * a[q].x);
+              atomicAdd(d + 1, gc * a[q].y);
+              atomicAdd(d + 2, gc * a[q].z);
+              atomicAdd(d + 3, gc * a[q].w);
+            }
           }
         }
       }
@@ -230,6 +248,13 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
     for (int q = 0; q < CQ; ++q)
       *reinterpret_cast<float4*>(df1 + pix * C + q * 32 + slot * 4) = da[q];
   }
+}
+
+// 32.32 fixed point (int64) -> fp32
+__global__ __launch_bounds__(256) void fx_to_f32_kernel(const long long* __restrict__ in, long n,
+                                                        float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (float)((double)in[i] * (1.0 / 4294967296.0));
 }
 
 }  // namespace otf
@@ -273,10 +298,12 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 #undef RS_L
 }
 
+// det: df2[l] are int64 fixed-point accumulators (zeroed) of the level sizes;
+// df2f[l] receive their fp32 values
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
-                         float* const* df2, hipStream_t stream) {
+                         float* const* df2, bool det, float* const* df2f, hipStream_t stream) {
   otf::Lvl p;
   otf::LvlMut d;
   for (int l = 0; l < 4; ++l) {
@@ -289,9 +316,14 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
   dim3 grid((unsigned)cdiv((int)npix, otf::WAVES)), block(otf::WAVES * 64);
   const int cq = C / 32;
 #define RS_L(T, GT)                                                                          \
-  hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ>), grid, block, 0, stream,              \
-                     static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,          \
-                     static_cast<const GT*>(dout), df1, d)
+  if (det)                                                                                   \
+    hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ, true>), grid, block, 0, stream,       \
+                       static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,        \
+                       static_cast<const GT*>(dout), df1, d);                                \
+  else                                                                                       \
+    hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ, false>), grid, block, 0, stream,      \
+                       static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,        \
+                       static_cast<const GT*>(dout), df1, d)
   if (fm_bf16) {
     if (dout_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_L(bf16_t, bf16_t)); }
     else { RS_OTF_DISPATCH_CQ(cq, RS_L(bf16_t, float)); }
@@ -300,6 +332,13 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     else { RS_OTF_DISPATCH_CQ(cq, RS_L(float, float)); }
   }
 #undef RS_L
+  if (det)
+    for (int l = 0; l < levels; ++l) {
+      const long n = (long)B * Hs[l] * Ws[l] * C;
+      const int g = (int)std::min<long>((n + 255) / 256, 16384);
+      hipLaunchKernelGGL(otf::fx_to_f32_kernel, dim3(g), dim3(256), 0, stream,
+                         reinterpret_cast<const long long*>(df2[l]), n, df2f[l]);
+    }
 }
 
 }  // namespace rs

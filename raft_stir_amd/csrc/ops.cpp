@@ -34,6 +34,9 @@ void corr_lookup_fwd_launch(const void* const* pyr, bool pyr_bf16, const int* Hs
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride);
+void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
+                     const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
+                     int NP, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
                           float scale, hipStream_t stream, void* out_bf16 = nullptr);
 void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
@@ -45,7 +48,7 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
-                         float* const* df2, hipStream_t stream);
+                         float* const* df2, bool det, float* const* df2f, hipStream_t stream);
 void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, int N, int H, int W,
                           float* out, hipStream_t stream);
 void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
@@ -256,6 +259,36 @@ void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Ten
   RS_CHECK_LAUNCH();
 }
 
+// Volume backward with the pyramid-gradient fold in the operand load
+// (csrc/corr_bwd.hip): (df1, df2) from the gradient pyramid, bf16 features.
+std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const Tensor& f1, const Tensor& f2,
+                                         double scale) {
+  check_gpu(f1, "f1");
+  check_gpu(f2, "f2");
+  check_dtype(f1, {at::kBFloat16}, "f1");
+  check_dtype(f2, {at::kBFloat16}, "f2");
+  TORCH_CHECK(f1.dim() == 3 && f1.is_contiguous(), "corr_volume_backward: f1 must be contiguous (B, N1, C)");
+  TORCH_CHECK(f2.dim() == 4 && f2.is_contiguous(), "corr_volume_backward: f2 must be contiguous (B, H2, W2, C)");
+  const int B = f1.size(0), N1 = f1.size(1), C = f1.size(2);
+  TORCH_CHECK(C == 128 || C == 256, "corr_volume_backward: 128 or 256 feature channels");
+  TORCH_CHECK(f2.size(0) == B && f2.size(3) == C, "corr_volume_backward: f1 / f2 shapes");
+  int Hs[4], Ws[4], Ss[4];
+  check_pyr(gpyr, B, N1, Hs, Ws, Ss);
+  TORCH_CHECK(Hs[0] == f2.size(1) && Ws[0] == f2.size(2), "corr_volume_backward: level 0 must be f2's grid");
+  TORCH_CHECK(Hs[0] * Ws[0] == N1, "corr_volume_backward: square volume (N1 = H2 * W2)");
+  TORCH_CHECK((int64_t)B * N1 * Ss[0] < (int64_t(1) << 40), "corr_volume_backward: pyramid too large");
+  const c10::DeviceGuard guard(f1.device());
+  const int NP = (N1 + 31) / 32 * 32;
+  Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
+  Tensor scratch = at::empty({(int64_t)B * C * NP}, f1.options());
+  float* ptrs[4];
+  for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
+  rs::corr_bwd_launch(ptrs, Hs, Ws, Ss, gpyr.size(), B, N1, C, f1.data_ptr(), f2.data_ptr(), (float)scale,
+                      df1.data_ptr(), df2.data_ptr(), false, scratch.data_ptr(), NP, cur_stream());
+  RS_CHECK_LAUNCH();
+  return {df1, df2};
+}
+
 // ---------------------------------------------------------------- on-the-fly corr
 void check_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords, int* Hs,
                int* Ws) {
@@ -305,9 +338,8 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
   const c10::DeviceGuard guard(f1.device());
   const int B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
   const int levels = f2.size(), D = 2 * radius + 1;
-  TORCH_CHECK(!rs::deterministic(),
-              "corr_otf_backward: the on-the-fly correlation backward scatters with fp32 atomics and has no "
-              "deterministic variant; train with the all-pairs correlation (no --alternate_corr) in deterministic mode");
+  // deterministic mode: df2 accumulates in 32.32 fixed point with int64 atomics (order-independent)
+  const bool det = rs::deterministic();
   check_gpu(dout, "dout");
   TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H1 && dout.size(2) == W1 &&
                   dout.size(3) == levels * D * D,
@@ -317,14 +349,23 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
   res.push_back(df1);
   const void* p[4];
   float* d[4];
+  float* df[4];
+  std::vector<Tensor> fx;
   for (int l = 0; l < levels; ++l) {
     p[l] = f2[l].data_ptr();
-    res.push_back(at::zeros({B, Hs[l], Ws[l], C}, f1.options().dtype(at::kFloat)));
-    d[l] = res.back().data_ptr<float>();
+    if (det) {
+      res.push_back(at::empty({B, Hs[l], Ws[l], C}, f1.options().dtype(at::kFloat)));
+      fx.push_back(at::zeros({B, Hs[l], Ws[l], C}, f1.options().dtype(at::kLong)));
+      d[l] = reinterpret_cast<float*>(fx.back().data_ptr<int64_t>());
+      df[l] = res.back().data_ptr<float>();
+    } else {
+      res.push_back(at::zeros({B, Hs[l], Ws[l], C}, f1.options().dtype(at::kFloat)));
+      d[l] = df[l] = res.back().data_ptr<float>();
+    }
   }
   rs::corr_otf_bwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
                           B, H1 * W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
-                          df1.data_ptr<float>(), d, cur_stream());
+                          df1.data_ptr<float>(), d, det, df, cur_stream());
   RS_CHECK_LAUNCH();
   return res;
 }
@@ -523,6 +564,7 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("corr_lookup_backward(Tensor(a!)[] gpyr, Tensor coords, int radius, Tensor dout) -> ()");
   m.def("pyr_grad_fold(Tensor(a!)[] gpyr, float scale) -> ()");
   m.def("pyr_grad_fold_bf16(Tensor[] gpyr, float scale, Tensor(a!) out) -> ()");
+  m.def("corr_volume_backward(Tensor[] gpyr, Tensor f1, Tensor f2, float scale) -> Tensor[]");
   m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
   m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
@@ -542,6 +584,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("corr_lookup_backward", &corr_lookup_backward);
   m.impl("pyr_grad_fold", &pyr_grad_fold);
   m.impl("pyr_grad_fold_bf16", &pyr_grad_fold_bf16);
+  m.impl("corr_volume_backward", &corr_volume_backward);
   m.impl("corr_otf", &corr_otf);
   m.impl("corr_otf_backward", &corr_otf_backward);
   m.impl("convex_upsample", &convex_upsample);

@@ -68,6 +68,10 @@ def _side_stream(dev):
     return _SIDE_STREAMS.get((dev.index, 0)) if OVERLAP.get("cnet", False) else None
 
 
+# RS_CORR_FUSED_BWD=0: the fold pass + two hipBLASLt bf16 GEMMs instead (A/B baseline)
+_FUSED_BWD = os.environ.get("RS_CORR_FUSED_BWD", "1") != "0"
+
+
 class _CorrVolume(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f1, f2, state: CorrState):
@@ -88,7 +92,13 @@ class _CorrVolume(torch.autograd.Function):
             return None, None, None
         B, N1, C = f1.shape
         _, H2, W2, _ = f2.shape
-        if f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16:
+        if (f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16 and _FUSED_BWD and C in (128, 256)
+                and N1 == H2 * W2):
+            # csrc/corr_bwd.hip: the pyramid-gradient fold in the operand load of
+            # two MFMA GEMM kernels (no 130 MB G, no library GEMMs)
+            df1, df2 = torch.ops.raft_stir.corr_volume_backward(state.gpyr, f1.contiguous(), f2.contiguous(),
+                                                               state.scale)
+        elif f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16:
             # bf16 GEMMs (fp32 accumulation) on a bf16 copy of the folded
             # gradient: ~5x faster than the fp32 GEMMs on MI355X
             G = torch.empty(B, N1, H2 * W2, device=f1.device, dtype=torch.bfloat16)

@@ -87,8 +87,8 @@ def build_parser():
     p.add_argument("--synthetic_length", type=int, default=22232)
     p.add_argument("--bucket_mb", type=float, default=5.0, help="DDP gradient bucket size")
     p.add_argument("--deterministic", action="store_true",
-                   help="bitwise-reproducible GPU steps: ordered reductions instead of fp32 atomics "
-                        "(runtime/determinism.py; not with --alternate_corr)")
+                   help="bitwise-reproducible GPU steps: ordered reductions instead of fp32 atomics, "
+                        "fixed-point on-the-fly correlation backward (runtime/determinism.py)")
     return p
 
 
@@ -117,8 +117,6 @@ def train(args):
     np.random.seed(args.seed + info.rank)
 
     if getattr(args, "deterministic", False):
-        if args.alternate_corr:
-            raise SystemExit("--deterministic: the on-the-fly correlation backward has no deterministic variant")
         from ..runtime.determinism import set_deterministic
         set_deterministic(True)
     margs = make_args(small=args.small, mixed_precision=args.mixed_precision,

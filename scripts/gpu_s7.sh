@@ -1,0 +1,15 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/s7
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  "tests/test_kernels_gpu.py::test_corr_volume_backward_fused" "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16" \
+  "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16_pyramid" tests/test_determinism_gpu.py > gpurun_out/s7/pytest.log 2>&1; rc=$?
+grep -E "PASS|FAIL|Error|assert" gpurun_out/s7/pytest.log | head -20
+if [[ $rc -ne 0 ]]; then exit $rc; fi
+ARGSTR="|RS_CORR_FUSED_BWD=0" 
+for rep in 1 2; do for e in "X=1" "RS_CORR_FUSED_BWD=0"; do
+  env $e timeout -k 10 240 python bench.py --steps 30 --warmup 5 --no-infer > gpurun_out/s7/ab.log 2>&1 || { tail -20 gpurun_out/s7/ab.log; exit 1; }
+  echo "[$e] $(tail -1 gpurun_out/s7/ab.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["final_loss"])')"
+done; done
+timeout -k 10 300 python scripts/host_ops_profile.py > gpurun_out/s7/host_ops.log 2>&1; head -60 gpurun_out/s7/host_ops.log

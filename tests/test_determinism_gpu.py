@@ -91,12 +91,24 @@ def test_flow_wgrad_deterministic(cuda):
     torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-4, atol=1e-2)
 
 
-def test_otf_backward_refused_in_deterministic_mode(cuda):
-    B, H, W, C = 1, 8, 8, 256
-    f1 = torch.randn(B, H, W, C, device=cuda)
-    f2 = [torch.randn(B, H >> l, W >> l, C, device=cuda) for l in range(2)]
-    coords = torch.rand(B, 2, H, W, device=cuda) * 7
-    dout = torch.randn(B, H, W, 2 * 81, device=cuda)
+@pytest.mark.parametrize("bf16", [False, True])
+def test_otf_backward_deterministic_mode(cuda, bf16):
+    """Deterministic mode: the on-the-fly correlation backward accumulates df2
+    in 32.32 fixed point with int64 atomics -- bitwise-identical runs, and
+    within the fixed-point resolution of the fp32-atomic result (reference:
+    /root/reference/alt_cuda_corr/correlation_kernel.cu:229-238 scatters with
+    float atomicAdd)."""
+    B, H, W, C = 2, 24, 40, 256
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    f1 = torch.randn(B, H, W, C, generator=g).to(cuda).to(dt)
+    f2 = [torch.randn(B, H >> l, W >> l, C, generator=g).to(cuda).to(dt) for l in range(4)]
+    coords = (torch.rand(B, 2, H, W, generator=g) * torch.tensor([W, H]).view(1, 2, 1, 1)).to(cuda)
+    dout = torch.randn(B, H, W, 4 * 81, generator=g).to(cuda)
+    ref = torch.ops.raft_stir.corr_otf_backward(f1, f2, coords, 4, 0.125, dout)
     with deterministic():
-        with pytest.raises(RuntimeError, match="deterministic"):
-            torch.ops.raft_stir.corr_otf_backward(f1, f2, coords, 4, 0.125, dout)
+        a = torch.ops.raft_stir.corr_otf_backward(f1, f2, coords, 4, 0.125, dout)
+        b = torch.ops.raft_stir.corr_otf_backward(f1, f2, coords, 4, 0.125, dout)
+    for x, y, r in zip(a, b, ref):
+        assert torch.equal(x, y)
+        torch.testing.assert_close(x, r, rtol=1e-5, atol=1e-5)

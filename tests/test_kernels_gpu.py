@@ -293,3 +293,34 @@ def test_pyr_grad_fold(cuda, HW, out_bf16):
     else:
         torch.ops.raft_stir.pyr_grad_fold(gpyr, scale)
         torch.testing.assert_close(gpyr[0], want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("HW,C", [((46, 62), 256), ((11, 37), 256), ((12, 20), 128), ((23, 31), 128)])
+def test_corr_volume_backward_fused(cuda, HW, C):
+    """csrc/corr_bwd.hip: df1 = G f2 and df2 = G^T f1 with G the folded
+    pyramid gradient (avg-pool adjoint of every level onto level 0, times
+    1/sqrt(C)) computed inside the GEMMs' operand staging, vs fp32 PyTorch
+    (fold by gather, then two bmm).  (11, 37): N = 407, ragged M and K tiles
+    and an odd row pitch (the scalar staging path)."""
+    H, W = HW
+    N = H * W
+    B, levels, scale = 2, 4, 1.0 / math.sqrt(C)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    shapes = [(H >> l, W >> l) for l in range(levels)]
+    gpyr = [torch.randn(B, N, h, w, generator=g).to(cuda) for h, w in shapes]
+    f1 = torch.randn(B, N, C, generator=g).to(cuda).to(torch.bfloat16)
+    f2 = torch.randn(B, H, W, C, generator=g).to(cuda).to(torch.bfloat16)
+    G = gpyr[0].clone()
+    for l in range(1, levels):
+        h, w = shapes[l]
+        ys, xs = torch.arange(H, device=cuda) >> l, torch.arange(W, device=cuda) >> l
+        m = (ys[:, None] < h) & (xs[None, :] < w)
+        G += 0.25 ** l * gpyr[l][:, :, ys.clamp(max=h - 1)][:, :, :, xs.clamp(max=w - 1)] * m
+    G = (G * scale).view(B, N, N)
+    want1 = torch.bmm(G, f2.float().view(B, N, C))
+    want2 = torch.bmm(G.transpose(1, 2), f1.float()).view(B, H, W, C)
+    df1, df2 = torch.ops.raft_stir.corr_volume_backward(gpyr, f1, f2, scale)
+    assert df1.dtype == torch.bfloat16 and df1.shape == f1.shape and df2.shape == f2.shape
+    for got, want in ((df1, want1), (df2, want2)):
+        rel = ((got.float() - want).norm() / want.norm()).item()
+        assert rel < 1e-2, rel  # bf16 G tile (the previous path's bf16 G as well)
