@@ -434,6 +434,66 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
   }
 }
 
+// fp32 feature maps on the bf16 flat GEMM by operand splitting (as the F32
+// conv tiles): x = xh + xl, xh = bf16(x), xl = bf16(x - xh), and
+// <f1, f2> ~= <f1h, f2h> + <f1h, f2l> + <f1l, f2h> (relative error ~2^-17;
+// the dropped <f1l, f2l> is ~2^-16 of a product) = ONE bf16 GEMM over K = 3C
+// with f1x = [f1h | f1h | f1l] and f2x = [f2h | f2l | f2h].  This kernel
+// writes those operands: level l of the source map averaged over 2^l x 2^l
+// blocks in fp32 (the pyramid by linearity, as pool_f2_kernel), then split;
+// pat 0: [h | h | l] (f1), pat 1: [h | l | h] (f2 levels).  One thread per
+// 4 channels of one output pixel.
+struct SplitArgs {
+  const float* x;  // (B, H, W, C) fp32 (the level-0 map)
+  bf16_t* o[5];    // o[0]: f1x (B, N1, 3C); o[1 + l]: f2x level l (B, H_l, W_l, 3C)
+  int B, H, W, C, levels, N1;
+  const float* f1;
+  long start[6];   // first thread of each job: 0 = f1, 1 + l = f2 level l; start[levels + 1] = total
+};
+
+__global__ __launch_bounds__(256) void split3_kernel(SplitArgs a) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cq = a.C >> 2;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {  // constant kernarg indices only (see pool_f2_kernel)
+    if (j > a.levels) break;
+    if (tid < a.start[j] || tid >= a.start[j + 1]) continue;
+    const long q = tid - a.start[j];
+    const int c4 = (int)(q % cq);
+    const long pix = q / cq;
+    float4 v;
+    if (j == 0) {
+      v = *reinterpret_cast<const float4*>(a.f1 + (size_t)pix * a.C + c4 * 4);
+    } else {
+      const int l = j - 1, k = 1 << l, Hl = a.H >> l, Wl = a.W >> l;
+      const int x = (int)(pix % Wl), y = (int)((pix / Wl) % Hl), b = (int)(pix / ((long)Wl * Hl));
+      v = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int dy = 0; dy < k; ++dy)
+        for (int dx = 0; dx < k; ++dx) {
+          const float4 u = *reinterpret_cast<const float4*>(
+              a.x + (((size_t)b * a.H + y * k + dy) * a.W + x * k + dx) * a.C + c4 * 4);
+          v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+      const float inv = 1.f / (float)(k * k);
+      v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+    }
+    const float f[4] = {v.x, v.y, v.z, v.w};
+    uint32_t hi[2], lo[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16_t h0 = f2bf(f[2 * i]), h1 = f2bf(f[2 * i + 1]);
+      hi[i] = uint32_t(h0) | (uint32_t(h1) << 16);
+      lo[i] = uint32_t(f2bf(f[2 * i] - bf2f(h0))) | (uint32_t(f2bf(f[2 * i + 1] - bf2f(h1))) << 16);
+    }
+    bf16_t* ob = (j == 0 ? a.o[0] : j == 1 ? a.o[1] : j == 2 ? a.o[2] : j == 3 ? a.o[3] : a.o[4]) +
+                 (size_t)pix * 3 * a.C + c4 * 4;
+    const uint2 H = make_uint2(hi[0], hi[1]), L = make_uint2(lo[0], lo[1]);
+    *reinterpret_cast<uint2*>(ob) = H;
+    *reinterpret_cast<uint2*>(ob + a.C) = j == 0 ? H : L;
+    *reinterpret_cast<uint2*>(ob + 2 * a.C) = j == 0 ? L : H;
+  }
+}
+
 }  // namespace corrvol
 
 // Host launcher. f1: (B,N1,C), f2: (B,H2,W2,C), both channels-last.
@@ -441,9 +501,68 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
 // when out_bf16 (bf16 inputs only).  bf16 inputs: pooled-f2 workspace `ws`
 // (>= sum_{l>=1} B*H_l*W_l*C bf16) and the flat grouped GEMM; fp32 inputs: the
 // exact fp32 2-D-block kernel.  C % 64 == 0 (bf16) / C % 32 == 0 (f32).
+static void flat_launch(const bf16_t* f1, const bf16_t* const* f2l, int B, int N1, int C, int levels,
+                        void* const* out, const int* Hs, const int* Ws, const int* Ss, bool out_bf16, float scale,
+                        hipStream_t stream) {
+  corrvol::FlatArgs fa{};
+  fa.f1 = f1;
+  fa.N1 = N1; fa.C = C; fa.levels = levels; fa.scale = scale;
+  fa.nq = cdiv(N1, corrvol::FB);
+  int acc_t = 0;
+  for (int l = 0; l < 4; ++l) {
+    fa.tstart[l] = acc_t;
+    if (l < levels) {
+      fa.f2[l] = f2l[l];
+      fa.out[l] = out[l];
+      fa.N2[l] = Hs[l] * Ws[l];
+      fa.S[l] = Ss[l];
+      acc_t += cdiv(fa.N2[l], corrvol::FB) * fa.nq;
+    }
+  }
+  fa.tstart[levels] = acc_t;
+  const dim3 grid((unsigned)(acc_t * B));
+  if (out_bf16)
+    hipLaunchKernelGGL(corrvol::corr_flat_kernel<true>, grid, dim3(256), 0, stream, fa);
+  else
+    hipLaunchKernelGGL(corrvol::corr_flat_kernel<false>, grid, dim3(256), 0, stream, fa);
+}
+
+// bytes of the fp32 split path's workspace (corr_volume_launch with bf16 = false, ws != null)
+size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws) {
+  size_t n = (size_t)B * N1 * 3 * C;
+  for (int l = 0; l < levels; ++l) n += (size_t)B * Hs[l] * Ws[l] * 3 * C;
+  return n * sizeof(bf16_t);
+}
+
 void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1, int H2, int W2,
                         int C, int levels, void* const* out, const int* Hs, const int* Ws, const int* Ss,
                         bool out_bf16, void* ws, float scale, hipStream_t stream) {
+  if (!bf16 && ws) {  // fp32 maps: split-bf16 operands + the flat GEMM over K = 3C
+    corrvol::SplitArgs sa{};
+    sa.x = static_cast<const float*>(f2);
+    sa.f1 = static_cast<const float*>(f1);
+    sa.B = B; sa.H = H2; sa.W = W2; sa.C = C; sa.levels = levels; sa.N1 = N1;
+    bf16_t* w = static_cast<bf16_t*>(ws);
+    long tot = 0;
+    sa.start[0] = 0;
+    sa.o[0] = w;
+    w += (size_t)B * N1 * 3 * C;
+    tot += (long)B * N1 * (C / 4);
+    const bf16_t* f2l[4];
+    for (int l = 0; l < 4; ++l) {
+      sa.start[1 + l] = tot;
+      if (l < levels) {
+        sa.o[1 + l] = w;
+        f2l[l] = w;
+        w += (size_t)B * Hs[l] * Ws[l] * 3 * C;
+        tot += (long)B * Hs[l] * Ws[l] * (C / 4);
+      }
+    }
+    sa.start[levels + 1] = tot;
+    hipLaunchKernelGGL(corrvol::split3_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, sa);
+    flat_launch(sa.o[0], f2l, B, N1, 3 * C, levels, out, Hs, Ws, Ss, false, scale, stream);
+    return;
+  }
   if (bf16) {
     corrvol::PoolArgs pa{};
     pa.f2 = static_cast<const bf16_t*>(f2);

@@ -6,6 +6,7 @@
 // shape must never reach a kernel) and launches on PyTorch's current HIP
 // stream, so the ops compose with torch streams and hipGraph capture.
 
+#include <stdlib.h>
 #include <atomic>
 #include <ATen/ATen.h>
 #include "host_common.h"
@@ -34,6 +35,7 @@ void corr_lookup_fwd_launch(const void* const* pyr, bool pyr_bf16, const int* Hs
 void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels,
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride);
+size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
 void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
                      const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
                      int NP, hipStream_t stream);
@@ -99,6 +101,15 @@ void level_sizes(int H, int W, int levels, int* Hs, int* Ws) {
 // Pyramid levels are (B, N1, H_l, W_l) views whose (b, i) rows start at a
 // padded pitch S_l = round_up(H_l*W_l, 64) elements (128-B aligned rows for the
 // flat volume kernel's whole-line stores); fp32, or bf16 when out_bf16.
+// RS_CORR_F32_SPLIT=0: the exact-fp32 MFMA kernel (mfma_f32_16x16x4f32) for fp32 maps instead
+static bool split_f32_volume() {
+  static const bool on = [] {
+    const char* e = getenv("RS_CORR_F32_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t levels, double scale, bool out_bf16) {
   check_gpu(f1, "f1");
   check_gpu(f2, "f2");
@@ -130,6 +141,9 @@ std::vector<Tensor> corr_volume(const Tensor& f1, const Tensor& f2, int64_t leve
     int64_t n = 0;
     for (int l = 1; l < levels; ++l) n += (int64_t)B * Hs[l] * Ws[l] * C;
     ws = at::empty({n}, f1.options());
+  } else if (!is_bf16(f1) && split_f32_volume() && (3 * C) % 64 == 0 && f1.is_contiguous() && f2.is_contiguous()) {
+    // fp32 maps: split-bf16 operands on the flat MFMA GEMM (csrc/corr_volume.hip split3_kernel)
+    ws = at::empty({(int64_t)rs::corr_volume_split_ws(B, N1, C, levels, Hs, Ws) / 2}, f1.options().dtype(at::kBFloat16));
   }
   rs::corr_volume_launch(f1.data_ptr(), f2.data_ptr(), is_bf16(f1), B, N1, H2, W2, C, levels, ptrs,
                          Hs, Ws, Ss, out_bf16, ws.defined() ? ws.data_ptr() : nullptr, (float)scale, cur_stream());

@@ -6,7 +6,7 @@ mkdir -p gpurun_out/s8
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   "tests/test_kernels_gpu.py::test_corr_volume_backward_fused" "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16" \
-  "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16_pyramid" tests/test_determinism_gpu.py > gpurun_out/s8/pytest.log 2>&1; rc=$?
+  "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16_pyramid" tests/test_determinism_gpu.py "tests/test_kernels_gpu.py::test_corr_volume_pyramid" tests/test_model_gpu.py > gpurun_out/s8/pytest.log 2>&1; rc=$?
 grep -E "PASS|FAIL|Error|assert" gpurun_out/s8/pytest.log | head -30
 if [[ $rc -ne 0 && $rc -ne 1 ]]; then exit $rc; fi
 timeout -k 10 300 python scripts/fp32_train_parity.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/s8/parity.log
