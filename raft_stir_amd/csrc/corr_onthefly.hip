@@ -141,6 +141,160 @@ __global__ __launch_bounds__(WAVES * 64) void otf_fwd_kernel(const T* __restrict
   }
 }
 
+// ------------------------------------------------------- tiled forward (MFMA)
+// Block = 4 waves = a 4 x 4 tile of query pixels.  Per level the 16 windows
+// of a tile nearly coincide under smooth flow (neighbouring centres differ by
+// a fraction of a cell at the coarse levels), so the bounding box of their
+// union, BW x BH cells (typically 120-170 at r = 4, <= MAXC), is gathered
+// ONCE for the whole tile and the cell dots become a small GEMM on
+// mfma_f32_16x16x32_bf16: A = the tile's 16 f1 rows (registers, loaded once
+// for all levels), B = 16 bounding-box cells x 32 channels per MFMA, one
+// 16-byte load per lane straight from the channels-last level (zero outside
+// the image).  Each cell's C-vector is read once per tile instead of once per
+// query: ~6x less gather traffic than otf_fwd_kernel at r = 4.  A level whose
+// bounding box exceeds MAXC (motion boundaries, large flow differences inside
+// the tile) falls back to otf_fwd_kernel's per-query v_dot2 cell loop, one
+// query per wave at a time.  Both paths park the cell dots in LDS (the box
+// layout, or the per-query E x E layout) and the bilinear taps are formed
+// from there with the same arithmetic as otf_fwd_kernel.  Blocks are ordered
+// XCD-major (block i runs on XCD i % 8), so each XCD's L2 sees a contiguous
+// run of tiles whose windows overlap.
+constexpr int TQ = 4;      // tile side, queries
+constexpr int MAXC = 256;  // bounding-box cells on the MFMA path (16 chunks of 16)
+
+template <typename OutT, int CQ>
+__global__ __launch_bounds__(256) void otf_tile_kernel(const bf16_t* __restrict__ f1, Lvl f2, int levels,
+                                                       const float* __restrict__ coords, int B, int H1, int W1,
+                                                       int tiles_x, int tiles_y, int per_xcd, int r, float scale,
+                                                       OutT* __restrict__ out) {
+  __shared__ float dots[16][MAXC + 4];
+  __shared__ int qoff[16];
+  __shared__ float qfx[16], qfy[16];
+  constexpr int C = CQ * 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (tile >= B * tiles_x * tiles_y) return;  // whole block, before any barrier
+  const int b = tile / (tiles_x * tiles_y), t2 = tile % (tiles_x * tiles_y);
+  const int ty = t2 / tiles_x, tx = t2 % tiles_x;
+  const int N1 = H1 * W1;
+  const int D = 2 * r + 1, K2 = D * D, E = D + 1, E2 = E * E, CH = levels * K2;
+  const int r16 = lane & 15, q4 = lane >> 4;
+
+  // lane's query = r16 (lanes 16.. mirror 0..15): the MFMA A row and the bounding-box input
+  const int qy = ty * TQ + (r16 >> 2), qx = tx * TQ + (r16 & 3);
+  const bool qact = qy < H1 && qx < W1;
+  const int qn = qact ? qy * W1 + qx : 0;
+  const float cx0 = coords[((size_t)b * 2 + 0) * N1 + qn];
+  const float cy0 = coords[((size_t)b * 2 + 1) * N1 + qn];
+  uint4 fa[CQ];  // A fragments: query r16, channels 32 s + 8 q4 .. + 8
+  {
+    const bf16_t* p = f1 + ((size_t)b * N1 + qn) * C + 8 * q4;
+#pragma unroll
+    for (int s = 0; s < CQ; ++s)
+      fa[s] = qact ? *reinterpret_cast<const uint4*>(p + 32 * s) : make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  for (int l = 0; l < levels; ++l) {
+    const float inv = 1.f / (float)(1 << l);
+    const float cx = cx0 * inv, cy = cy0 * inv;
+    const float bx = floorf(cx), by = floorf(cy);
+    const int X0 = (int)bx - r, Y0 = (int)by - r;
+    int xmn = qact ? X0 : 0x7fffffff, ymn = qact ? Y0 : 0x7fffffff;
+    int xmx = qact ? X0 : -0x7fffffff, ymx = qact ? Y0 : -0x7fffffff;
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {  // within each 16-lane group: the tile's extremes
+      xmn = min(xmn, __shfl_xor(xmn, o, 64));
+      ymn = min(ymn, __shfl_xor(ymn, o, 64));
+      xmx = max(xmx, __shfl_xor(xmx, o, 64));
+      ymx = max(ymx, __shfl_xor(ymx, o, 64));
+    }
+    const int BW = xmx - xmn + E, BH = ymx - ymn + E;
+    const bool tiled = BW * BH <= MAXC;  // identical in every wave
+    const int sx = tiled ? 1 : E, sy = tiled ? BW : 1;
+    if (wave == 0 && lane < 16) {
+      qoff[lane] = tiled ? (Y0 - ymn) * BW + (X0 - xmn) : 0;
+      qfx[lane] = cx - bx;
+      qfy[lane] = cy - by;
+    }
+    const int H = f2.H[l], W = f2.W[l];
+    const bf16_t* f2b = static_cast<const bf16_t*>(f2.p[l]) + (size_t)b * H * W * C;
+    if (tiled) {
+      const int ncell = BW * BH, nch = cdiv(ncell, 16);
+      // two 16-cell chunks per pass (2 CQ loads in flight per lane)
+      for (int c0 = wave; c0 < nch; c0 += 8) {
+        uint4 fb[2][CQ];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = (c0 + 4 * h) * 16 + r16;
+          const int X = xmn + n % BW, Y = ymn + n / BW;
+          const bool ok = c0 + 4 * h < nch && n < ncell && X >= 0 && X < W && Y >= 0 && Y < H;
+          const bf16_t* p = f2b + (size_t)(ok ? Y * W + X : 0) * C + 8 * q4;
+#pragma unroll
+          for (int s = 0; s < CQ; ++s)
+            fb[h][s] = ok ? *reinterpret_cast<const uint4*>(p + 32 * s) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (c0 + 4 * h >= nch) break;
+          f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < CQ; ++s)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[s]),
+                                                          __builtin_bit_cast(bf16x8_t, fb[h][s]), acc, 0, 0, 0);
+          // D[query 4 q4 + j][cell r16 of the chunk]
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dots[4 * q4 + j][(c0 + 4 * h) * 16 + r16] = acc[j];
+        }
+      }
+    } else {
+      // per-query fallback (otf_fwd_kernel's layout: lane = 8 * cell slot + channel slot)
+      const int slot = lane & 7, grp = lane >> 3;
+      for (int qq = wave; qq < 16; qq += 4) {
+        const int y = ty * TQ + (qq >> 2), x = tx * TQ + (qq & 3);
+        if (y >= H1 || x >= W1) continue;  // wave-uniform
+        const int qX0 = __shfl(X0, qq, 64), qY0 = __shfl(Y0, qq, 64);
+        const bf16_t* f1p = f1 + ((size_t)b * N1 + y * W1 + x) * C + slot * 4;
+        uint2 ab[CQ];
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) ab[q] = *reinterpret_cast<const uint2*>(f1p + q * 32);
+        for (int base = 0; base < E2; base += 8) {
+          const int cell = base + grp;
+          const int X = qX0 + cell / E, Y = qY0 + cell % E;
+          float s = 0.f;
+          if (cell < E2 && X >= 0 && X < W && Y >= 0 && Y < H) {
+            const bf16_t* row = f2b + ((size_t)Y * W + X) * C + slot * 4;
+#pragma unroll
+            for (int q = 0; q < CQ; ++q) {
+              const uint2 v = *reinterpret_cast<const uint2*>(row + q * 32);
+              s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_v, ab[q].x),
+                                                  __builtin_bit_cast(bf16x2_v, v.x), s, false);
+              s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_v, ab[q].y),
+                                                  __builtin_bit_cast(bf16x2_v, v.y), s, false);
+            }
+          }
+          s += __shfl_xor(s, 1, 64);
+          s += __shfl_xor(s, 2, 64);
+          s += __shfl_xor(s, 4, 64);
+          if (slot == 0 && cell < E2) dots[qq][cell] = s;
+        }
+      }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 16 * K2; idx += 256) {
+      const int qq = idx / K2, t = idx % K2;
+      const int y = ty * TQ + (qq >> 2), x = tx * TQ + (qq & 3);
+      if (y >= H1 || x >= W1) continue;
+      const int i = t / D, j = t % D;  // cell (X0 + i, Y0 + j) is the tap's lower corner
+      const float* d = &dots[qq][qoff[qq] + i * sx + j * sy];
+      const float fx = qfx[qq], fy = qfy[qq];
+      const float v = (1.f - fx) * (1.f - fy) * d[0] + fx * (1.f - fy) * d[sx] + (1.f - fx) * fy * d[sy] +
+                      fx * fy * d[sx + sy];
+      io<OutT>::st(out + ((size_t)b * N1 + y * W1 + x) * CH + l * K2 + t, v * scale);
+    }
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ void fx_add(unsigned long long* p, float v) {
   atomicAdd(p, (unsigned long long)__double2ll_rn((double)v * 4294967296.0));
 }
@@ -273,7 +427,7 @@ bool corr_otf_supported_channels(int C) {
 }
 
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
-                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, void* out, bool out_bf16, hipStream_t stream) {
   otf::Lvl p;
   for (int l = 0; l < 4; ++l) {
@@ -281,9 +435,26 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     p.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = l < levels ? Ws[l] : 0;
   }
+  const int N1 = H1 * W1;
+  const int cq = C / 32;
+  static const bool tile_env = [] {  // RS_OTF_TILE=0: per-query kernel only (A/B)
+    const char* e = getenv("RS_OTF_TILE");
+    return !(e && e[0] == '0');
+  }();
+  if (fm_bf16 && tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+    const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
+    const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
+#define RS_L(OT)                                                                                        \
+  hipLaunchKernelGGL((otf::otf_tile_kernel<OT, CQ>), dim3(8 * per_xcd), dim3(256), 0, stream,           \
+                     static_cast<const bf16_t*>(f1), p, levels, coords, B, H1, W1, tiles_x, tiles_y,    \
+                     per_xcd, r, scale, static_cast<OT*>(out))
+    if (out_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_L(bf16_t)); }
+    else { RS_OTF_DISPATCH_CQ(cq, RS_L(float)); }
+#undef RS_L
+    return;
+  }
   const long npix = (long)B * N1;
   dim3 grid((unsigned)cdiv((int)npix, otf::WAVES)), block(otf::WAVES * 64);
-  const int cq = C / 32;
 #define RS_L(T, OT)                                                                           \
   hipLaunchKernelGGL((otf::otf_fwd_kernel<T, OT, CQ>), grid, block, 0, stream,               \
                      static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,           \

@@ -45,7 +45,7 @@ void wpack_gather_launch(const int* code, long long n, const long long* tab, voi
                          const long long* lo, const long long* hi, const float* s, int nr, hipStream_t stream);
 bool corr_otf_supported_channels(int C);
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
-                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, void* out, bool out_bf16, hipStream_t stream);
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
@@ -338,7 +338,7 @@ Tensor corr_otf(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& c
   const void* p[4];
   for (int l = 0; l < levels; ++l) p[l] = f2[l].data_ptr();
   rs::corr_otf_fwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
-                          B, H1 * W1, C, radius, (float)scale, out.data_ptr(), out_bf16,
+                          B, H1, W1, C, radius, (float)scale, out.data_ptr(), out_bf16,
                           cur_stream());
   RS_CHECK_LAUNCH();
   return out;

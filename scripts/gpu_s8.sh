@@ -4,6 +4,9 @@
 set -o pipefail
 mkdir -p gpurun_out/s8
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread "tests/test_kernels_gpu.py::test_onthefly_tiled_forward" "tests/test_kernels_gpu.py::test_onthefly_corr_fwd_bwd" "tests/test_kernels_gpu.py::test_onthefly_matches_allpairs" > gpurun_out/s8/otf.log 2>&1; rc=$?
+grep -E "PASS|FAIL|Error|assert" gpurun_out/s8/otf.log | head -30
+if [[ $rc -ne 0 && $rc -ne 1 ]]; then tail -20 gpurun_out/s8/otf.log; exit $rc; fi
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   "tests/test_kernels_gpu.py::test_corr_volume_backward_fused" "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16" \
   "tests/test_kernels_gpu.py::test_allpairs_corr_autograd_bf16_pyramid" tests/test_determinism_gpu.py "tests/test_kernels_gpu.py::test_corr_volume_pyramid" tests/test_model_gpu.py > gpurun_out/s8/pytest.log 2>&1; rc=$?

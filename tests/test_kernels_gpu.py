@@ -7,6 +7,7 @@ import math
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 from raft_stir_amd.ops import reference as ref
 
@@ -150,6 +151,36 @@ def test_onthefly_corr_fwd_bwd(cuda, C, bf16):
     tol = 2e-2 if bf16 else 1e-3
     torch.testing.assert_close(b1.grad.float().cpu(), a1.grad, rtol=tol, atol=tol)
     torch.testing.assert_close(b2.grad.float().cpu(), a2.grad, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("C,r", [(256, 4), (128, 3), (96, 4)])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_onthefly_tiled_forward(cuda, C, r, out_bf16):
+    """csrc/corr_onthefly.hip otf_tile_kernel (4 x 4 query tiles, bounding-box
+    cell GEMM on MFMA) vs the fp32 reference: smooth affine flow (every level
+    on the MFMA path), a band of random flow (per-query fallback tiles next to
+    MFMA tiles), partial tiles on both edges, flow pointing out of the image."""
+    B, H, W = 2, 23, 38
+    f1, f2 = _fmaps(B, C, H, W, "cpu", seed=21)
+    f1, f2 = f1.bfloat16().float(), f2.bfloat16().float()
+    g = torch.Generator().manual_seed(4)
+    base = ref.coords_grid(B, H, W)
+    ys, xs = base[:, 1:2], base[:, 0:1]
+    flow = torch.cat([3.0 + 0.08 * xs - 0.05 * ys, -2.0 + 0.04 * ys], 1) + 0.3 * torch.randn(B, 2, H, W, generator=g)
+    flow[:, :, 8:13] = 9.0 * torch.randn(B, 2, 5, W, generator=g)  # incoherent band
+    flow[1, 0, :, -6:] += 30.0  # off the right edge
+    coords = base + flow
+    want = ref.corr_onthefly(f1, f2, coords, r)  # (B, L*K2, H, W)
+    b1 = f1.to(cuda, torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+    f2l = [f2]
+    for _ in range(3):
+        f2l.append(F.avg_pool2d(f2l[-1], 2, stride=2))
+    # levels pooled in fp32, stored in bf16 (as OnTheFlyCorr does)
+    b2 = [t.to(cuda, torch.bfloat16).permute(0, 2, 3, 1).contiguous() for t in f2l]
+    got = torch.ops.raft_stir.corr_otf(b1, b2, coords.to(cuda), r, 1.0 / math.sqrt(C), out_bf16)
+    got = got.float().permute(0, 3, 1, 2).cpu()
+    ftol = 2e-2 if out_bf16 else 1e-2
+    torch.testing.assert_close(got, want.detach(), rtol=ftol, atol=ftol)
 
 
 def test_onthefly_matches_allpairs(cuda):
