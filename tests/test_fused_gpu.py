@@ -53,6 +53,33 @@ def test_conv_segments_vs_conv2d(cuda, k, tile, epi):
     assert (out[..., :4] == 7).all() and (out[..., 4 + cout:] == 7).all()  # no writes outside the window
 
 
+@pytest.mark.parametrize("k", [(3, 3), (1, 5), (5, 1)])
+@pytest.mark.parametrize("tile", list(range(42, 54)))
+@pytest.mark.parametrize("shape", [(2, 11, 19), (1, 9, 70)])
+def test_conv_v2_tiles_vs_conv2d(cuda, k, tile, shape):
+    """csrc/conv_v2.hip (unrolled taps, 32x32x16 MFMAs, halo per 64-channel
+    chunk): every tile 42-53 -- 4- and 8-wave blocks, one or two A fragments
+    per wave, 2- to 6-slot weight rings -- on partial patches in both
+    directions, three input segments (two 64-channel, one 128), Cout not a
+    multiple of the block's."""
+    torch.manual_seed(3)
+    B, H, W = shape
+    kh, kw = k
+    segs = [torch.randn(B, H, W, c, device=cuda).to(torch.bfloat16) for c in (64, 64, 128)]
+    cin = 64 + 64 + 128
+    cout = 200
+    w = torch.randn(cout, cin, kh, kw, device=cuda) * 0.05
+    b = torch.randn(cout, device=cuda)
+    wp = pack_weight(w, [(64, [(0, 64, 0)]), (64, [(64, 64, 0)]), (128, [(128, 128, 0)])], pad_to(cout, 256))
+    out = torch.full((B, H, W, cout + 8), 7.0, device=cuda, dtype=torch.bfloat16)
+    conv_fused([(s, 0, s.shape[-1]) for s in segs], wp, pack_bias(b), kh, kw, cout, EPI_RELU, out, 0, tile=tile)
+    x = torch.cat(segs, -1).float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2)).relu()
+    got = out[..., :cout].float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
+    assert (out[..., cout:] == 7).all()
+
+
 def test_gru_epilogues(cuda):
     torch.manual_seed(1)
     B, H, W, hd = 1, 9, 13, 64
