@@ -151,8 +151,11 @@ def main():
             preds = ddp(i1, i2, iters=a.iters)
             loss, _ = sequence_loss(preds, flow, valid, gamma=0.8, sync_metrics=False)
             loss.backward()
-            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-            optimizer.step()
+            if hasattr(optimizer, "clip_and_step"):  # clip + AdamW, two native launches
+                optimizer.clip_and_step(1.0)
+            else:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+                optimizer.step()
             scheduler.step()
             return loss
 

@@ -146,9 +146,12 @@ class GraphedTrainStep:
         preds = self.model(i1, i2, iters=self.iters)
         loss = self.loss_fn(preds, flow, valid)
         loss.backward()
-        if self.clip and self.clip > 0:
-            torch.nn.utils.clip_grad_norm_(self.params, self.clip)
-        self.optimizer.step()
+        if hasattr(self.optimizer, "clip_and_step"):
+            self.optimizer.clip_and_step(self.clip if self.clip and self.clip > 0 else 0.0)
+        else:
+            if self.clip and self.clip > 0:
+                torch.nn.utils.clip_grad_norm_(self.params, self.clip)
+            self.optimizer.step()
         return loss.detach()
 
     def step(self, batch):

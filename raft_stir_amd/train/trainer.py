@@ -197,13 +197,19 @@ def train(args):
             loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma,
                                           sync_metrics=False)
             loss.backward()
-            total_norm = torch.nn.utils.clip_grad_norm_(params, args.clip)
-            found_inf = (~torch.isfinite(total_norm)).float()
-            if fused_opt:
-                optimizer.found_inf = found_inf   # fused AdamW skips the update on the device
-                optimizer.step()
-            elif float(found_inf) == 0.0:
-                optimizer.step()
+            if hasattr(optimizer, "clip_and_step"):
+                # clip + AdamW in two native launches; a non-finite norm skips
+                # the update on the device (train/optim.py FusedClipAdamW)
+                total_norm = optimizer.clip_and_step(args.clip)
+                found_inf = (~torch.isfinite(total_norm)).float()
+            else:
+                total_norm = torch.nn.utils.clip_grad_norm_(params, args.clip)
+                found_inf = (~torch.isfinite(total_norm)).float()
+                if fused_opt:
+                    optimizer.found_inf = found_inf   # fused AdamW skips the update on the device
+                    optimizer.step()
+                elif float(found_inf) == 0.0:
+                    optimizer.step()
             scheduler.step()
             skipped += found_inf
             consecutive = (consecutive + found_inf) * found_inf

@@ -43,8 +43,11 @@ def main():
         t1 = time.perf_counter()
         loss.backward()
         t2 = time.perf_counter()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
+        if hasattr(opt, "clip_and_step"):
+            opt.clip_and_step(1.0)
+        else:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
         sched.step()
         t3 = time.perf_counter()
         if rec:
