@@ -45,6 +45,7 @@ struct GArgs {
   void* out;         // [B][M][256]
   int M, K;          // output rows, reduction length
   int vec;           // g_0 rows 16-byte aligned (8-float loads) -- the non-transposed staging
+  int ksplit, kchunk;  // K split over ksplit blocks of kchunk (a multiple of KS) each: fp32 atomics into out
 };
 
 constexpr int BMR = 64, KS = 32, GP = 40;  // G tile rows, K step, LDS pitch (bf16)
@@ -52,17 +53,25 @@ constexpr int BMR = 64, KS = 32, GP = 40;  // G tile rows, K step, LDS pitch (bf
 __device__ __forceinline__ uint32_t pk2(float a, float b) { return uint32_t(f2bf(a)) | (uint32_t(f2bf(b)) << 16); }
 
 // C: feature channels (256: RAFT, 128: RAFT-small); a wave owns C/4 of them (NT 16-channel tiles)
-template <bool TRANS, typename OT, int C>
+// SPLIT: the K range is split over a.ksplit blocks (more blocks in flight for
+// the latency-bound G staging); each adds its partial tile into the zeroed
+// fp32 output with atomics (not used in deterministic mode).
+template <bool TRANS, typename OT, int C, bool SPLIT>
 __global__ __launch_bounds__(256) void corr_bwd_kernel(GArgs a_) {
   constexpr int NT = C / 64;
+  static_assert(!SPLIT || sizeof(OT) == 4, "split-K accumulates in fp32");
   __shared__ __attribute__((aligned(16))) bf16_t gs[2][BMR * GP];
   const GArgs a = a_;  // a local copy: the staging lambdas capture it (not the kernarg segment)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int mblocks = cdiv(a.M, BMR);
-  const int b = blockIdx.x / mblocks, m0 = (blockIdx.x - b * mblocks) * BMR;
+  const int ks = SPLIT ? (int)(blockIdx.x % a.ksplit) : 0;
+  const int bid = SPLIT ? (int)(blockIdx.x / a.ksplit) : (int)blockIdx.x;
+  const int b = bid / mblocks, m0 = (bid - b * mblocks) * BMR;
   const int W0 = a.W[0];
   const size_t rowbase = (size_t)b * a.N1;  // g rows of image b
-  const int nsteps = cdiv(a.K, KS);
+  const int kbeg = SPLIT ? ks * a.kchunk : 0;
+  const int kend = SPLIT ? min(a.K, kbeg + a.kchunk) : a.K;
+  const int nsteps = kend > kbeg ? cdiv(kend - kbeg, KS) : 0;
 
   // ---- G-tile staging: this thread's 8 values of the 64 x 32 tile
   // !TRANS: row m = m0 + t/4 (p1), K = k0 + 8*(t&3) .. +7 (p2)
@@ -142,15 +151,24 @@ __global__ __launch_bounds__(256) void corr_bwd_kernel(GArgs a_) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  store(0);
+  // the features' fragments of step s + 1 are loaded during step s (a dependent
+  // global load per step otherwise exposes its full latency every K step)
+  uint4 fa[NT], fn[NT];
+  if (nsteps > 0) {
+    load(kbeg);
+    store(0);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) fa[nt] = *reinterpret_cast<const uint4*>(fT + (size_t)nt * 16 * a.NP + kbeg);
+  }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1, k0 = s * KS;
-    uint4 fa[NT];
+    const int buf = s & 1, k0 = kbeg + s * KS;
+    const bool more = s + 1 < nsteps;
+    if (more) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) fa[nt] = *reinterpret_cast<const uint4*>(fT + (size_t)nt * 16 * a.NP + k0);
-    if (s + 1 < nsteps) load(k0 + KS);
+      for (int nt = 0; nt < NT; ++nt) fn[nt] = *reinterpret_cast<const uint4*>(fT + (size_t)nt * 16 * a.NP + k0 + KS);
+      load(k0 + KS);
+    }
     uint4 gb[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) gb[mt] = *reinterpret_cast<const uint4*>(&gs[buf][(mt * 16 + r16) * GP + 8 * q]);
@@ -161,9 +179,14 @@ __global__ __launch_bounds__(256) void corr_bwd_kernel(GArgs a_) {
         acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[nt]),
                                                               __builtin_bit_cast(bf16x8_t, gb[mt]), acc[nt][mt], 0,
                                                               0, 0);
-    if (s + 1 < nsteps) store(buf ^ 1);
+    if (more) {
+      store(buf ^ 1);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) fa[nt] = fn[nt];
+    }
     __syncthreads();
   }
+  if (SPLIT && nsteps == 0) return;
 
   // ---- epilogue: D[channel = 4q + j][row = r16] of each tile -> out[b][row][channel]
 #pragma unroll
@@ -174,7 +197,11 @@ __global__ __launch_bounds__(256) void corr_bwd_kernel(GArgs a_) {
     for (int nt = 0; nt < NT; ++nt) {
       const int c = wave * (C / 4) + nt * 16 + 4 * q;
       const size_t o = ((size_t)b * a.M + row) * C + c;
-      if constexpr (sizeof(OT) == 2) {
+      if constexpr (SPLIT) {
+        float* op = static_cast<float*>(a.out) + o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(op + j, acc[nt][mt][j]);
+      } else if constexpr (sizeof(OT) == 2) {
         *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.out) + o) =
             make_uint2(pk2(acc[nt][mt][0], acc[nt][mt][1]), pk2(acc[nt][mt][2], acc[nt][mt][3]));
       } else {
@@ -208,9 +235,10 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict
 
 // gpyr: levels of [B][N1][cells] fp32 (row pitch S[l]); f1 [B][N1][C], f2 [B][N2][C] bf16 (N2 = H0*W0 = N1)
 // -> df1 [B][N1][C], df2 [B][N2][C] (bf16, or fp32: out_f32); scratch: xT [B][C][NP] bf16, NP = round_up(N, 32)
+// ksplit > 1: df1 / df2 must be ZEROED fp32 (out_f32) -- the K-split blocks add into them
 void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
                      const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
-                     int NP, hipStream_t stream) {
+                     int NP, int ksplit, hipStream_t stream) {
   corrbwd::GArgs a{};
   for (int l = 0; l < 4; ++l) {
     a.g[l] = l < levels ? g[l] : g[0];
@@ -227,11 +255,18 @@ void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, 
   a.vec = (S[0] % 4 == 0) && ((uintptr_t)g[0] % 16 == 0);
   bf16_t* xT = static_cast<bf16_t*>(scratch);
   const dim3 gt(B * cdiv(NP, 64) * (C / 64));
+  a.ksplit = ksplit > 1 ? ksplit : 1;
 #define RS_CB(TR, OT_)                                                                                   \
   do {                                                                                                  \
-    const dim3 g_(B * cdiv(a.M, corrbwd::BMR));                                                         \
-    if (C == 256) hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 256>), g_, dim3(256), 0, stream, a); \
-    else hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 128>), g_, dim3(256), 0, stream, a);     \
+    a.kchunk = round_up(cdiv(a.K, a.ksplit), corrbwd::KS);                                              \
+    const dim3 g_(B * cdiv(a.M, corrbwd::BMR) * a.ksplit);                                              \
+    if (a.ksplit > 1) {                                                                                 \
+      if (C == 256) hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, float, 256, true>), g_, dim3(256), 0, stream, a); \
+      else hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, float, 128, true>), g_, dim3(256), 0, stream, a);     \
+    } else {                                                                                            \
+      if (C == 256) hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 256, false>), g_, dim3(256), 0, stream, a); \
+      else hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 128, false>), g_, dim3(256), 0, stream, a);     \
+    }                                                                                                   \
   } while (0)
   // df1 = G f2: fT = f2^T
   hipLaunchKernelGGL(corrbwd::transpose_kernel, gt, dim3(256), 0, stream, static_cast<const bf16_t*>(f2), a.N2, NP,

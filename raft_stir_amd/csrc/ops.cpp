@@ -38,7 +38,7 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
 size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
 void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
                      const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
-                     int NP, hipStream_t stream);
+                     int NP, int ksplit, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
                           float scale, hipStream_t stream, void* out_bf16 = nullptr);
 void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
@@ -293,12 +293,31 @@ std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const 
   TORCH_CHECK((int64_t)B * N1 * Ss[0] < (int64_t(1) << 40), "corr_volume_backward: pyramid too large");
   const c10::DeviceGuard guard(f1.device());
   const int NP = (N1 + 31) / 32 * 32;
-  Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
+  // K split over blocks (fp32 atomics into zeroed outputs, then one cast
+  // each): the G-tile staging is latency-bound and one block per 64 output
+  // rows gives only ~1.4 blocks per CU at the training shape.  Deterministic
+  // mode keeps one block per row range (plain stores).  RS_CORR_BWD_KSPLIT
+  // overrides the split (1: no split).
+  static const int ks_env = [] {
+    const char* e = getenv("RS_CORR_BWD_KSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  int ksplit = ks_env > 0 ? ks_env : 4;
+  if (rs::deterministic()) ksplit = 1;
   Tensor scratch = at::empty({(int64_t)B * C * NP}, f1.options());
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
+  if (ksplit > 1) {
+    Tensor a1 = at::zeros(f1.sizes(), f1.options().dtype(at::kFloat));
+    Tensor a2 = at::zeros(f2.sizes(), f2.options().dtype(at::kFloat));
+    rs::corr_bwd_launch(ptrs, Hs, Ws, Ss, gpyr.size(), B, N1, C, f1.data_ptr(), f2.data_ptr(), (float)scale,
+                        a1.data_ptr(), a2.data_ptr(), true, scratch.data_ptr(), NP, ksplit, cur_stream());
+    RS_CHECK_LAUNCH();
+    return {a1.to(at::kBFloat16), a2.to(at::kBFloat16)};
+  }
+  Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
   rs::corr_bwd_launch(ptrs, Hs, Ws, Ss, gpyr.size(), B, N1, C, f1.data_ptr(), f2.data_ptr(), (float)scale,
-                      df1.data_ptr(), df2.data_ptr(), false, scratch.data_ptr(), NP, cur_stream());
+                      df1.data_ptr(), df2.data_ptr(), false, scratch.data_ptr(), NP, 1, cur_stream());
   RS_CHECK_LAUNCH();
   return {df1, df2};
 }
