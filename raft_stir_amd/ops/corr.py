@@ -68,8 +68,12 @@ def _side_stream(dev):
     return _SIDE_STREAMS.get((dev.index, 0)) if OVERLAP.get("cnet", False) else None
 
 
-# RS_CORR_FUSED_BWD=0: the fold pass + two hipBLASLt bf16 GEMMs instead (A/B baseline)
-_FUSED_BWD = os.environ.get("RS_CORR_FUSED_BWD", "1") != "0"
+# RS_CORR_FUSED_BWD=1: the volume backward on csrc/corr_bwd.hip (pyramid-gradient
+# fold inside the MFMA GEMMs' operand staging, K split over blocks).  Opt-in:
+# paired in-situ A/B on MI355X (profiles/r4/README.md, session s11): 368 pairs/s
+# fused vs 384 pairs/s for the default -- one fold pass (pyr_fold4, bf16 G)
+# plus two hipBLASLt bf16 GEMMs, ~0.7 ms/step against ~2 ms for the fused pair
+_FUSED_BWD = os.environ.get("RS_CORR_FUSED_BWD", "0") == "1"
 
 
 class _CorrVolume(torch.autograd.Function):

@@ -145,8 +145,13 @@ def test_fused_fp32_training_matches_module_graph(cuda, small):
     """fp32 training (the reference's standard schedule, no --mixed_precision)
     through the fused engine -- split-bf16 F32 conv tiles forward and dgrad,
     split-product weight gradients, fp32 gate / ReLU / flow-head kernels -- vs
-    the fp32 module graph (PyTorch convs): loss, predictions and every
-    parameter gradient within 1e-3 relative."""
+    the fp32 module graph (PyTorch convs): loss and predictions within 1e-4,
+    the whole gradient vector within 1e-3 and every parameter within 1e-2
+    relative.  Against the fp32 CPU oracle (scripts/fp32_train_parity.py,
+    profiles/r4/fp32_parity.txt) BOTH GPU paths are ~2e-4 off over the whole
+    vector and up to ~5e-3 on single deep-encoder weights (round-off of the
+    long encoder backward chain), so the per-parameter bound between them
+    is set by that, not by the fused engine."""
     from raft_stir_amd.data.synthetic import make_batch
     from raft_stir_amd.models.fused_train import FusedTrainEngine
     from raft_stir_amd.train.loss import sequence_loss
@@ -175,17 +180,21 @@ def test_fused_fp32_training_matches_module_graph(cuda, small):
     for a, b in zip(pf, pr):
         assert ((a - b).norm() / b.norm()).item() < 1e-4
     assert gf.keys() == gr.keys()
-    bad = []
+    bad, va, vb = [], [], []
     for k in gr:
         a, b = gf[k].flatten(), gr[k].flatten()
         normed = k.split(".")[0] in ("fnet", "cnet") and k.endswith(".bias") and k not in (
             "fnet.conv2.bias", "cnet.conv2.bias")
         if b.norm() < 1e-8 or normed:
             continue
+        va.append(a)
+        vb.append(b)
         rel = ((a - b).norm() / b.norm()).item()
-        if rel > 1e-3:
+        if rel > 1e-2:
             bad.append((k, rel))
     assert not bad, bad
+    va, vb = torch.cat(va), torch.cat(vb)
+    assert ((va - vb).norm() / vb.norm()).item() < 1e-3
 
 
 @pytest.mark.parametrize("small", [False, True], ids=["raft_r4", "raft_small_r3"])
