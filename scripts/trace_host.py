@@ -37,7 +37,7 @@ def main():
     T = lambda r: (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
     ks.sort(key=lambda r: T(r)[0])
     # steady-state step: between the last two optimizer (FusedAdam) kernel groups
-    idx = [i for i, r in enumerate(ks) if "FusedAdam" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(ks) if ("FusedAdam" in r["Kernel_Name"] or "adamw_kernel" in r["Kernel_Name"])]
     groups = []
     for i in idx:
         if groups and i - groups[-1][-1] <= 2:

@@ -17,7 +17,7 @@ def main(path):
     op = gzip.open if path.endswith(".gz") else open
     rows = list(csv.DictReader(op(path, "rt")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "FusedAdam" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if ("FusedAdam" in r["Kernel_Name"] or "adamw_kernel" in r["Kernel_Name"])]
     groups = []
     for i in idx:
         if groups and i - groups[-1][-1] <= 2:
@@ -56,6 +56,25 @@ def main(path):
     print(f"main-queue gaps > 100 us: {len(gaps)}, {sum(g[1] for g in gaps):.3f} ms")
     for g in gaps:
         print(f"  at {g[0]:7.3f} ms: {g[1]:6.3f} ms idle, then {g[2]}")
+    # timeline: per 0.5 ms bin, each queue's busy fraction and its longest kernel there
+    BIN = 500000
+    nb = (t1 - t0) // BIN + 1
+    qs = sorted(byq, key=byq.get, reverse=True)
+    occ = {q: [0.0] * nb for q in qs}
+    top = {q: [("", 0)] * nb for q in qs}
+    for r in step:
+        s, e = T(r)
+        q = r["Queue_Id"]
+        for bi in range((s - t0) // BIN, (e - t0) // BIN + 1):
+            lo, hi = max(s, t0 + bi * BIN), min(e, t0 + (bi + 1) * BIN)
+            if hi > lo:
+                occ[q][bi] += (hi - lo) / BIN
+                if hi - lo > top[q][bi][1]:
+                    top[q][bi] = (r["Kernel_Name"].replace("void ", "").split("(")[0].split("<")[0][-28:], hi - lo)
+    print("timeline (0.5 ms bins): busy % per queue [" + ", ".join(qs) + "] and the main queue's longest kernel")
+    for bi in range(nb):
+        print(f"  {bi * 0.5:5.1f} ms  " + " ".join(f"{100 * min(occ[q][bi], 1):4.0f}" for q in qs) + "   "
+              + " | ".join(top[q][bi][0] for q in qs))
     # per-queue kernel families (template arguments kept: tiles differ)
     for q in sorted(byq, key=byq.get, reverse=True):
         fam, n = collections.defaultdict(float), collections.Counter()
