@@ -57,7 +57,6 @@ instantiations.
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -610,18 +609,7 @@ class FusedTrainLoop(torch.autograd.Function):
         dflow, dmask = R.convex_upsample_backward(flows, S["mask"], g_up.contiguous())
         S["d_mask"][..., :576].copy_(dmask)
         S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
-        pre, split_at = None, None
-        if _WGRAD_SPLIT and ctx.defer and side is not None and iters >= 4 and not _deterministic():
-            split_at = iters // 2
-            pre = eng.grad_buffers(dev)  # zeroed on main, before the loop
-            pre[0].record_stream(side)
         for i in reversed(range(iters)):
-            if i + 1 == split_at:
-                # iterations [split_at, iters) are done: their weight gradients
-                # overlap the remaining iterations' dgrads on the wgrad stream
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    FusedTrainLoop._wgrads(eng, S, C, *pre, B, H, W, n, split_at, iters)
             hx, hx1, head = sl(S["hx"], i), sl(S["hx"], i + 1), sl(S["head"], i)
             dm, df, dh = sl(S["d_mask"], i), sl(S["d_flow"], i), sl(S["d_head"], i)
             conv_fused([(dm, 0, 576)], eng.mask2.wd, None, 1, 1, 256, EPI_RELU_BWD, dh, 256, aux1=head, a1off=256)
@@ -673,7 +661,7 @@ class FusedTrainLoop(torch.autograd.Function):
         d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
         d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
-        grads = FusedTrainLoop._param_grads(ctx, FusedTrainLoop._wgrads, S, C, B, H, W, n, main, side, pre, split_at)
+        grads = FusedTrainLoop._param_grads(ctx, FusedTrainLoop._wgrads, S, C, B, H, W, n, main, side)
         if otf is None:
             token_grad, otf_grads = torch.zeros((), device=dev), ()
         else:
@@ -682,14 +670,12 @@ class FusedTrainLoop(torch.autograd.Function):
         return (None, None, token_grad, d_net, d_inp, None, None, None, None, None, *otf_grads, *grads)
 
     @staticmethod
-    def _param_grads(ctx, wgrads, S, C, B, H, W, n, main, side, pre=None, upto=None):
+    def _param_grads(ctx, wgrads, S, C, B, H, W, n, main, side):
         """Weight / bias gradients batched over all iterations (``wgrads``), the
         data-parallel all-reduce of the packed buffer and the unpacking --
-        deferred onto the weight-gradient stream when ``ctx.defer``.  ``pre``:
-        the gradient buffers the later iterations' wgrads already accumulated
-        into (RS_WGRAD_SPLIT); then only iterations [0, upto) remain."""
+        deferred onto the weight-gradient stream when ``ctx.defer``."""
         eng = ctx.eng
-        gbuf, dwf, dbf = pre if pre is not None else eng.grad_buffers(main.device)
+        gbuf, dwf, dbf = eng.grad_buffers(main.device)
         if ctx.defer:  # on the weight-gradient stream, joined by DeferGrads.backward
             side.wait_stream(main)
             gbuf.record_stream(side)
@@ -699,10 +685,7 @@ class FusedTrainLoop(torch.autograd.Function):
                 main.wait_stream(side)
             wstream = contextlib.nullcontext()
         with wstream:
-            if upto is None:
-                wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
-            else:
-                wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n, 0, upto)
+            wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n)
             eng.__dict__.pop("_split_cache", None)  # fp32 engine: the split operands of this step
             if eng.grad_group is not None:  # data parallel: one RCCL all-reduce of the packed buffer
                 eng.reduce_packed(gbuf)
@@ -714,20 +697,9 @@ class FusedTrainLoop(torch.autograd.Function):
         return grads
 
     @staticmethod
-    def _wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n, i0=0, i1=None):
-        """Weight gradients over iterations [i0, i1) (default: all): every
-        per-iteration buffer is sliced by whole iterations (iteration-major
-        rows); the broadcast context features keep their own period."""
-        i1 = n // B if i1 is None else i1
-        a, b = i0 * B, i1 * B
-        src = S
-        S = {k: (v[a:b] if k in _ITER_BUFS else [t[a:b] for t in v] if k in _ITER_BUF_PAIRS else v)
-             for k, v in src.items()}
-        S["hx_next"] = src["hx"][a + B:b + B]
-        C = C[a:b]
-        n = b - a
+    def _wgrads(eng, S, C, gbuf, dwf, dbf, B, H, W, n):
         inpb = S["inp"]
-        hxs = S["hx"]
+        hxs = S["hx"][:n]
 
         def wg(pc, dy, yoff, segs, bn128=0):
             # weight gradient + fused bias gradient (column sums of dY); tile
@@ -739,7 +711,7 @@ class FusedTrainLoop(torch.autograd.Function):
 
         wg(eng.mask2, S["d_mask"], 0, [(S["head"], 256, 256)])
         wg(eng.flow, S["d_flow"], 0, [(S["head"], 0, 256)])
-        wg(eng.head, S["d_head"], 0, [(S["hx_next"], 0, HD)], 2)
+        wg(eng.head, S["d_head"], 0, [(S["hx"][B:], 0, HD)], 2)
         hins = [hxs, S["h1"]]
         for p in range(2):
             wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)], 4)
@@ -748,26 +720,7 @@ class FusedTrainLoop(torch.autograd.Function):
         wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], 4)
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])
-        R.flow_wgrad(C, S["d_f1"], dwf, dbf)
-
-
-# per-iteration buffers of the full engine (first dim = iteration * B + image),
-# sliced by FusedTrainLoop._wgrads ("hx" holds iters + 1 slots: hx_next = the
-# slots one iteration later, the flow head's input)
-_ITER_BUFS = ("hx", "h1", "mot", "c1", "f1", "corr", "head", "mask", "d_mask", "d_flow", "d_head", "d_conv",
-              "d_c2f2", "d_c1", "d_f1", "d_corr")
-_ITER_BUF_PAIRS = ("z", "r", "q", "rh", "d_zr", "d_q")
-# RS_WGRAD_SPLIT: launch the weight gradients of the later half of the
-# iterations on the weight-gradient stream as soon as the backward loop has
-# passed them, so they overlap the earlier iterations' dgrads instead of all
-# of them competing with the encoders' backward (not in deterministic mode:
-# the deterministic wgrad reduction writes rather than accumulates)
-_WGRAD_SPLIT = os.environ.get("RS_WGRAD_SPLIT", "1") != "0"
-
-
-def _deterministic() -> bool:
-    from ..runtime.determinism import is_deterministic
-    return is_deterministic()
+        R.flow_wgrad(C[:n], S["d_f1"], dwf, dbf)
 
 
 # ------------------------------------------------------------------ RAFT-small
