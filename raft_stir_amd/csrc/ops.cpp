@@ -43,6 +43,7 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, cons
                           float scale, hipStream_t stream, void* out_bf16 = nullptr);
 void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
                          const long long* lo, const long long* hi, const float* s, int nr, hipStream_t stream);
+void split_bf16_launch(const float* x, long n, uint16_t* hi, uint16_t* lo, hipStream_t s);
 bool corr_otf_supported_channels(int C);
 void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
@@ -587,6 +588,22 @@ void wpack_gather(const Tensor& code, const Tensor& tab, const Tensor& out, at::
   RS_CHECK_LAUNCH();
 }
 
+// fp32 -> (hi, lo) bf16 with hi = bf16(x), lo = bf16(x - hi) (csrc/split.hip)
+std::vector<Tensor> split_bf16(const Tensor& x) {
+  check_gpu(x, "x");
+  check_dtype(x, {at::kFloat}, "x");
+  TORCH_CHECK(x.is_contiguous(), "split_bf16: x must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "split_bf16: x must be 16-byte aligned");
+  const c10::DeviceGuard guard(x.device());
+  Tensor hi = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  Tensor lo = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  if (x.numel() > 0)
+    rs::split_bf16_launch(x.data_ptr<float>(), x.numel(), reinterpret_cast<uint16_t*>(hi.data_ptr()),
+                          reinterpret_cast<uint16_t*>(lo.data_ptr()), cur_stream());
+  RS_CHECK_LAUNCH();
+  return {hi, lo};
+}
+
 TORCH_LIBRARY(raft_stir, m) {
   m.def("wpack_gather(Tensor code, Tensor tab, Tensor(a!) out, int[] rlo, int[] rhi, float[] rs) -> ()");
   m.def("set_deterministic(bool on) -> ()", &set_deterministic);
@@ -598,6 +615,7 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("pyr_grad_fold(Tensor(a!)[] gpyr, float scale) -> ()");
   m.def("pyr_grad_fold_bf16(Tensor[] gpyr, float scale, Tensor(a!) out) -> ()");
   m.def("corr_volume_backward(Tensor[] gpyr, Tensor f1, Tensor f2, float scale) -> Tensor[]");
+  m.def("split_bf16(Tensor x) -> Tensor[]");
   m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
   m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
@@ -618,6 +636,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("pyr_grad_fold", &pyr_grad_fold);
   m.impl("pyr_grad_fold_bf16", &pyr_grad_fold_bf16);
   m.impl("corr_volume_backward", &corr_volume_backward);
+  m.impl("split_bf16", &split_bf16);
   m.impl("corr_otf", &corr_otf);
   m.impl("corr_otf_backward", &corr_otf_backward);
   m.impl("convex_upsample", &convex_upsample);

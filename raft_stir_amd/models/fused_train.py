@@ -436,7 +436,11 @@ class FusedTrainEngine:
 
 
 def _split_bf16(t: torch.Tensor):
-    """fp32 -> (hi, lo) bf16 with hi = bf16(t), lo = bf16(t - hi)."""
+    """fp32 -> (hi, lo) bf16 with hi = bf16(t), lo = bf16(t - hi): one pass of
+    csrc/split.hip for contiguous device tensors."""
+    if t.is_cuda and t.is_contiguous() and t.data_ptr() % 16 == 0:
+        hi, lo = R.split_bf16(t)
+        return hi, lo
     hi = t.to(torch.bfloat16)
     return hi, (t - hi.float()).to(torch.bfloat16)
 

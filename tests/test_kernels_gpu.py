@@ -364,3 +364,15 @@ def test_corr_volume_backward_fused(cuda, HW, C, det):
     for got, want in ((df1, want1), (df2, want2)):
         rel = ((got.float() - want).norm() / want.norm()).item()
         assert rel < 1e-2, rel  # bf16 G tile (the previous path's bf16 G as well)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 1000003])
+def test_split_bf16_matches_aten(cuda, n):
+    """csrc/split.hip: hi = bf16(x), lo = bf16(x - hi), bitwise equal to the
+    ATen casts (round-to-nearest-even), tails of n % 4 elements included."""
+    g = torch.Generator().manual_seed(n)
+    x = (torch.randn(n, generator=g) * torch.logspace(-8, 8, n)).to(cuda)
+    hi, lo = torch.ops.raft_stir.split_bf16(x)
+    want_hi = x.to(torch.bfloat16)
+    want_lo = (x - want_hi.float()).to(torch.bfloat16)
+    assert torch.equal(hi, want_hi) and torch.equal(lo, want_lo)
