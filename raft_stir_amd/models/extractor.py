@@ -15,8 +15,9 @@ reference creates by registering the same norm module twice).
 
 MI355X notes: the encoders run once per image pair; on the GPU bf16 path
 their 3x3 (stride 1 and 2) and 1x1 convolutions run on the hand-written
-implicit-GEMM kernels (ops/enc_conv.py; the 7x7 stem runs on csrc/stem.hip
-for fp32 inference and on MIOpen under bf16, measured faster there; RAFT-small's
+implicit-GEMM kernels (ops/enc_conv.py; fp32 -- inference and training -- on
+the split-bf16 F32 tiles; the 7x7 stem runs on csrc/stem.hip for fp32
+inference and on MIOpen in training, measured faster there; RAFT-small's
 narrow bottleneck convs run on csrc/sconv.hip at inference), and every
 norm -> ReLU (-> residual add -> ReLU) chain is one fused NHWC pass of
 csrc/norm.hip (ops/norm.py) instead of PyTorch's instance_norm, which would
@@ -173,6 +174,8 @@ class _Encoder(nn.Module):
         and on the split-bf16 F32 tiles for fp32 inference."""
         if enc_conv.eligible_f32(self.conv2, x):
             return enc_conv.conv_f32(self.conv2, x)
+        if enc_conv.eligible_f32_train(self.conv2, x):  # fp32 training (split-bf16 F32 tiles)
+            return enc_conv.conv_f32_train(self.conv2, x)
         if not self.hip_geo and enc_conv.sconv_eligible(self.conv2, x):  # RAFT-small inference
             return enc_conv.sconv(self.conv2, x)
         if enc_conv.eligible_geo(self.conv2, x):

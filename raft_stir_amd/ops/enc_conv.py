@@ -421,6 +421,122 @@ def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None, sc
     return out.permute(0, 3, 1, 2)
 
 
+# -------------------------------------------------------------- fp32 training
+# fp32 encoder convs in TRAINING (the reference's default precision,
+# /root/reference/train_standard.sh) on the same split-bf16 F32 tiles:
+#   forward : conv_f32 (above);
+#   dgrad   : stride 1 -- the conv of dY with the flipped, transposed weight;
+#             stride 2 / 1x1 -- the phase-split dgrad of conv_geo -- both on
+#             the F32 tiles with split-packed weights, fp32 in and out;
+#   wgrad   : three bf16 MFMA GEMMs over split operands, dYh.Xh + dYl.Xh +
+#             dYh.Xl (csrc/split.hip, then enc_wgrad / conv_wgrad_strided):
+#             ~2^-16 relative, the same scheme as the fused update block;
+#   bias    : column sum of dY in fp32 (the projection head only; the other
+#             convs' biases fold into their normalisation).
+_F32_TRAIN = os.environ.get("RS_F32_ENC_TRAIN", "1") != "0"
+
+
+def _f32_shape_ok(conv: nn.Conv2d) -> bool:
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros" or isinstance(p, str):
+        return False
+    return (k == (3, 3) and p == (1, 1) and s in ((1, 1), (2, 2))) or (k == (1, 1) and p == (0, 0) and s in ((1, 1), (2, 2)))
+
+
+def eligible_f32_train(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """fp32 training conv on the F32 tiles (see above): the eligible_f32
+    shapes, input and output channels multiples of 32 (>= 64 for the weight
+    gradient kernels), something to differentiate."""
+    if not (_ENABLED and _F32_ENC and _F32_TRAIN and _GEO_SCOPE[0]) or x.dtype != torch.float32 or x.dim() != 4:
+        return False
+    if not _ext.use_hip(x) or torch.is_autocast_enabled("cuda") or not torch.is_grad_enabled():
+        return False
+    if not (x.requires_grad or conv.weight.requires_grad or (conv.bias is not None and conv.bias.requires_grad)):
+        return False
+    if conv.weight.dtype != torch.float32 or not _f32_shape_ok(conv):
+        return False
+    cin, cout = conv.in_channels, conv.out_channels
+    if cin % 32 or cout % 32 or min(cin, cout) < 64 or not x.is_contiguous(memory_format=_CL):
+        return False
+    return x.numel() * 4 < (1 << 31)
+
+
+def _split(t: torch.Tensor):
+    """(hi, lo) bf16 of a contiguous fp32 tensor (csrc/split.hip)."""
+    t = t.contiguous()
+    if t.data_ptr() % 16 == 0:
+        hi, lo = torch.ops.raft_stir.split_bf16(t)
+        return hi, lo
+    hi = t.to(torch.bfloat16)
+    return hi, (t - hi.float()).to(torch.bfloat16)
+
+
+def _split_dgrad_weight(weight: torch.Tensor) -> torch.Tensor:
+    cout, cin = weight.shape[:2]
+    return wpack.packed_split(("s1_dgrad", id(weight)), [weight], lambda ws: pack_weight(
+        ws[0].transpose(0, 1).flip(2, 3), [(cout, [(0, cout, 0)])], pad_to(cin, 128), _F32))
+
+
+def _f32_wgrad(conv: nn.Conv2d, dyn, x, want_w: bool, want_b: bool):
+    weight = conv.weight
+    dw = db = None
+    if want_w:
+        dyh, dyl = _split(dyn)
+        xh, xl = _split(_nhwc(x))
+        cin, cout = conv.in_channels, conv.out_channels
+        if conv.kernel_size == (3, 3) and conv.stride == (1, 1):
+            P = xh.shape[0] * xh.shape[1] * xh.shape[2]
+            f = lambda d, xx: _wgrad3x3(d, xx.permute(0, 3, 1, 2), xx, weight, cin, cout, P)
+        else:
+            f = lambda d, xx: _conv_geo_wgrad(d, xx.permute(0, 3, 1, 2), weight, tuple(conv.stride), False)[0]
+        dw = f(dyh, xh) + f(dyl, xh) + f(dyh, xl)
+    if want_b:
+        db = dyn.sum((0, 1, 2)).to(conv.bias.dtype)
+    return dw, db
+
+
+class _ConvF32(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, hold, wstream):
+        conv = hold.p
+        out = conv_f32(conv, x, bias=bias is not None)
+        ctx.save_for_backward(x)
+        ctx.conv, ctx.wstream, ctx.has_bias = conv, wstream, bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        conv = ctx.conv
+        dyn = _nhwc(dy.float().contiguous(memory_format=_CL))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if conv.kernel_size == (3, 3) and conv.stride == (1, 1):
+                N, H, W, cout = dyn.shape
+                dxn = torch.empty(N, H, W, conv.in_channels, device=dy.device, dtype=torch.float32)
+                conv_fused([(dyn, 0, cout)], _split_dgrad_weight(conv.weight), None, 3, 3, conv.in_channels,
+                           EPI_BIAS, dxn, 0, tile=None)
+                dx = dxn.permute(0, 3, 1, 2)
+            else:
+                dx = _conv_geo_dgrad([dyn], [conv.weight], x.shape, tuple(conv.stride), tuple(conv.padding),
+                                     f32=True).permute(0, 3, 1, 2)
+        want_w = ctx.needs_input_grad[1]
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if want_w or want_b:
+            dw, db = _wgrad_on(ctx.wstream, lambda: _f32_wgrad(conv, dyn, x, want_w, want_b), [dyn, x])
+        return dx, dw, db, None, None
+
+
+def conv_f32_train(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
+    """fp32 training ``conv(x)`` (:func:`eligible_f32_train`); ``bias=False``
+    drops the conv bias (folded into the following normalisation)."""
+    w, st = _weight_in(conv.weight)
+    b = conv.bias if (bias and conv.bias is not None) else None
+    if b is not None and st is not None:
+        b = _DEFER["views"].get(id(conv.bias), b)
+    return _ConvF32.apply(x, w, b, _Hold(conv), st)
+
+
 def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residual=None) -> torch.Tensor:
     """Inference (no autograd): ``[relu](conv_nobias(x) * scale + shift)``, then
     ``relu(. + residual)`` -- an eval-mode BatchNorm (scale / shift per output
@@ -520,9 +636,9 @@ def _fwd_weight(weight):
                         lambda ws: pack_weight(ws[0], [(cin, [(0, cin, 0)])], pad_to(cout, 128), _F32))
 
 
-def _phase_weight(weights, ry, rx, strides, pads):
+def _phase_weight(weights, ry, rx, strides, pads, f32=False):
     """Packed dgrad weight of phase (ry, rx) of one strided conv:
-    [pad128(Cin)][kh' * kw'][Cout]."""
+    [pad128(Cin)][kh' * kw'][Cout] (``f32``: the split [wh | wl] form)."""
     assert len(weights) == 1, "several convs share a phase weight through _pair_phase_weight"
     w0 = weights[0]
     cout, cin, kh, kw = w0.shape
@@ -532,7 +648,8 @@ def _phase_weight(weights, ry, rx, strides, pads):
     def layout(ws):
         sub = ws[0][:, :, [k for _, k in ty]][:, :, :, [k for _, k in tx]]  # [cout, cin, kh', kw']
         return pack_weight(sub.transpose(0, 1), [(cout, [(0, cout, 0)])], pad_to(cin, 128), _F32)
-    return wpack.packed(("phase", id(w0), ry, rx, tuple(strides), tuple(pads)), [w0], layout)
+    pk = wpack.packed_split if f32 else wpack.packed
+    return pk(("phase", id(w0), ry, rx, tuple(strides), tuple(pads)), [w0], layout)
 
 
 def _geo_tile(cout: int, chans) -> int:
@@ -559,9 +676,10 @@ def _conv_geo_fwd(x, weight, bias, stride, pad, stats=None):
     return out
 
 
-def _conv_geo_dgrad(dys, weights, x_shape, stride, pad):
-    """dX (NHWC bf16) of convs sharing the input: sum over ``weights`` of
-    their input gradients from ``dys`` (NHWC bf16 output gradients)."""
+def _conv_geo_dgrad(dys, weights, x_shape, stride, pad, f32=False):
+    """dX (NHWC bf16; ``f32``: fp32 on the split-bf16 F32 tiles) of convs
+    sharing the input: sum over ``weights`` of their input gradients from
+    ``dys`` (NHWC output gradients of the same dtype)."""
     N, cin, Hi, Wi = x_shape
     kh, kw = weights[0].shape[2:]
     Ho, Wo = dys[0].shape[1:3]
@@ -573,7 +691,8 @@ def _conv_geo_dgrad(dys, weights, x_shape, stride, pad):
                    if _phase_taps(w.shape[2], sy, pad[0], ry) and _phase_taps(w.shape[3], sx, pad[1], rx)]
             phases.append((ry, rx, use))
     full = all(len(u) > 0 for _, _, u in phases)
-    dx = (torch.empty if full else torch.zeros)(N, Hi, Wi, cin, device=dys[0].device, dtype=torch.bfloat16)
+    dx = (torch.empty if full else torch.zeros)(N, Hi, Wi, cin, device=dys[0].device,
+                                                dtype=torch.float32 if f32 else torch.bfloat16)
     for ry, rx, use in phases:
         if not use:
             continue
@@ -585,11 +704,11 @@ def _conv_geo_dgrad(dys, weights, x_shape, stride, pad):
         tx = _phase_taps(ws[0].shape[3], sx, pad[1], rx)
         for w in ws[1:]:  # fused K segments must share the sub-kernel
             assert _phase_taps(w.shape[2], sy, pad[0], ry) == ty and _phase_taps(w.shape[3], sx, pad[1], rx) == tx
-        wp = _phase_weight(ws, ry, rx, stride, pad)
+        wp = _phase_weight(ws, ry, rx, stride, pad, f32)
         chans = [weights[i].shape[0] for i in use]
+        tile = choose_tile_f32(N * mh * mw, cin, geo=True) if f32 else _geo_tile(cin, chans)
         torch.ops.raft_stir.conv_geo([dys[i] for i in use], [0] * len(use), chans, wp, None, len(ty), len(tx),
-                                     -ty[0][0], -tx[0][0], 1, 1, mh, mw, cin, dx, 0, sy, sx, ry, rx,
-                                     _geo_tile(cin, chans))
+                                     -ty[0][0], -tx[0][0], 1, 1, mh, mw, cin, dx, 0, sy, sx, ry, rx, tile)
     return dx
 
 

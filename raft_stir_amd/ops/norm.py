@@ -315,6 +315,8 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
             return enc_conv.stem_norm(conv, x, sc, sh, relu)
         st = _stats_request(norm, x, conv.out_channels)
         return norm_act(norm, enc_conv.stem(conv, x, st), relu, residual, bias=conv.bias, stats=st)
+    if enc_conv.eligible_f32_train(conv, x):  # fp32 training on the split-bf16 F32 tiles
+        return norm_act(norm, enc_conv.conv_f32_train(conv, x, bias=False), relu, residual, bias=conv.bias)
     if _eval_fused_ok(conv, norm, x, residual):  # eval BatchNorm: everything in the conv epilogue
         sc, sh = _eval_affine(norm, conv.bias)
         return enc_conv.conv_norm(conv, x, sc, sh, relu, residual)
@@ -341,7 +343,7 @@ def conv_pair_norm_act(conv1: nn.Conv2d, norm1: nn.Module, down: nn.Conv2d, norm
     3x3's (0, 0) phase) instead of two dgrads and an add."""
     fold = (conv1.bias is not None and down.bias is not None and _FOLD_BIAS and _ext.use_hip(x)
             and _norm_kind_ok(norm1) and _norm_kind_ok(norm_d))
-    if fold and x.dtype == torch.float32 and enc_conv.eligible_f32(conv1, x) and enc_conv.eligible_f32(down, x):
+    if fold and x.dtype == torch.float32:  # fp32: each conv on its own F32 path (inference or training)
         return conv_norm_act(conv1, norm1, x), conv_norm_act(down, norm_d, x, relu=False)
     if fold and enc_conv.pair_eligible(conv1, down, x):
         if _eval_fused_ok(conv1, norm1, x, None) and _eval_fused_ok(down, norm_d, x, None):

@@ -1,0 +1,47 @@
+"""fp32 encoder TRAINING on the split-bf16 F32 tiles (ops/enc_conv.py
+conv_f32_train: F32 forward, F32 dgrad -- flipped weight at stride 1, phase
+split at stride 2 / 1x1 -- and the three-product split weight gradient) vs
+the fp32 CPU autograd of the same module (reference core/extractor.py:118-192)."""
+import copy
+
+import pytest
+import torch
+
+from raft_stir_amd.models.extractor import BasicEncoder
+from raft_stir_amd.ops import enc_conv
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("norm_fn", ["instance", "batch"])
+def test_basic_encoder_fp32_training_on_f32_tiles(cuda, norm_fn):
+    torch.manual_seed(0)
+    cpu = BasicEncoder(output_dim=256, norm_fn=norm_fn).train()
+    gpu = copy.deepcopy(cpu).to(cuda).to(memory_format=torch.channels_last).train()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 3, 96, 128, generator=g)
+    calls = []
+    orig = enc_conv.conv_f32_train
+    enc_conv.conv_f32_train = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        yg = gpu(x.to(cuda).contiguous(memory_format=torch.channels_last))
+    finally:
+        enc_conv.conv_f32_train = orig
+    yc = cpu(x)
+    # every 3x3 / strided / 1x1 conv (all but the 7x7 stem) took the F32 training path
+    assert len(calls) == 6 * 2 + 2 + 1, len(calls)
+    torch.testing.assert_close(yg.float().cpu(), yc, rtol=1e-4, atol=1e-4)
+    w = torch.randn(yc.shape, generator=g)
+    (yc * w).sum().backward()
+    (yg * w.to(cuda)).sum().backward()
+    gc = {n: p.grad for n, p in cpu.named_parameters() if p.grad is not None}
+    gg = {n: p.grad.float().cpu() for n, p in gpu.named_parameters() if p.grad is not None}
+    assert gc.keys() == gg.keys()
+    worst = []
+    for n in gc:
+        if n.endswith(".bias") and n != "conv2.bias":  # biases folded into a norm: true gradient is zero
+            continue
+        rel = ((gg[n] - gc[n]).norm() / gc[n].norm().clamp_min(1e-12)).item()
+        worst.append((rel, n))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 1e-3, worst[:5]
