@@ -57,7 +57,9 @@ class _NormAct(torch.autograd.Function):
         want_g = gamma is not None and ctx.needs_input_grad[1]
         want_b = beta is not None and ctx.needs_input_grad[2]
         if want_g and want_b:
-            d = s12.sum(1)  # (2, C): one reduction for dbeta and dgamma (s1 = s12[0], s2 = s12[1])
+            # (2, C): dbeta and dgamma (s1 = s12[0], s2 = s12[1]); batch statistics
+            # have one group -- a view, no reduction launch
+            d = s12[:, 0] if s12.shape[1] == 1 else s12.sum(1)
             dbeta, dgamma = d[0], d[1]
         else:
             dgamma = s2.sum(0) if want_g else None
