@@ -47,7 +47,7 @@ struct HArgs {
   const float* chs;
   const float* shift;
   const bf16_t* res;
-  int rstr, relu;
+  int rstr, relu, res_relu;
   float* stats;
   int stats_ps;
 };
@@ -293,10 +293,14 @@ __global__ __launch_bounds__(256) void enc_halo_kernel(HArgs a) {
                 for (int j = 0; j < 4; ++j) v[j] = acc[r][mi][4 * g + j];
                 if (rp) {
                   const uint2 u = *reinterpret_cast<const uint2*>(rp + cb);
-                  v[0] = fmaxf(v[0] + __uint_as_float(u.x << 16), 0.f);
-                  v[1] = fmaxf(v[1] + __uint_as_float(u.x & 0xffff0000u), 0.f);
-                  v[2] = fmaxf(v[2] + __uint_as_float(u.y << 16), 0.f);
-                  v[3] = fmaxf(v[3] + __uint_as_float(u.y & 0xffff0000u), 0.f);
+                  v[0] += __uint_as_float(u.x << 16);
+                  v[1] += __uint_as_float(u.x & 0xffff0000u);
+                  v[2] += __uint_as_float(u.y << 16);
+                  v[3] += __uint_as_float(u.y & 0xffff0000u);
+                  if (a.res_relu) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+                  }
                 }
                 const uint2 pk = make_uint2(uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
                                             uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16));
@@ -321,7 +325,7 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
                      int cin, int cout, int num_cus, const EncEpi& e, hipStream_t stream) {
   if (!enc_halo_supported(cin, cout)) return false;
   ench::HArgs a{};
-  a.chs = e.chs; a.shift = e.shift; a.res = e.res; a.rstr = e.rstr; a.relu = e.relu;
+  a.chs = e.chs; a.shift = e.shift; a.res = e.res; a.rstr = e.rstr; a.relu = e.relu; a.res_relu = e.res_relu;
   a.stats = e.stats; a.stats_ps = e.stats_ps;
   a.x = x; a.w = w; a.y = y;
   a.xstr = xstr; a.ystr = ystr; a.Ktot = Ktot;

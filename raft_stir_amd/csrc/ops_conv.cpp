@@ -760,7 +760,8 @@ int num_cus(int dev) {
 // (cout of its y.size(3) channels), no bias.
 void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin, int64_t cout,
                   const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale,
-                  const c10::optional<Tensor>& nshift, const c10::optional<Tensor>& res, bool relu) {
+                  const c10::optional<Tensor>& nshift, const c10::optional<Tensor>& res, bool relu,
+                  bool accumulate) {
   TORCH_CHECK(x.dim() == 4, "conv3x3_halo: x must be NHWC");
   const int B = x.size(0), H = x.size(1), W = x.size(2);
   check_nhwc(x, B, H, W, "conv3x3_halo: x");
@@ -787,6 +788,12 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
                 "conv3x3_halo: res channels / alignment");
     e.res = static_cast<const uint16_t*>(res->data_ptr());
     e.rstr = res->size(3);
+  }
+  if (accumulate) {  // y += conv(x): the epilogue reads y as a plain (no ReLU) residual
+    TORCH_CHECK(!res && !nscale && !stats, "conv3x3_halo: accumulate excludes res / nscale / stats");
+    e.res = static_cast<const uint16_t*>(y.data_ptr());
+    e.rstr = y.size(3);
+    e.res_relu = 0;
   }
   const c10::DeviceGuard guard(x.device());
   rs::enc_halo_launch(static_cast<const uint16_t*>(x.data_ptr()), x.size(3), static_cast<const uint16_t*>(w.data_ptr()),
@@ -867,7 +874,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("stem_wgrad(Tensor x, Tensor dy, int Cout, Tensor(a!) dw) -> ()");
   m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout, Tensor(b!)? stats=None, "
         "bool stats_per_sample=False, Tensor? nscale=None, Tensor? nshift=None, Tensor? res=None, "
-        "bool relu=False) -> ()");
+        "bool relu=False, bool accumulate=False) -> ()");
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
         "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
   m.def("flow_head(Tensor x, int xoff, int cin, Tensor w, Tensor bias, Tensor(a!) crd, Tensor? src) -> ()");

@@ -65,12 +65,15 @@ class ResidualBlock(nn.Module):
                 nn.Conv2d(in_planes, planes, 1, stride=stride), self.norm3)
 
     def forward(self, x):
+        sink = None
         if self.downsample is None:
-            y, skip = conv_norm_act(self.conv1, self.norm1, x), x
+            # the skip gradient goes straight into conv1's input-gradient epilogue
+            sink = enc_conv.GradSink() if x.is_cuda else None
+            y, skip = conv_norm_act(self.conv1, self.norm1, x, grad_sink=sink), x
         else:
             y, skip = conv_pair_norm_act(self.conv1, self.norm1, self.downsample[0], self.norm3, x)
         # relu(skip + relu(norm2(conv2(y)))) as one fused pass on GPU
-        return conv_norm_act(self.conv2, self.norm2, y, relu=True, residual=skip)
+        return conv_norm_act(self.conv2, self.norm2, y, relu=True, residual=skip, res_sink=sink)
 
 
 class BottleneckBlock(nn.Module):

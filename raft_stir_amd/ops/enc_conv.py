@@ -177,9 +177,23 @@ def _wgrad_on(stream, fn, inputs):
     return out
 
 
+class GradSink:
+    """Hands a residual block's skip-path gradient (produced by the second
+    normalisation's backward, ops/norm.py _NormAct) to the block's first conv,
+    whose input-gradient kernel adds it in its epilogue (conv3x3_halo
+    accumulate): no separate add over the block input's gradient.  ``armed``
+    is set by a first conv that will consume it; unarmed, the norm returns
+    the skip gradient to autograd as usual."""
+    __slots__ = ("armed", "dres")
+
+    def __init__(self):
+        self.armed = False
+        self.dres = None
+
+
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, hold, wstream, stats):
+    def forward(ctx, x, weight, hold, wstream, stats, sink=None):
         weight = hold.p
         ctx.param, ctx.wstream = weight, wstream
         xn = _nhwc(x)
@@ -190,6 +204,9 @@ class _Conv3x3(torch.autograd.Function):
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
         _conv3x3_into(xn, wp, cin, cout, out, P, stats)
         ctx.save_for_backward(x)
+        ctx.sink = sink if sink is not None and _halo_ok(cout, cin) else None
+        if ctx.sink is not None:
+            ctx.sink.armed = True
         return out.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -204,12 +221,18 @@ class _Conv3x3(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             wd = _packed(weight, True)
-            dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
-            _conv3x3_into(dyn, wd, cout, cin, dxn, P)
+            sink = ctx.sink
+            if sink is not None and sink.dres is not None:
+                # dX = skip gradient + dgrad, accumulated in the halo kernel's epilogue
+                dxn, sink.dres = sink.dres, None
+                torch.ops.raft_stir.conv3x3_halo(dyn, wd, dxn, cout, cin, accumulate=True)
+            else:
+                dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
+                _conv3x3_into(dyn, wd, cout, cin, dxn, P)
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 # csrc/enc_wgrad.hip: all nine taps of a 64 x 64 channel slice per block over
@@ -244,11 +267,12 @@ def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
         [0, 0], 1, [False, True, False])[1].to(weight.dtype)
 
 
-def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
+def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None, sink=None) -> torch.Tensor:
     """conv(x) without its bias (see :func:`eligible`); ``stats``: see
-    :func:`_conv3x3_into`."""
+    :func:`_conv3x3_into`; ``sink``: a :class:`GradSink` whose skip gradient
+    the input gradient absorbs."""
     w, st = _weight_in(conv.weight)
-    return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats)
+    return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats, sink)
 
 
 # ------------------------------------------------------------------- 7x7 stem

@@ -38,12 +38,13 @@ def _nhwc(x):
 
 class _NormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, mean, rstd, relu, batch_stats, bias=None):
+    def forward(ctx, x, gamma, beta, res, mean, rstd, relu, batch_stats, bias=None, sink=None):
         xn = _nhwc(x)
         rn = _nhwc(res) if res is not None else None
         y = torch.ops.raft_stir.norm_act(xn, mean, rstd, gamma, beta, rn, relu)
         ctx.save_for_backward(x, gamma, beta, res, mean, rstd)
         ctx.relu, ctx.batch_stats = relu, batch_stats
+        ctx.sink = sink
         ctx.bias_meta = (bias.shape, bias.dtype) if bias is not None else None
         return y.permute(0, 3, 1, 2)
 
@@ -65,6 +66,9 @@ class _NormAct(torch.autograd.Function):
             dgamma = s2.sum(0) if want_g else None
             dbeta = s1.sum(0) if want_b else None
         dres_out = dres.permute(0, 3, 1, 2) if res is not None else None
+        if res is not None and ctx.sink is not None and ctx.sink.armed:
+            # the block's first conv adds it into its input gradient (enc_conv.GradSink)
+            ctx.sink.dres, dres_out = dres, None
         dbias = None
         if ctx.bias_meta is not None and ctx.needs_input_grad[8]:
             shape, dtype = ctx.bias_meta
@@ -75,7 +79,7 @@ class _NormAct(torch.autograd.Function):
             else:  # running statistics: d pre / d bias = gamma * rstd
                 g = gamma.float() if gamma is not None else 1.0
                 dbias = (s1.sum(0) * g * rstd.reshape(-1)).to(dtype)
-        return dx.permute(0, 3, 1, 2), dgamma, dbeta, dres_out, None, None, None, None, dbias
+        return dx.permute(0, 3, 1, 2), dgamma, dbeta, dres_out, None, None, None, None, dbias, None
 
 
 def _hip_ok(norm, x, residual):
@@ -216,7 +220,8 @@ def _eval_fused_ok(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, residual) 
     return residual is None and enc_conv.eligible_geo(conv, x)
 
 
-def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None, stats=None):
+def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None, stats=None,
+             res_sink=None):
     """``bias``: the producing convolution's bias, folded into the statistics
     (see :func:`conv_norm_act`); None if already applied.  ``stats``: the
     (sums buffer, per_sample) the producing conv filled (:func:`_stats_request`)."""
@@ -243,7 +248,7 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
             return torch.ops.raft_stir.norm_stats(xn, per_sample, norm.eps)
     if isinstance(norm, nn.InstanceNorm2d):
         mean, rstd = batch_moments(True)
-        return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True, bias)
+        return _NormAct.apply(x, None, None, residual, mean, rstd, relu, True, bias, res_sink)
     # BatchNorm2d
     batch_stats = norm.training
     if batch_stats:
@@ -270,7 +275,7 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
     else:
         mean, rstd = _eval_moments(norm, bias)
     return _NormAct.apply(x, norm.weight, norm.bias, residual, mean.contiguous(), rstd.contiguous(),
-                          relu, batch_stats, bias)
+                          relu, batch_stats, bias, res_sink)
 
 
 def _eval_moments(norm: nn.BatchNorm2d, bias):
@@ -295,12 +300,16 @@ def _norm_kind_ok(norm):
     return False
 
 
-def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None):
+def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
+                  grad_sink=None, res_sink=None):
     """``norm_act(norm, conv(x), relu, residual)``.  On the GPU path the conv
     runs without its bias and the bias is folded into the normalisation
     (instance / train-mode batch norm remove it exactly; eval-mode batch norm
     shifts its running mean by it): no bias-add pass over the conv output
-    forward and no bias-gradient reduction over it backward."""
+    forward and no bias-gradient reduction over it backward.  ``grad_sink`` /
+    ``res_sink``: an enc_conv.GradSink shared by a residual block's first conv
+    (absorbs the skip gradient in its input gradient) and its second norm
+    (hands the skip gradient over instead of returning it)."""
     if enc_conv.sconv_eligible(conv, x, residual):  # narrow channels (RAFT-small encoders), inference
         if isinstance(norm, nn.Sequential) and len(norm) == 0:  # norm_fn 'none': all in the conv epilogue
             return enc_conv.sconv(conv, x, True, relu, residual)
@@ -328,7 +337,8 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
                         stats=st)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
         st = _stats_request(norm, x, conv.out_channels)
-        return norm_act(norm, enc_conv.conv3x3(conv, x, st), relu, residual, bias=conv.bias, stats=st)
+        return norm_act(norm, enc_conv.conv3x3(conv, x, st, sink=grad_sink), relu, residual, bias=conv.bias,
+                        stats=st, res_sink=res_sink)
     if enc_conv.eligible_geo(conv, x):  # stride-2 3x3 / 1x1 (strided geometry of the same kernels)
         st = _stats_request(norm, x, conv.out_channels)
         return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False, stats=st), relu, residual, bias=conv.bias,
