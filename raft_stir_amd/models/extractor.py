@@ -27,12 +27,19 @@ correlation MFMA GEMM (csrc/corr_volume.hip).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops import enc_conv
 from ..ops.fp32conv import conv_module
 from ..ops.norm import conv_norm_act, conv_pair_norm_act
+
+
+# RS_RES_SINK=0: the residual blocks' skip gradient returns to autograd (a
+# separate add) instead of the first conv's input-gradient epilogue (A/B)
+_RES_SINK = os.environ.get("RS_RES_SINK", "1") != "0"
 
 
 def make_norm(kind: str, channels: int, groups: int) -> nn.Module:
@@ -68,7 +75,7 @@ class ResidualBlock(nn.Module):
         sink = None
         if self.downsample is None:
             # the skip gradient goes straight into conv1's input-gradient epilogue
-            sink = enc_conv.GradSink() if x.is_cuda else None
+            sink = enc_conv.GradSink() if (x.is_cuda and _RES_SINK) else None
             y, skip = conv_norm_act(self.conv1, self.norm1, x, grad_sink=sink), x
         else:
             y, skip = conv_pair_norm_act(self.conv1, self.norm1, self.downsample[0], self.norm3, x)

@@ -69,28 +69,31 @@ def use_hip(*tensors) -> bool:
     tracing/export always takes the ATen path so exported graphs hold only
     standard ops.
     """
-    if _exporting():
-        return False
     dev = None
     for t in tensors:
         if isinstance(t, torch.Tensor):
             dev = t.device
             break
-    if dev is None or dev.type != "cuda":
+    if dev is None or dev.type != "cuda" or _exporting():
         return False
-    load(raise_on_error=True)
+    if not _LOADED:
+        load(raise_on_error=True)
     return True
 
 
+try:  # bound once: called for every op dispatch on the hot path
+    _onnx_exporting = torch.onnx.is_in_onnx_export
+except Exception:  # pragma: no cover - onnx namespace unavailable
+    _onnx_exporting = lambda: False  # noqa: E731
+
+
 def _exporting() -> bool:
-    if torch.jit.is_tracing() or torch.jit.is_scripting():
+    if _FORCE_REFERENCE[0] or torch.jit.is_tracing() or torch.jit.is_scripting():
         return True
     try:
-        if torch.onnx.is_in_onnx_export():
-            return True
+        return bool(_onnx_exporting())
     except Exception:
-        pass
-    return _FORCE_REFERENCE[0]
+        return False
 
 
 _FORCE_REFERENCE = [False]
