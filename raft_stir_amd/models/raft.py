@@ -134,9 +134,10 @@ class RAFT(nn.Module):
         """slot 0: context encoder / flow branch; slot 1: deferred weight gradients."""
         st = _SIDE_STREAMS.get((dev.index, slot))
         if st is None:
-            # RS_SIDE_PRIO: priority of the context-encoder / flow-branch stream
-            # (lower = more urgent; the deferred weight-gradient stream keeps the default)
-            prio = int(os.environ.get("RS_SIDE_PRIO", "0")) if slot == 0 else 0
+            # RS_SIDE_PRIO / RS_WGRAD_PRIO: priority of the context-encoder /
+            # flow-branch stream and of the deferred weight-gradient stream
+            # (lower = more urgent; A/B switches, default 0)
+            prio = int(os.environ.get("RS_SIDE_PRIO" if slot == 0 else "RS_WGRAD_PRIO", "0"))
             st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev, priority=prio)
         return st
 
