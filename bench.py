@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--fp32", action="store_true", help="disable bf16 autocast")
+    ap.add_argument("--alternate-corr", action="store_true",
+                    help="on-the-fly (memory-efficient) correlation instead of the all-pairs pyramid")
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--infer-size", type=int, nargs=2, default=[436, 1088])
     ap.add_argument("--infer-reps", type=int, default=20)
@@ -116,7 +118,8 @@ def main():
         torch.cuda.set_device(dev)
     torch.manual_seed(1234)
 
-    margs = make_args(small=a.small, mixed_precision=not a.fp32 and not cpu, corr_dtype=a.corr_dtype)
+    margs = make_args(small=a.small, mixed_precision=not a.fp32 and not cpu, corr_dtype=a.corr_dtype,
+                      alternate_corr=a.alternate_corr)
     model = RAFT(margs).to(dev)
     if not cpu:
         model = model.to(memory_format=torch.channels_last)
@@ -202,6 +205,7 @@ def main():
                 "parallelism": f"dp{info.world_size}",
                 "ops": "stock-pytorch (reference semantics)" if (a.reference_ops or cpu) else "hip-kernels",
                 "corr_pyramid": "fp32" if (a.reference_ops or cpu) else str(model_cfg_pyr(model)),
+                "correlation": "on-the-fly" if a.alternate_corr else "all-pairs",
                 "train_step": "hipgraph" if use_graph else "eager",
                 "grad_allreduce": ("none" if info.world_size == 1 else
                                    "rccl: packed update-block buffer + DDP encoder buckets"
