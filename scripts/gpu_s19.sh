@@ -15,3 +15,4 @@ done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/potf -o t -- python3 bench.py --steps 3 --warmup 2 --no-infer --small --alternate-corr > gpurun_out/s19/prof_otf.log 2>&1 || { tail -5 gpurun_out/s19/prof_otf.log; exit 1; }
 find /tmp/potf -name "*kernel_stats.csv" -exec cp {} gpurun_out/s19/small_otf_kernel_stats.csv \;
 python3 scripts/prof_categories.py gpurun_out/s19/small_otf_kernel_stats.csv 5 2>&1 | head -16 || true
+timeout -k 10 900 python -u scripts/fidelity_ensemble.py --seeds 3 > gpurun_out/s19/fid_ens.log 2>&1; grep -v "amdgpu\|Warning\|sched.step" gpurun_out/s19/fid_ens.log
