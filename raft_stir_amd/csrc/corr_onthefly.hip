@@ -404,6 +404,190 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
   }
 }
 
+// ------------------------------------------------------- tiled backward
+// The per-query backward (otf_bwd_kernel) scatters every cell gradient times
+// the query's f1 into df2 with one atomic per (query, cell, channel): 16k
+// atomics per query and level at r = 3, C = 128.  Here a block owns the same
+// 4 x 4 query tile as otf_tile_kernel; per level:
+//  * the tile's cell gradients G[q][cell] over the bounding box of the 16
+//    windows are gathered into LDS (each window cell sums its <= 4 taps, the
+//    reverse of the forward's bilinear taps -- no LDS atomics);
+//  * per 32-channel chunk the box's f2 cells are staged in LDS (fp32), then
+//    half the block accumulates df1[q][c] = sum_cell G[q][cell] f2[cell][c]
+//    (registers, summed over chunks and levels, one plain store per query at
+//    the end) while the other half forms df2[cell][c] = sum_q G[q][cell]
+//    f1[q][c] for the box and issues ONE atomic per (cell, channel) for the
+//    whole tile (fp32 atomics, or 32.32 fixed point in deterministic mode);
+//  * a box wider than MAXC cells (incoherent flow inside the tile) is
+//    processed one query window at a time with the same machinery.
+template <typename T, typename GT, int CQ, bool DET>
+__global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__ f1, Lvl f2, int levels,
+                                                           const float* __restrict__ coords, int B, int H1,
+                                                           int W1, int tiles_x, int tiles_y, int per_xcd, int r,
+                                                           float scale, const GT* __restrict__ dout,
+                                                           float* __restrict__ df1, LvlMut df2) {
+  constexpr int C = CQ * 32;
+  __shared__ float Gs[16][MAXC];
+  __shared__ float f2s[MAXC][33];
+  __shared__ float f1s[16][C];
+  __shared__ int qX0[16], qY0[16], qn[16];
+  __shared__ float qfx[16], qfy[16];
+  const int t = threadIdx.x;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (tile >= B * tiles_x * tiles_y) return;  // whole block, before any barrier
+  const int b = tile / (tiles_x * tiles_y), t2 = tile % (tiles_x * tiles_y);
+  const int ty = t2 / tiles_x, tx = t2 % tiles_x;
+  const int N1 = H1 * W1;
+  const int D = 2 * r + 1, K2 = D * D, E = D + 1, E2 = E * E, CH = levels * K2;
+
+  if (t < 16) {
+    const int y = ty * TQ + (t >> 2), x = tx * TQ + (t & 3);
+    qn[t] = (y < H1 && x < W1) ? y * W1 + x : -1;
+  }
+  __syncthreads();
+  for (int i = t; i < 16 * C; i += 256) {
+    const int q = i / C, c = i % C;
+    f1s[q][c] = qn[q] >= 0 ? io<T>::ld(f1 + ((size_t)b * N1 + qn[q]) * C + c) : 0.f;
+  }
+  // df1 accumulators: threads 0..127 own query dq = t >> 3, channels 32 k + 4 cg .. + 4 of every chunk k
+  float a1[CQ][4];
+#pragma unroll
+  for (int k = 0; k < CQ; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a1[k][j] = 0.f;
+
+  for (int l = 0; l < levels; ++l) {
+    const int H = f2.H[l], W = f2.W[l];
+    if (t < 16) {
+      const int n = qn[t] >= 0 ? qn[t] : 0;
+      const float inv = 1.f / (float)(1 << l);
+      const float cx = coords[((size_t)b * 2 + 0) * N1 + n] * inv, cy = coords[((size_t)b * 2 + 1) * N1 + n] * inv;
+      const float bx = floorf(cx), by = floorf(cy);
+      qX0[t] = (int)bx - r;
+      qY0[t] = (int)by - r;
+      qfx[t] = cx - bx;
+      qfy[t] = cy - by;
+    }
+    __syncthreads();
+    int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -0x7fffffff, ymx = -0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (qn[q] >= 0) {
+        xmn = min(xmn, qX0[q]);
+        xmx = max(xmx, qX0[q]);
+        ymn = min(ymn, qY0[q]);
+        ymx = max(ymx, qY0[q]);
+      }
+    const bool fallback = (xmx - xmn + E) * (ymx - ymn + E) > MAXC;  // identical in every thread
+    const T* f2b = static_cast<const T*>(f2.p[l]) + (size_t)b * H * W * C;
+    for (int sub = 0; sub < (fallback ? 16 : 1); ++sub) {
+      if (fallback && qn[sub] < 0) continue;  // uniform
+      const int bx0 = fallback ? qX0[sub] : xmn, by0 = fallback ? qY0[sub] : ymn;
+      const int bw = fallback ? E : xmx - xmn + E, bh = fallback ? E : ymx - ymn + E;
+      const int nc = bw * bh;
+      for (int i = t; i < 16 * MAXC; i += 256) (&Gs[0][0])[i] = 0.f;
+      __syncthreads();
+      // G[q][box cell]: each window cell (ca along x, cc along y) sums its <= 4 taps
+      for (int i = t; i < 16 * E2; i += 256) {
+        const int q = i / E2, cell = i - q * E2;
+        if (qn[q] < 0 || (fallback && q != sub)) continue;
+        const int ca = cell / E, cc = cell - ca * E;
+        const float fx = qfx[q], fy = qfy[q];
+        const GT* g = dout + ((size_t)b * N1 + qn[q]) * CH + l * K2;
+        float acc = 0.f;
+#pragma unroll
+        for (int di = 0; di < 2; ++di) {
+          const int ii = ca - di;
+          if (ii < 0 || ii >= D) continue;
+          const float wx = di == 0 ? (1.f - fx) : fx;
+#pragma unroll
+          for (int dj = 0; dj < 2; ++dj) {
+            const int jj = cc - dj;
+            if (jj < 0 || jj >= D) continue;
+            const float wy = dj == 0 ? (1.f - fy) : fy;
+            acc += wx * wy * io<GT>::ld(g + ii * D + jj);
+          }
+        }
+        Gs[q][(qY0[q] + cc - by0) * bw + (qX0[q] + ca - bx0)] = acc * scale;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < CQ; ++k) {
+        for (int i = t; i < nc * 8; i += 256) {  // f2 box cells, 32-channel chunk k, 4 channels per piece
+          const int cell = i >> 3, pc = i & 7;
+          const int X = bx0 + cell % bw, Y = by0 + cell / bw;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (X >= 0 && X < W && Y >= 0 && Y < H) v = ld4<T>(f2b + ((size_t)Y * W + X) * C + 32 * k + 4 * pc);
+          f2s[cell][4 * pc + 0] = v.x;
+          f2s[cell][4 * pc + 1] = v.y;
+          f2s[cell][4 * pc + 2] = v.z;
+          f2s[cell][4 * pc + 3] = v.w;
+        }
+        __syncthreads();
+        if (t < 128) {  // df1[q][32 k + 4 cg ..] += sum_cell G[q][cell] f2[cell][..]
+          const int dq = t >> 3, cg = t & 7;
+          float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+          for (int cell = 0; cell < nc; ++cell) {
+            const float gv = Gs[dq][cell];
+            s0 += gv * f2s[cell][4 * cg + 0];
+            s1 += gv * f2s[cell][4 * cg + 1];
+            s2 += gv * f2s[cell][4 * cg + 2];
+            s3 += gv * f2s[cell][4 * cg + 3];
+          }
+          a1[k][0] += s0;
+          a1[k][1] += s1;
+          a1[k][2] += s2;
+          a1[k][3] += s3;
+        } else {  // df2[box cell][32 k + 4 cg ..] += sum_q G[q][cell] f1[q][..]: one atomic per element per tile
+          const int u = t - 128, cg = u & 7;
+          for (int cell = u >> 3; cell < nc; cell += 16) {
+            const int X = bx0 + cell % bw, Y = by0 + cell / bw;
+            if (X < 0 || X >= W || Y < 0 || Y >= H) continue;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const float gv = Gs[q][cell];
+              if (gv != 0.f) {
+                any = true;
+                s0 += gv * f1s[q][32 * k + 4 * cg + 0];
+                s1 += gv * f1s[q][32 * k + 4 * cg + 1];
+                s2 += gv * f1s[q][32 * k + 4 * cg + 2];
+                s3 += gv * f1s[q][32 * k + 4 * cg + 3];
+              }
+            }
+            if (!any) continue;
+            const size_t off = ((size_t)b * H * W + (size_t)Y * W + X) * C + 32 * k + 4 * cg;
+            if constexpr (DET) {
+              unsigned long long* d = reinterpret_cast<unsigned long long*>(df2.p[l]) + off;
+              fx_add(d + 0, s0);
+              fx_add(d + 1, s1);
+              fx_add(d + 2, s2);
+              fx_add(d + 3, s3);
+            } else {
+              float* d = df2.p[l] + off;
+              atomicAdd(d + 0, s0);
+              atomicAdd(d + 1, s1);
+              atomicAdd(d + 2, s2);
+              atomicAdd(d + 3, s3);
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (t < 128) {
+    const int dq = t >> 3, cg = t & 7;
+    if (qn[dq] >= 0) {
+      float* o = df1 + ((size_t)b * N1 + qn[dq]) * C;
+#pragma unroll
+      for (int k = 0; k < CQ; ++k)
+        *reinterpret_cast<float4*>(o + 32 * k + 4 * cg) = make_float4(a1[k][0], a1[k][1], a1[k][2], a1[k][3]);
+    }
+  }
+}
+
 // 32.32 fixed point (int64) -> fp32
 __global__ __launch_bounds__(256) void fx_to_f32_kernel(const long long* __restrict__ in, long n,
                                                         float* __restrict__ out) {
@@ -472,9 +656,10 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 // det: df2[l] are int64 fixed-point accumulators (zeroed) of the level sizes;
 // df2f[l] receive their fp32 values
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
-                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
                          float* const* df2, bool det, float* const* df2f, hipStream_t stream) {
+  const int N1 = H1 * W1;
   otf::Lvl p;
   otf::LvlMut d;
   for (int l = 0; l < 4; ++l) {
@@ -483,9 +668,35 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     p.H[l] = d.H[l] = l < levels ? Hs[l] : 0;
     p.W[l] = d.W[l] = l < levels ? Ws[l] : 0;
   }
+  const int cq = C / 32;
+  static const bool tile_env = [] {  // RS_OTF_TILE=0 or RS_OTF_TILE_BWD=0: per-query backward (A/B)
+    const char* e = getenv("RS_OTF_TILE");
+    const char* e2 = getenv("RS_OTF_TILE_BWD");
+    return !(e && e[0] == '0') && !(e2 && e2[0] == '0');
+  }();
+  if (tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+    const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
+    const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
+#define RS_LT(T, GT)                                                                                      \
+  if (det)                                                                                                \
+    hipLaunchKernelGGL((otf::otf_tile_bwd_kernel<T, GT, CQ, true>), dim3(8 * per_xcd), dim3(256), 0, stream, \
+                       static_cast<const T*>(f1), p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, \
+                       scale, static_cast<const GT*>(dout), df1, d);                                       \
+  else                                                                                                    \
+    hipLaunchKernelGGL((otf::otf_tile_bwd_kernel<T, GT, CQ, false>), dim3(8 * per_xcd), dim3(256), 0, stream, \
+                       static_cast<const T*>(f1), p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, \
+                       scale, static_cast<const GT*>(dout), df1, d)
+    if (fm_bf16) {
+      if (dout_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_LT(bf16_t, bf16_t)); }
+      else { RS_OTF_DISPATCH_CQ(cq, RS_LT(bf16_t, float)); }
+    } else {
+      if (dout_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_LT(float, bf16_t)); }
+      else { RS_OTF_DISPATCH_CQ(cq, RS_LT(float, float)); }
+    }
+#undef RS_LT
+  } else {
   const long npix = (long)B * N1;
   dim3 grid((unsigned)cdiv((int)npix, otf::WAVES)), block(otf::WAVES * 64);
-  const int cq = C / 32;
 #define RS_L(T, GT)                                                                          \
   if (det)                                                                                   \
     hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ, true>), grid, block, 0, stream,       \
@@ -503,6 +714,7 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     else { RS_OTF_DISPATCH_CQ(cq, RS_L(float, float)); }
   }
 #undef RS_L
+  }
   if (det)
     for (int l = 0; l < levels; ++l) {
       const long n = (long)B * Hs[l] * Ws[l] * C;

@@ -49,7 +49,7 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
                          int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, void* out, bool out_bf16, hipStream_t stream);
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
-                         int levels, bool fm_bf16, const float* coords, int B, int N1, int C,
+                         int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
                          float* const* df2, bool det, float* const* df2f, hipStream_t stream);
 void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, int N, int H, int W,
@@ -398,7 +398,7 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
     }
   }
   rs::corr_otf_bwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
-                          B, H1 * W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
+                          B, H1, W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
                           df1.data_ptr<float>(), d, det, df, cur_stream());
   RS_CHECK_LAUNCH();
   return res;

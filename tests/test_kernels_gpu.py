@@ -183,6 +183,56 @@ def test_onthefly_tiled_forward(cuda, C, r, out_bf16):
     torch.testing.assert_close(got, want.detach(), rtol=ftol, atol=ftol)
 
 
+@pytest.mark.parametrize("C,r", [(256, 4), (128, 3), (96, 4)])
+@pytest.mark.parametrize("det", [False, True])
+def test_onthefly_tiled_backward(cuda, C, r, det):
+    """csrc/corr_onthefly.hip otf_tile_bwd_kernel (4 x 4 query tiles: cell
+    gradients gathered over the tile's bounding box, one df2 atomic per
+    (cell, channel) per tile, per-window fallback for incoherent tiles) vs
+    fp32 autograd through a per-level bilinear oracle (ops/reference.py
+    corr_onthefly with the pooled levels as leaves).  Deterministic mode
+    (32.32 fixed-point atomics) is bitwise repeatable."""
+    B, H, W = 2, 23, 38
+    f1, f2 = _fmaps(B, C, H, W, "cpu", seed=31)
+    f1, f2 = f1.bfloat16().float(), f2.bfloat16().float()
+    g = torch.Generator().manual_seed(6)
+    base = ref.coords_grid(B, H, W)
+    ys, xs = base[:, 1:2], base[:, 0:1]
+    flow = torch.cat([3.0 + 0.08 * xs - 0.05 * ys, -2.0 + 0.04 * ys], 1) + 0.3 * torch.randn(B, 2, H, W, generator=g)
+    flow[:, :, 8:13] = 9.0 * torch.randn(B, 2, 5, W, generator=g)  # incoherent band: fallback tiles
+    flow[1, 0, :, -6:] += 30.0  # off the right edge
+    coords = base + flow
+    f2l = [f2]
+    for _ in range(3):
+        f2l.append(F.avg_pool2d(f2l[-1], 2, stride=2))
+    f2l = [t.bfloat16().float() for t in f2l]  # the op stores the pooled levels in bf16
+    a1 = f1.clone().requires_grad_()
+    a2 = [t.clone().requires_grad_() for t in f2l]
+    delta = ref._window_delta(r, coords.device, coords.dtype).reshape(-1, 2)
+    pos0 = coords.permute(0, 2, 3, 1)
+    outs = []
+    for lvl, t in enumerate(a2):
+        outs += [(ref.bilinear_sampler(t, pos0 / 2 ** lvl + delta[k]) * a1).sum(1) for k in range(delta.shape[0])]
+    want = torch.stack(outs, -1) / math.sqrt(C)  # (B, H, W, L*K2)
+    dout = torch.randn(want.shape, generator=g)
+    (want * dout).sum().backward()
+
+    b1 = f1.to(cuda, torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+    b2 = [t.to(cuda, torch.bfloat16).permute(0, 2, 3, 1).contiguous() for t in f2l]
+    args = (b1, b2, coords.to(cuda), r, 1.0 / math.sqrt(C), dout.to(cuda))
+    torch.ops.raft_stir.set_deterministic(det)
+    try:
+        got = torch.ops.raft_stir.corr_otf_backward(*args)
+        if det:
+            again = torch.ops.raft_stir.corr_otf_backward(*args)
+            assert all(torch.equal(x, y) for x, y in zip(got, again))
+    finally:
+        torch.ops.raft_stir.set_deterministic(False)
+    torch.testing.assert_close(got[0].cpu(), a1.grad.permute(0, 2, 3, 1), rtol=1e-4, atol=1e-4)
+    for lvl in range(4):
+        torch.testing.assert_close(got[1 + lvl].cpu(), a2[lvl].grad.permute(0, 2, 3, 1), rtol=1e-4, atol=1e-4)
+
+
 def test_onthefly_matches_allpairs(cuda):
     """pyramid[l] == corr(f1, avgpool^l f2): both paths agree."""
     from raft_stir_amd.ops.corr import OnTheFlyCorr, AllPairsCorr
