@@ -1005,10 +1005,8 @@ struct ConvLaunch {
   unsigned w_bytes;
   int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
   int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
-  // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
+  // EPI_NORM per-channel scale (conv_common.h Args)
   const float* chs;
-  float* stats;
-  int stats_ps;
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 
@@ -1033,7 +1031,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.aux2 = static_cast<const bf16_t*>(L.aux2); a.a2str = L.a2str; a.a2off = L.a2off;
   for (int s = 0; s < 3; ++s) a.seg_bytes[s] = L.seg_bytes[s];
   a.w_bytes = L.w_bytes;
-  a.chs = L.chs; a.stats = L.stats; a.stats_ps = L.stats_ps;
+  a.chs = L.chs;
   a.f32 = L.f32;
   static const int xcd_env = [] {
     const char* e = getenv("RS_CONV_XCD_REMAP");

@@ -63,13 +63,8 @@ struct Args {
   // output pixel ((b*oH + y*OSY + OOY)*oW + x*OSX + OOX)
   int Hi, Wi, SY, SX;
   int oH, oW, OSY, OSX, OOY, OOX;
-  // EPI_NORM per-channel scale; normalisation statistics of the stored output
-  // (bf16-rounded acc + bias): stats[(g * Cout + co) * 2 + {0, 1}] += {sum, sum of
-  // squares} with g = image (stats_ps) or 0 (vector atomics; the buffer is
-  // zeroed by whoever consumes it, ops/norm.py)
+  // EPI_NORM per-channel scale
   const float* chs;
-  float* stats;
-  int stats_ps;
   int f32;  // fp32 activations / outputs (conv_lds_kernel<..., F32>, epilogue_pix_f32)
 };
 
@@ -349,86 +344,10 @@ __device__ __forceinline__ void epi_loop(const Args& a, const f32x4_t (&acc)[WM]
   }
 }
 
-// Normalisation statistics of this wave's output tile (Args::stats).  The 16
-// lanes sharing lane >> 4 hold the same 4*WM channels at 16 pixels each: per
-// lane sums over the n-tiles, a reduce-scatter over those 16 lanes, then one
-// atomic per (channel, statistic) per wave.  A tile whose pixels span two
-// images (per-sample statistics only) takes per-element atomics instead.
-template <int WM, int WN, bool RND = true>
-__device__ __forceinline__ void stats_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
-                                          const int (&pb)[WN]) {
-  // RND: statistics of the bf16-rounded stored values (bf16 outputs), else of the fp32 values
-  auto rnd = [](float x) { return RND ? bf2f(f2bf(x)) : x; };
-  const int b0 = __builtin_amdgcn_readfirstlane(pb[0]);  // lane 0 / n-tile 0 holds the wave's first pixel
-  if (b0 < 0) return;
-  bool same = true;
-#pragma unroll
-  for (int nt = 0; nt < WN; ++nt) same = same && (pb[nt] < 0 || pb[nt] == b0);
-  const int cq = (lane >> 4) * 4;
-  float bs[WM][4];
-#pragma unroll
-  for (int mt = 0; mt < WM; ++mt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = m0 + mt * 16 + cq + j;
-      bs[mt][j] = a.bias && c < a.Cout ? a.bias[c] : 0.f;
-    }
-  if (!a.stats_ps || __all(same)) {
-    constexpr int NV = (WM * 8 + 15) / 16 * 16;
-    float v[NV];
-#pragma unroll
-    for (int mt = 0; mt < WM; ++mt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < WN; ++nt) {
-          const float x = pb[nt] >= 0 ? rnd(acc[mt][nt][j] + bs[mt][j]) : 0.f;
-          s1 += x;
-          s2 += x * x;
-        }
-        v[mt * 4 + j] = s1;
-        v[WM * 4 + mt * 4 + j] = s2;
-      }
-#pragma unroll
-    for (int i = WM * 8; i < NV; ++i) v[i] = 0.f;
-    lane_reduce_scatter<NV, 16>(v, lane);
-    constexpr int K = NV / 16;
-    float* st = a.stats + (size_t)(a.stats_ps ? b0 : 0) * a.Cout * 2;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int e = K * (lane & 15) + k;
-      if (e < WM * 8) {
-        const int stat = e / (WM * 4), slot = e % (WM * 4);
-        const int c = m0 + (slot / 4) * 16 + cq + (slot % 4);
-        if (c < a.Cout) atomicAdd(st + c * 2 + stat, v[k]);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int nt = 0; nt < WN; ++nt) {
-      if (pb[nt] < 0) continue;
-      float* st = a.stats + (size_t)pb[nt] * a.Cout * 2;
-#pragma unroll
-      for (int mt = 0; mt < WM; ++mt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = m0 + mt * 16 + cq + j;
-          if (c < a.Cout) {
-            const float x = rnd(acc[mt][nt][j] + bs[mt][j]);
-            atomicAdd(st + c * 2, x);
-            atomicAdd(st + c * 2 + 1, x * x);
-          }
-        }
-    }
-  }
-}
-
 template <int WM, int WN>
 __device__ __forceinline__ void epilogue_pix(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
                                              const int (&pp)[WN], const int (&pb)[WN], const int (&py)[WN],
                                              const int (&px)[WN]) {
-  if (a.stats) stats_pix<WM, WN>(a, acc, m0, lane, pb);
   switch (a.epi) {
 #define RS_EPI(E) \
   case E: epi_loop<WM, WN, E>(a, acc, m0, lane, pp, pb, py, px); break
@@ -598,7 +517,6 @@ __device__ __forceinline__ void epi_loop_f32(const Args& a, const f32x4_t (&acc)
 template <int WM, int WN>
 __device__ __forceinline__ void epilogue_pix_f32(const Args& a, const f32x4_t (&acc)[WM][WN], int m0, int lane,
                                                  const int (&pp)[WN], const int (&pb)[WN]) {
-  if (a.stats) stats_pix<WM, WN, false>(a, acc, m0, lane, pb);
   switch (a.epi) {
 #define RS_EPI32(E) \
   case E: epi_loop_f32<WM, WN, E>(a, acc, m0, lane, pp, pb); break

@@ -10,7 +10,5 @@ struct EncEpi {
   const uint16_t* res = nullptr;  // ... then relu(y + res)  (bf16 NHWC, rstr elements per pixel)
   int rstr = 0, relu = 0;
   int res_relu = 1;               // 0: plain y + res (res may alias y: in-place accumulation)
-  float* stats = nullptr;         // += (sum, sum of squares) per channel, [G][Cout][2]
-  int stats_ps = 0;               // G = images (1) or 1 (0)
 };
 }  // namespace rs

@@ -43,13 +43,10 @@ struct HArgs {
   int tpb;  // consecutive tiles per block
   // optional epilogue extras (ops_conv.cpp conv3x3_halo):
   //   chs / shift: y = [relu](acc * chs + shift) [then relu(y + res)] (eval-mode BatchNorm)
-  //   stats: += per-channel (sum, sum of squares) of the bf16 output, [G][Cout][2]
   const float* chs;
   const float* shift;
   const bf16_t* res;
   int rstr, relu, res_relu;
-  float* stats;
-  int stats_ps;
 };
 
 template <int CIN, int COB>
@@ -243,38 +240,6 @@ __global__ __launch_bounds__(256) void enc_halo_kernel(HArgs a) {
               }
           }
       }
-      if (a.stats) {
-        // per-channel (sum, sum of squares) over the wave's 32 x RPW pixels:
-        // sums over the rows in-lane, then a reduce-scatter over the 32 lanes
-        // of each half-wave; each lane then owns NV/32 totals (one atomic each)
-        constexpr int NS = C::NMF * 16, NV = 2 * NS;
-        float v[NV];
-#pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = 0.f;
-#pragma unroll
-        for (int r = 0; r < C::RPW; ++r) {
-          const int oy = th * C::TH + wave * C::RPW + r;
-          if (oy < a.H && ox < a.W) {
-#pragma unroll
-            for (int mi = 0; mi < C::NMF; ++mi)
-#pragma unroll
-              for (int k = 0; k < 16; ++k) {
-                const float x = bf2f(f2bf(acc[r][mi][k]));
-                v[mi * 16 + k] += x;
-                v[NS + mi * 16 + k] += x * x;
-              }
-          }
-        }
-        lane_reduce_scatter<NV, 32>(v, lane);
-        float* st = a.stats + (size_t)(a.stats_ps ? bi : 0) * a.Cout * 2;
-#pragma unroll
-        for (int q = 0; q < NV / 32; ++q) {
-          const int e = (NV / 32) * (lane & 31) + q;
-          const int stat = e / NS, slot = e % NS;  // slot = mi*16 + 4g + j
-          const int c = co0 + (slot / 16) * 32 + 8 * ((slot % 16) / 4) + 4 * (lane >> 5) + (slot % 4);
-          if (c < a.Cout) atomicAdd(st + c * 2 + stat, v[q]);
-        }
-      }
 #pragma unroll
       for (int r = 0; r < C::RPW; ++r) {
         const int oy = th * C::TH + wave * C::RPW + r;
@@ -318,7 +283,7 @@ __global__ __launch_bounds__(256) void enc_halo_kernel(HArgs a) {
 
 // Supported (cin, cout-block) instantiations; false = caller falls back.
 bool enc_halo_supported(int cin, int cout) {
-  return (cin == 64 && cout % 64 == 0) || ((cin == 96 || cin == 128) && cout % 32 == 0);
+  return (cin == 64 && cout % 64 == 0) || (cin == 96 && cout % 32 == 0);
 }
 
 bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_t* y, int ystr, int B, int H, int W,
@@ -326,12 +291,12 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   if (!enc_halo_supported(cin, cout)) return false;
   ench::HArgs a{};
   a.chs = e.chs; a.shift = e.shift; a.res = e.res; a.rstr = e.rstr; a.relu = e.relu; a.res_relu = e.res_relu;
-  a.stats = e.stats; a.stats_ps = e.stats_ps;
   a.x = x; a.w = w; a.y = y;
   a.xstr = xstr; a.ystr = ystr; a.Ktot = Ktot;
   a.B = B; a.H = H; a.W = W; a.Cout = cout;
   a.tiles_w = cdiv(W, 32);
-  a.tiles_img = cdiv(H, cin == 128 ? ench::Cfg<128, 32>::TH : ench::Cfg<64, 64>::TH) * a.tiles_w;
+  static_assert(ench::Cfg<64, 64>::TH == ench::Cfg<96, 32>::TH, "one tile height for both channel counts");
+  a.tiles_img = cdiv(H, ench::Cfg<64, 64>::TH) * a.tiles_w;
   a.ntiles = B * a.tiles_img;
   if (a.ntiles == 0) return true;
   const int cob = cin == 64 ? 64 : 32;
@@ -352,10 +317,8 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   const int gx = cdiv(a.ntiles, a.tpb);
   if (cin == 64)
     hipLaunchKernelGGL((ench::enc_halo_kernel<64, 64>), dim3(gx, gy), dim3(256), 0, stream, a);
-  else if (cin == 96)
-    hipLaunchKernelGGL((ench::enc_halo_kernel<96, 32>), dim3(gx, gy), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL((ench::enc_halo_kernel<128, 32>), dim3(gx, gy), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((ench::enc_halo_kernel<96, 32>), dim3(gx, gy), dim3(256), 0, stream, a);
   return true;
 }
 

@@ -406,31 +406,7 @@ __global__ __launch_bounds__(256) void bn_running_kernel(const float* __restrict
   if (c == 0 && nbt) nbt[0] += 1;
 }
 
-// mean / rstd from the (sum, sum of squares) a convolution epilogue
-// accumulated (conv_common.h stats_pix, enc_halo.hip), then the sums are
-// zeroed for that conv's next use: sums [G][C][2] -> mean, rstd [G][C].
-// var = E[x^2] - mean^2 in fp64 from the fp32 sums (the inputs are conv outputs
-// without their bias, so |mean| is of the order of the spread).
-__global__ __launch_bounds__(256) void sums_finalize_kernel(float* __restrict__ sums, int GC, float inv_n, float eps,
-                                                            float* __restrict__ mean, float* __restrict__ rstd) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < GC) {
-    const float2 s = *reinterpret_cast<const float2*>(sums + 2 * i);
-    const double m = (double)s.x * inv_n;
-    double var = (double)s.y * inv_n - m * m;
-    var = var < 0.0 ? 0.0 : var;
-    mean[i] = (float)m;
-    rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
-    *reinterpret_cast<float2*>(sums + 2 * i) = make_float2(0.f, 0.f);
-  }
-}
-
 }  // namespace norm
-
-void norm_sums_finalize_launch(float* sums, int GC, float inv_n, float eps, float* mean, float* rstd, hipStream_t s) {
-  hipLaunchKernelGGL(norm::sums_finalize_kernel, dim3(cdiv(GC, 256)), dim3(256), 0, s, sums, GC, inv_n, eps, mean,
-                     rstd);
-}
 
 // ------------------------------------------------------------------ launchers
 int norm_ws_floats(int B, int P, int C, bool bf16) {

@@ -33,10 +33,8 @@ struct ConvLaunch {
   unsigned w_bytes;
   int geo;  // 1: strided / remapped geometry below (conv_lds tiles 2-4, 6-8)
   int Hi, Wi, SY, SX, oH, oW, OSY, OSX, OOY, OOX;
-  // EPI_NORM per-channel scale, normalisation statistics (conv_common.h Args)
+  // EPI_NORM per-channel scale (conv_common.h Args)
   const float* chs;
-  float* stats;
-  int stats_ps;
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 void conv_launch(const ConvLaunch& L, hipStream_t stream);
@@ -113,8 +111,7 @@ struct StemLaunch {  // must match stem.hip
   const void* res;
   int rstr;
   const float* chs;
-  float* stats;
-  int stats_ps, f32;
+  int f32;
 };
 void stem_launch(const StemLaunch& L, hipStream_t stream);
 int stem_wgrad_blocks(long P, int* px_per_block);
@@ -136,15 +133,10 @@ void check_nhwc(const Tensor& t, int B, int H, int W, const char* n, at::ScalarT
   TORCH_CHECK(t.scalar_type() == dt, n, ": ", dt, " required");
 }
 
-// Encoder-normalisation extras shared by conv_fused / conv_geo / conv3x3_halo:
-//   stats (fp32 [G][Cout][2], G = B if per_sample else 1): the kernel ADDS the
-//     per-channel sum and sum of squares of its bf16 output (the buffer is
-//     zeroed by its consumer, norm_finalize);
+// Encoder-normalisation extra shared by conv_fused / conv_geo / conv3x3_halo / stem_conv:
 //   nscale (fp32, >= round_up(Cout, 4), 16-B aligned; epi EPI_NORM only) with
 //     the bias as the shift: out = [relu](acc * nscale + bias) [then relu(. + aux1)].
 struct NormX {
-  float* stats = nullptr;
-  int stats_ps = 0;
   const float* chs = nullptr;
 };
 void check_vec4(const c10::optional<Tensor>& t, int Cout, const char* op, const char* n) {
@@ -152,18 +144,9 @@ void check_vec4(const c10::optional<Tensor>& t, int Cout, const char* op, const 
                   t->numel() >= (Cout + 3) / 4 * 4 && (uintptr_t)t->data_ptr() % 16 == 0,
               op, ": ", n, " must be 16-B aligned fp32 with round_up(Cout, 4) values");
 }
-NormX norm_extras(const c10::optional<Tensor>& stats, bool per_sample, const c10::optional<Tensor>& nscale,
-                  const c10::optional<Tensor>& bias, int epi, int B, int Cout, const char* op) {
+NormX norm_extras(const c10::optional<Tensor>& nscale, const c10::optional<Tensor>& bias, int epi, int Cout,
+                  const char* op) {
   NormX x;
-  if (stats) {
-    const int64_t G = per_sample ? B : 1;
-    TORCH_CHECK(stats->is_cuda() && stats->is_contiguous() && stats->scalar_type() == at::kFloat &&
-                    stats->numel() == G * Cout * 2,
-                op, ": stats must be contiguous fp32 [", G, "][", Cout, "][2]");
-    TORCH_CHECK(epi == 0, op, ": statistics are taken with the plain (bias) epilogue only");
-    x.stats = stats->data_ptr<float>();
-    x.stats_ps = per_sample ? 1 : 0;
-  }
   TORCH_CHECK(bool(nscale) == (epi == EPI_NORM), op, ": nscale is the EPI_NORM scale (and only that)");
   if (nscale) {
     check_vec4(nscale, Cout, op, "nscale");
@@ -308,10 +291,9 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
-  if (nx.stats || nx.chs)
-    TORCH_CHECK(!(tile >= 42 && tile <= 53),
-                "conv_fused: statistics / EPI_NORM need a tile with the shared epilogue (not 42-53)");
-  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
+  if (nx.chs)
+    TORCH_CHECK(!(tile >= 42 && tile <= 53), "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-53)");
+  L.chs = nx.chs;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();
 }
@@ -321,9 +303,8 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
                 int64_t epi, double scale, int64_t hd, const Tensor& out, int64_t ooff,
                 const c10::optional<Tensor>& out2, int64_t o2off, const c10::optional<Tensor>& out3,
                 int64_t o3off, const c10::optional<Tensor>& aux1, int64_t a1off,
-                const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile,
-                const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale) {
-  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, segs.at(0).size(0), Cout, "conv_fused");
+                const c10::optional<Tensor>& aux2, int64_t a2off, int64_t tile, const c10::optional<Tensor>& nscale) {
+  const NormX nx = norm_extras(nscale, bias, epi, Cout, "conv_fused");
   conv_impl(segs, seg_off, seg_C, w, bias, KH, KW, Cout, epi, scale, hd, out, ooff, out2, o2off, out3, o3off,
             aux1, a1off, aux2, a2off, tile, nx);
 }
@@ -339,8 +320,7 @@ void conv_fused(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::In
 void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntArrayRef seg_C, const Tensor& w,
               const c10::optional<Tensor>& bias, int64_t KH, int64_t KW, int64_t PH, int64_t PW, int64_t SY,
               int64_t SX, int64_t Ho, int64_t Wo, int64_t Cout, const Tensor& out, int64_t ooff, int64_t OSY,
-              int64_t OSX, int64_t OOY, int64_t OOX, int64_t tile, const c10::optional<Tensor>& stats,
-              bool stats_per_sample, const c10::optional<Tensor>& nscale, bool relu) {
+              int64_t OSX, int64_t OOY, int64_t OOX, int64_t tile, const c10::optional<Tensor>& nscale, bool relu) {
   TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size(),
               "conv_geo: 1..3 input segments");
   TORCH_CHECK(tile == 2 || tile == 3 || tile == 4 || tile == 6 || tile == 7 || tile == 8,
@@ -393,10 +373,10 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   L.Cout = Cout; L.Cout_pad = w.size(0); L.Ktot = w.size(2);
   L.f32 = f32 ? 1 : 0;
   const int epi = nscale ? EPI_NORM : 0;
-  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, B, Cout, "conv_geo");
+  const NormX nx = norm_extras(nscale, bias, epi, Cout, "conv_geo");
   TORCH_CHECK(!relu || nscale, "conv_geo: relu goes with the EPI_NORM epilogue");
   L.epi = epi; L.scale = 1.f; L.hd = relu ? 1 : 0;
-  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps;
+  L.chs = nx.chs;
   L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = ooff;
   L.tile = tile;
   L.geo = 1;
@@ -759,7 +739,7 @@ int num_cus(int dev) {
 // x NHWC (cin of its x.size(3) channels), w packed [Cout_pad][9][Ktot], y NHWC
 // (cout of its y.size(3) channels), no bias.
 void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin, int64_t cout,
-                  const c10::optional<Tensor>& stats, bool stats_per_sample, const c10::optional<Tensor>& nscale,
+                  const c10::optional<Tensor>& nscale,
                   const c10::optional<Tensor>& nshift, const c10::optional<Tensor>& res, bool relu,
                   bool accumulate) {
   TORCH_CHECK(x.dim() == 4, "conv3x3_halo: x must be NHWC");
@@ -776,8 +756,8 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
               "conv3x3_halo: alignment");
   TORCH_CHECK(x.numel() < (int64_t(1) << 31) && y.numel() < (int64_t(1) << 31), "conv3x3_halo: tensor too large");
   rs::EncEpi e;
-  const NormX nx = norm_extras(stats, stats_per_sample, nscale, nshift, nscale ? EPI_NORM : 0, B, cout, "conv3x3_halo");
-  e.stats = nx.stats; e.stats_ps = nx.stats_ps; e.chs = nx.chs;
+  const NormX nx = norm_extras(nscale, nshift, nscale ? EPI_NORM : 0, cout, "conv3x3_halo");
+  e.chs = nx.chs;
   e.shift = nscale ? nshift->data_ptr<float>() : nullptr;
   TORCH_CHECK(!relu || nscale, "conv3x3_halo: relu goes with nscale / nshift");
   TORCH_CHECK(!res || nscale, "conv3x3_halo: the residual goes with nscale / nshift");
@@ -790,7 +770,7 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
     e.rstr = res->size(3);
   }
   if (accumulate) {  // y += conv(x): the epilogue reads y as a plain (no ReLU) residual
-    TORCH_CHECK(!res && !nscale && !stats, "conv3x3_halo: accumulate excludes res / nscale / stats");
+    TORCH_CHECK(!res && !nscale, "conv3x3_halo: accumulate excludes res / nscale");
     e.res = static_cast<const uint16_t*>(y.data_ptr());
     e.rstr = y.size(3);
     e.res_relu = 0;
@@ -805,11 +785,10 @@ void conv3x3_halo(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cin
 // 7x7 / stride-2 / pad-3 stem conv, 3 -> Cout <= 64 (csrc/stem.hip).
 //   x: NHWC image [B, Hi, Wi, 3] fp32 or bf16; w: packed [64][7][32] bf16 (k = kx*3 + ci;
 //   fp32 output: the split [64][7][64] layout); out: NHWC [B, Ho, Wo, >= Cout] (bf16, or
-//   fp32 -> the split-bf16 MFMA path); epi 0 (+ bias, + stats) or EPI_NORM (nscale with
+//   fp32 -> the split-bf16 MFMA path); epi 0 (+ bias) or EPI_NORM (nscale with
 //   bias = shift, relu).
 void stem_conv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const Tensor& out, int64_t Cout,
-               int64_t epi, const c10::optional<Tensor>& stats, bool stats_per_sample,
-               const c10::optional<Tensor>& nscale, bool relu) {
+               int64_t epi, const c10::optional<Tensor>& nscale, bool relu) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(3) == 3 &&
                   (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "stem_conv: x must be a contiguous NHWC [B,H,W,3] fp32 / bf16 image");
@@ -826,7 +805,7 @@ void stem_conv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bi
   if (bias)
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
                     bias->numel() >= Cout, "stem_conv: bias fp32 (Cout,)");
-  const NormX nx = norm_extras(stats, stats_per_sample, nscale, bias, epi, B, Cout, "stem_conv");
+  const NormX nx = norm_extras(nscale, bias, epi, Cout, "stem_conv");
   TORCH_CHECK(!relu || epi == EPI_NORM, "stem_conv: relu goes with EPI_NORM");
   TORCH_CHECK((uintptr_t)out.data_ptr() % 16 == 0, "stem_conv: out alignment");
   TORCH_CHECK(out.numel() < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 31), "stem_conv: size");
@@ -836,7 +815,7 @@ void stem_conv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bi
   L.w = w.data_ptr(); L.bias = bias ? bias->data_ptr<float>() : nullptr;
   L.Cout = Cout; L.epi = epi; L.relu = relu ? 1 : 0;
   L.out = out.data_ptr(); L.ostr = out.size(3); L.ooff = 0;
-  L.chs = nx.chs; L.stats = nx.stats; L.stats_ps = nx.stats_ps; L.f32 = f32 ? 1 : 0;
+  L.chs = nx.chs; L.f32 = f32 ? 1 : 0;
   const c10::DeviceGuard guard(x.device());
   rs::stem_launch(L, stream());
   RS_CHECK_LAUNCH();
@@ -869,11 +848,11 @@ void stem_wgrad(const Tensor& x, const Tensor& dy, int64_t Cout, const Tensor& d
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
-  m.def("stem_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) out, int Cout, int epi, Tensor(b!)? stats=None, "
-        "bool stats_per_sample=False, Tensor? nscale=None, bool relu=False) -> ()");
+  m.def("stem_conv(Tensor x, Tensor w, Tensor? bias, Tensor(a!) out, int Cout, int epi, Tensor? nscale=None, "
+        "bool relu=False) -> ()");
   m.def("stem_wgrad(Tensor x, Tensor dy, int Cout, Tensor(a!) dw) -> ()");
-  m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout, Tensor(b!)? stats=None, "
-        "bool stats_per_sample=False, Tensor? nscale=None, Tensor? nshift=None, Tensor? res=None, "
+  m.def("conv3x3_halo(Tensor x, Tensor w, Tensor(a!) y, int cin, int cout, "
+        "Tensor? nscale=None, Tensor? nshift=None, Tensor? res=None, "
         "bool relu=False, bool accumulate=False) -> ()");
   m.def("conv_wgrad(Tensor dy, int yoff, int Cout, Tensor[] segs, int[] seg_off, int[] seg_C, int[] seg_period, "
         "int KH, int KW, Tensor(a!) dw, Tensor(b!)? db=None, int bn128=0) -> ()");
@@ -888,14 +867,13 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("conv_fused(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, "
         "int Cout, int epi, float scale, int hd, Tensor(a!) out, int ooff, Tensor(b!)? out2, int o2off, "
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
-        "Tensor(d!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None) -> ()");
+        "Tensor? nscale=None) -> ()");
   m.def("enc_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("sconv(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool relu, Tensor(a!) out, int yoff, "
         "Tensor? res) -> ()");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
         "int PW, int SY, int SX, int Ho, int Wo, int Cout, Tensor(a!) out, int ooff, int OSY, int OSX, int OOY, "
-        "int OOX, int tile, Tensor(b!)? stats=None, bool stats_per_sample=False, Tensor? nscale=None, "
-        "bool relu=False) -> ()");
+        "int OOX, int tile, Tensor? nscale=None, bool relu=False) -> ()");
   m.def("flow_encode(Tensor coords, Tensor w, Tensor bias, Tensor(a!) out, int ooff, Tensor(b!)? fout, "
         "int foff) -> ()");
 }

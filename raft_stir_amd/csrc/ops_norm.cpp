@@ -17,7 +17,6 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
                      void* dres, hipStream_t s);
-void norm_sums_finalize_launch(float* sums, int GC, float inv_n, float eps, float* mean, float* rstd, hipStream_t s);
 void bn_running_launch(const float* mean, const float* rstd, const float* bias, int C, float eps, float mom,
                        float unb, float* rmean, float* rvar, long long* nbt, hipStream_t s);
 }  // namespace rs
@@ -123,24 +122,6 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
   return {dx, dres, s1, s2, s12};
 }
 
-// Statistics a conv epilogue accumulated into sums ([G][C][2] fp32: sum,
-// sum of squares over n values per group) -> (mean, rstd) [G][C]; sums is
-// zeroed again (ready for the conv's next accumulation).
-std::vector<Tensor> norm_finalize(const Tensor& sums, int64_t n, double eps) {
-  TORCH_CHECK(sums.is_cuda() && sums.is_contiguous() && sums.scalar_type() == at::kFloat && sums.dim() == 3 &&
-                  sums.size(2) == 2,
-              "norm_finalize: sums must be contiguous fp32 [G][C][2]");
-  TORCH_CHECK(n > 0, "norm_finalize: n");
-  const c10::DeviceGuard g(sums.device());
-  const int G = sums.size(0), C = sums.size(1);
-  auto fo = sums.options();
-  Tensor mean = at::empty({G, C}, fo), rstd = at::empty({G, C}, fo);
-  rs::norm_sums_finalize_launch(sums.data_ptr<float>(), G * C, (float)(1.0 / (double)n), (float)eps,
-                                mean.data_ptr<float>(), rstd.data_ptr<float>(), stream());
-  RS_CHECK_LAUNCH();
-  return {mean, rstd};
-}
-
 }  // namespace
 
 // In-place BatchNorm running-statistics update (see bn_running_kernel).
@@ -165,14 +146,12 @@ void bn_running_update(const Tensor& mean, const Tensor& rstd, const c10::option
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("bn_running_update(Tensor mean, Tensor rstd, Tensor? bias, Tensor(a!) running_mean, Tensor(b!) running_var, Tensor(c!)? nbt, float eps, float momentum, int n) -> ()");
   m.def("norm_stats(Tensor x, bool per_sample, float eps) -> Tensor[]");
-  m.def("norm_finalize(Tensor(a!) sums, int n, float eps) -> Tensor[]");
   m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu) -> Tensor");
   m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, bool batch_stats) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("norm_stats", &norm_stats);
-  m.impl("norm_finalize", &norm_finalize);
   m.impl("bn_running_update", &bn_running_update);
   m.impl("norm_act", &norm_act);
   m.impl("norm_act_backward", &norm_act_backward);

@@ -267,8 +267,7 @@ struct StemLaunch {
   const void* res;
   int rstr;
   const float* chs;
-  float* stats;
-  int stats_ps, f32;
+  int f32;
 };
 
 void stem_launch(const StemLaunch& L, hipStream_t stream) {
@@ -280,7 +279,7 @@ void stem_launch(const StemLaunch& L, hipStream_t stream) {
   a.epi = L.epi; a.hd = L.relu; a.scale = 1.f;
   a.out = L.out; a.ostr = L.ostr; a.ooff = L.ooff;
   a.aux1 = static_cast<const bf16_t*>(L.res); a.a1str = L.rstr; a.a1off = 0;
-  a.chs = L.chs; a.stats = L.stats; a.stats_ps = L.stats_ps; a.f32 = L.f32;
+  a.chs = L.chs; a.f32 = L.f32;
   stem::SArgs s{L.x, L.x_bf16, L.B, L.Hi, L.Wi, L.Ho, L.Wo};
   const dim3 grid((unsigned)(L.B * L.Ho * cdiv(L.Wo, stem::PXB)));
   if (L.f32)

@@ -164,19 +164,17 @@ def tuned_tiles_f32() -> dict:
 
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=None, stats=None, stats_per_sample=False, nscale=None):
+               aux2=None, a2off=0, tile=None, nscale=None):
     """segs: list of (NHWC bf16 buffer, channel offset, channels read).
-    ``stats`` (fp32 [G][cout][2]): the epilogue adds each channel's (sum, sum of
-    squares) of the output (ops/norm.py); ``nscale`` with ``epi=EPI_NORM``:
-    out = [relu if hd](acc * nscale + bias) [then relu(. + aux1)]."""
+    ``nscale`` with ``epi=EPI_NORM``: out = [relu if hd](acc * nscale + bias)
+    [then relu(. + aux1)]."""
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
     if _RECORD is not None:
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
-                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, stats=stats,
-                            stats_per_sample=stats_per_sample, nscale=nscale))
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, nscale=nscale))
     if tile is None:
         t0 = tensors[0]
         key = tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi)
@@ -187,10 +185,10 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
             tile = tuned_tiles().get(key)
             if tile is None:
                 tile = choose_tile(P, cout, chans, kh * kw)
-    if stats is None and nscale is None:
+    if nscale is None:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)
     else:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile,
-                                       stats, bool(stats_per_sample), nscale)
+                                       nscale)

@@ -46,34 +46,27 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
 
 _WGRAD_DMA = os.environ.get("RS_WGRAD_DMA", "1") != "0"
 _HALO = os.environ.get("RS_ENC_HALO", "1") != "0"
-_HALO128 = os.environ.get("RS_ENC_HALO128", "0") == "1"  # layer3 (128 ch): opt-in, measured slower (profiles/r2/enc_halo_bench.txt)
 
 
 def _halo_ok(cin: int, cout: int) -> bool:
     """csrc/enc_halo.hip (halo tiles, weights resident in LDS) has
-    this conv: 64 input channels with a multiple of 64 outputs, or 96 / 128
-    inputs with a multiple of 32 (the encoders' layer1 / 2 / 3 3x3 convs)."""
+    this conv: 64 input channels with a multiple of 64 outputs, or 96 inputs
+    with a multiple of 32 (the encoders' layer1 / layer2 3x3 convs; layer3's
+    128-channel convs measured faster on the implicit-GEMM tiles,
+    profiles/r2/enc_halo_bench.txt, and the 128-channel halo variant was
+    removed)."""
     if not _HALO:
         return False
     if cin == 64:
         return cout % 64 == 0
-    if cin == 128 and not _HALO128:
-        return False
-    return cin in (96, 128) and cout % 32 == 0
+    return cin == 96 and cout % 32 == 0
 
 
-def _conv3x3_into(xn, wp, cin, cout, out, P, stats=None):
-    """``stats`` = (fp32 [G][cout][2] buffer, per_sample) or None: the conv
-    epilogue adds the output's per-channel sums (ops/norm.py)."""
-    st, ps = stats if stats is not None else (None, False)
+def _conv3x3_into(xn, wp, cin, cout, out, P):
     if _halo_ok(cin, cout):
-        if st is None:
-            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout)
-        else:
-            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout, st, ps)
+        torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout)
     else:
-        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout),
-                   stats=st, stats_per_sample=ps)
+        conv_fused([(xn, 0, cin)], wp, None, 3, 3, cout, EPI_BIAS, out, 0, tile=choose_enc_tile(P, cin, cout))
 
 
 def _wgrad_covers(cin: int, cout: int) -> bool:
@@ -193,7 +186,7 @@ class GradSink:
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, hold, wstream, stats, sink=None):
+    def forward(ctx, x, weight, hold, wstream, sink=None):
         weight = hold.p
         ctx.param, ctx.wstream = weight, wstream
         xn = _nhwc(x)
@@ -202,7 +195,7 @@ class _Conv3x3(torch.autograd.Function):
         P = N * H * W
         wp = _packed(weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
-        _conv3x3_into(xn, wp, cin, cout, out, P, stats)
+        _conv3x3_into(xn, wp, cin, cout, out, P)
         ctx.save_for_backward(x)
         ctx.sink = sink if sink is not None and _halo_ok(cout, cin) else None
         if ctx.sink is not None:
@@ -232,7 +225,7 @@ class _Conv3x3(torch.autograd.Function):
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None
 
 
 # csrc/enc_wgrad.hip: all nine taps of a 64 x 64 channel slice per block over
@@ -267,18 +260,17 @@ def _wgrad3x3(dyn, x, xn, weight, cin, cout, P):
         [0, 0], 1, [False, True, False])[1].to(weight.dtype)
 
 
-def conv3x3(conv: nn.Conv2d, x: torch.Tensor, stats=None, sink=None) -> torch.Tensor:
-    """conv(x) without its bias (see :func:`eligible`); ``stats``: see
-    :func:`_conv3x3_into`; ``sink``: a :class:`GradSink` whose skip gradient
-    the input gradient absorbs."""
+def conv3x3(conv: nn.Conv2d, x: torch.Tensor, sink=None) -> torch.Tensor:
+    """conv(x) without its bias (see :func:`eligible`); ``sink``: a
+    :class:`GradSink` whose skip gradient the input gradient absorbs."""
     w, st = _weight_in(conv.weight)
-    return _Conv3x3.apply(x, w, _Hold(conv.weight), st, stats, sink)
+    return _Conv3x3.apply(x, w, _Hold(conv.weight), st, sink)
 
 
 # ------------------------------------------------------------------- 7x7 stem
 # The encoders' 7x7 / stride-2 stem (3 -> 64 / 32 channels) on csrc/stem.hip:
 # forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
-# conv epilogues (normalisation statistics, eval-BN scale / shift + ReLU) and a
+# conv epilogues (bias, eval-BN scale / shift + ReLU) and a
 # deterministic MFMA weight gradient; the image needs no input gradient.
 # RS_STEM: "auto" (default) runs the HIP stem for fp32 inference and for
 # full RAFT's bf16 inference (64 channels: 285.6 vs 283.3 FPS paired, the
@@ -336,11 +328,10 @@ def _stem_out(conv, x):
 
 class _Stem(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, hold, wstream, stats):
+    def forward(ctx, x, weight, hold, wstream):
         conv = hold.p
         out, wp = _stem_out(conv, x)
-        st, ps = stats if stats is not None else (None, False)
-        torch.ops.raft_stir.stem_conv(_nhwc(x), wp, None, out, conv.out_channels, 0, st, ps)
+        torch.ops.raft_stir.stem_conv(_nhwc(x), wp, None, out, conv.out_channels, 0)
         ctx.save_for_backward(x)
         ctx.param, ctx.wstream = conv.weight, wstream
         return out.permute(0, 3, 1, 2)
@@ -358,22 +349,20 @@ class _Stem(torch.autograd.Function):
                 torch.ops.raft_stir.stem_wgrad(_nhwc(x), dyn, weight.shape[0], g)
                 return (g.to(weight.dtype),)
             dw, = _wgrad_on(ctx.wstream, wgrad, [dyn, x])
-        return None, dw, None, None, None
+        return None, dw, None, None
 
 
-def stem(conv: nn.Conv2d, x: torch.Tensor, stats=None) -> torch.Tensor:
-    """conv(x) without its bias (:func:`stem_eligible`); ``stats``: see
-    :func:`_conv3x3_into`."""
+def stem(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """conv(x) without its bias (:func:`stem_eligible`)."""
     w, st = _weight_in(conv.weight)
-    return _Stem.apply(x, w, _Hold(conv), st, stats)
+    return _Stem.apply(x, w, _Hold(conv), st)
 
 
 @torch.no_grad()
 def stem_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool) -> torch.Tensor:
     """Inference: ``[relu](conv_nobias(x) * scale + shift)`` (eval BatchNorm in the epilogue)."""
     out, wp = _stem_out(conv, x)
-    torch.ops.raft_stir.stem_conv(_nhwc(x), wp, shift, out, conv.out_channels, EPI_NORM, None, False, scale,
-                                  bool(relu))
+    torch.ops.raft_stir.stem_conv(_nhwc(x), wp, shift, out, conv.out_channels, EPI_NORM, scale, bool(relu))
     return out.permute(0, 3, 1, 2)
 
 
@@ -415,32 +404,30 @@ def eligible_f32(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:
 
 
 @torch.no_grad()
-def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None, scale=None, shift=None,
+def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, scale=None, shift=None,
              relu: bool = False, residual=None) -> torch.Tensor:
-    """fp32 ``conv(x)`` (:func:`eligible_f32`) with the optional epilogue extras:
-    ``stats`` (see :func:`_conv3x3_into`) or eval-BN ``scale`` / ``shift``
-    (+ ReLU, + residual; the conv bias must already be folded into shift)."""
+    """fp32 ``conv(x)`` (:func:`eligible_f32`) with the optional eval-BN
+    ``scale`` / ``shift`` epilogue (+ ReLU, + residual; the conv bias must
+    already be folded into shift)."""
     xn = _nhwc(x)
     N, H, W, cin = xn.shape
     cout = conv.out_channels
     kh, kw = conv.kernel_size
     pad, stride = conv.padding, conv.stride
     wp = _split_weight(conv.weight)
-    st, ps = stats if stats is not None else (None, False)
     norm = scale is not None
     b = shift if norm else (conv.bias.detach().float().contiguous() if (bias and conv.bias is not None) else None)
     if stride == (1, 1) and (kh, kw) == (3, 3):
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.float32)
         rn = _nhwc(residual) if residual is not None else None
         conv_fused([(xn, 0, cin)], wp, b, 3, 3, cout, EPI_NORM if norm else EPI_BIAS, out, 0,
-                   hd=int(bool(relu)), aux1=rn, tile=None, stats=st,
-                   stats_per_sample=ps, nscale=scale)
+                   hd=int(bool(relu)), aux1=rn, tile=None, nscale=scale)
         return out.permute(0, 3, 1, 2)
     Ho = (H + 2 * pad[0] - kh) // stride[0] + 1
     Wo = (W + 2 * pad[1] - kw) // stride[1] + 1
     out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.float32)
     torch.ops.raft_stir.conv_geo([xn], [0], [cin], wp, b, kh, kw, pad[0], pad[1], stride[0], stride[1], Ho, Wo,
-                                 cout, out, 0, 1, 1, 0, 0, choose_tile_f32(N * Ho * Wo, cout, geo=True), st, bool(ps), scale,
+                                 cout, out, 0, 1, 1, 0, 0, choose_tile_f32(N * Ho * Wo, cout, geo=True), scale,
                                  bool(relu))
     return out.permute(0, 3, 1, 2)
 
@@ -578,7 +565,7 @@ def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residu
         wp = _packed(conv.weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
         if _halo_ok(cin, cout):
-            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout, None, False, scale, shift, rn, bool(relu))
+            torch.ops.raft_stir.conv3x3_halo(xn, wp, out, cin, cout, scale, shift, rn, bool(relu))
         else:
             conv_fused([(xn, 0, cin)], wp, shift, 3, 3, cout, EPI_NORM, out, 0, hd=int(bool(relu)), aux1=rn,
                        tile=choose_enc_tile(N * H * W, cin, cout), nscale=scale)
@@ -683,7 +670,7 @@ def _geo_tile(cout: int, chans) -> int:
     return 6 if k64 else 3
 
 
-def _conv_geo_fwd(x, weight, bias, stride, pad, stats=None):
+def _conv_geo_fwd(x, weight, bias, stride, pad):
     xn = _nhwc(x)
     N, Hi, Wi, cin = xn.shape
     cout, _, kh, kw = weight.shape
@@ -691,12 +678,8 @@ def _conv_geo_fwd(x, weight, bias, stride, pad, stats=None):
     Wo = (Wi + 2 * pad[1] - kw) // stride[1] + 1
     out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.bfloat16)
     b = None if bias is None else bias.detach().float().contiguous()
-    args = ([xn], [0], [cin], _fwd_weight(weight), b, kh, kw, pad[0], pad[1], stride[0], stride[1], Ho, Wo, cout,
-            out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]))
-    if stats is None:
-        torch.ops.raft_stir.conv_geo(*args)
-    else:
-        torch.ops.raft_stir.conv_geo(*args, stats[0], stats[1])
+    torch.ops.raft_stir.conv_geo([xn], [0], [cin], _fwd_weight(weight), b, kh, kw, pad[0], pad[1], stride[0],
+                                 stride[1], Ho, Wo, cout, out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]))
     return out
 
 
@@ -756,9 +739,9 @@ def _conv_geo_wgrad(dy, x, weight, stride, want_bias):
 
 class _ConvGeo(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, hold, wstream, stats):
+    def forward(ctx, x, weight, bias, stride, pad, hold, wstream):
         weight = hold.p
-        out = _conv_geo_fwd(x, weight, bias, stride, pad, stats)
+        out = _conv_geo_fwd(x, weight, bias, stride, pad)
         ctx.save_for_backward(x)
         ctx.param, ctx.wstream = weight, wstream
         ctx.stride, ctx.pad, ctx.has_bias = stride, pad, bias is not None
@@ -775,18 +758,17 @@ class _ConvGeo(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             want_b = ctx.has_bias and ctx.needs_input_grad[2]
             dw, db = _wgrad_on(ctx.wstream, lambda: _conv_geo_wgrad(dyn, x, weight, ctx.stride, want_b), [dyn, x])
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, stats=None) -> torch.Tensor:
+def conv_geo(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
     """conv(x) on the HIP kernels (see :func:`eligible_geo`); ``bias=False``
-    drops the conv's bias (folded into a following normalisation); ``stats``:
-    see :func:`_conv3x3_into`."""
+    drops the conv's bias (folded into a following normalisation)."""
     b = conv.bias if bias else None
     w, st = _weight_in(conv.weight)
     if b is not None and st is not None:
         b = _DEFER["views"].get(id(conv.bias), b)
-    return _ConvGeo.apply(x, w, b, tuple(conv.stride), tuple(conv.padding), _Hold(conv.weight), st, stats)
+    return _ConvGeo.apply(x, w, b, tuple(conv.stride), tuple(conv.padding), _Hold(conv.weight), st)
 
 
 class _ConvPair(torch.autograd.Function):
@@ -795,11 +777,10 @@ class _ConvPair(torch.autograd.Function):
     gradient, with the shortcut's term fused into the 3x3's (0, 0) phase."""
 
     @staticmethod
-    def forward(ctx, x, w1, wd, stride, holds, wstream, stats):
+    def forward(ctx, x, w1, wd, stride, holds, wstream):
         w1, wd = holds.p
-        s1, sd = stats if stats is not None else (None, None)
-        y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1), s1)
-        yd = _conv_geo_fwd(x, wd, None, stride, (0, 0), sd)
+        y1 = _conv_geo_fwd(x, w1, None, stride, (1, 1))
+        yd = _conv_geo_fwd(x, wd, None, stride, (0, 0))
         ctx.save_for_backward(x)
         ctx.params, ctx.wstream = (w1, wd), wstream
         ctx.stride = stride
@@ -820,7 +801,7 @@ class _ConvPair(torch.autograd.Function):
             dw1, dwd = _wgrad_on(ctx.wstream, lambda: (_conv_geo_wgrad(d1, x, w1, s, False)[0] if n1 else None,
                                                        _conv_geo_wgrad(dd, x, wd, s, False)[0] if n2 else None),
                                  [d1, dd, x])
-        return dx, dw1, dwd, None, None, None, None
+        return dx, dw1, dwd, None, None, None
 
 
 def _pair_dgrad(d1, dd, w1, wd, x_shape, stride):
@@ -869,12 +850,11 @@ def pair_eligible(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor) -> bool:
             and down.kernel_size == (1, 1) and down.stride == (2, 2) and down.out_channels == conv1.out_channels)
 
 
-def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor, stats=None):
-    """(conv1(x), down(x)) without biases (both folded into their norms);
-    ``stats`` = (conv1's, down's) statistics requests (:func:`_conv3x3_into`)."""
+def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor):
+    """(conv1(x), down(x)) without biases (both folded into their norms)."""
     w1, st = _weight_in(conv1.weight)
     wd, _ = _weight_in(down.weight)
-    return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st, stats)
+    return _ConvPair.apply(x, w1, wd, tuple(conv1.stride), _Hold((conv1.weight, down.weight)), st)
 
 
 # ------------------------------------------------------- narrow-channel convs

@@ -102,49 +102,6 @@ def _hip_ok(norm, x, residual):
     return False
 
 
-# ------------------------------------------------------------ fused statistics
-# Instance norm and train-mode batch norm need per-channel statistics of the
-# conv output.  Where the conv runs on the hand-written kernels its epilogue
-# accumulates (sum, sum of squares) per channel into a per-norm-module fp32
-# buffer (vector atomics), and one tiny launch turns them into mean / rstd
-# and zeroes the buffer again (torch.ops.raft_stir.norm_finalize): no
-# separate reduction pass over the activation.  The fp32 atomics make the
-# sums order-dependent, so deterministic mode keeps the two-level reduction.
-# Opt-in (RS_NORM_FUSED_STATS=1): measured SLOWER in situ -- the statistics
-# epilogue raises the halo / tile kernels' register use and contends on the
-# per-channel atomics (enc_halo 64->64: 115 -> 209 us per training call);
-# paired bench, round 3: 381 vs 368 pairs/s, 279 vs 269 FPS
-# (profiles/r3/README.md).  The two-level reduction is the default.
-_FUSED_STATS = os.environ.get("RS_NORM_FUSED_STATS", "0") == "1"
-
-
-def _deterministic() -> bool:
-    from ..runtime.determinism import is_deterministic
-    return is_deterministic()
-
-
-def _stats_request(norm: nn.Module, x: torch.Tensor, cout: int):
-    """(fp32 [G][cout][2] zeroed sums buffer, per_sample) for a fused-statistics
-    conv feeding ``norm``, or None (norm kind / mode without batch statistics,
-    deterministic mode, opt-out)."""
-    if not _FUSED_STATS:
-        return None
-    if isinstance(norm, nn.InstanceNorm2d):
-        per_sample = True
-    elif isinstance(norm, nn.BatchNorm2d) and norm.training:
-        per_sample = False
-    else:
-        return None
-    if _deterministic():
-        return None
-    G = x.shape[0] if per_sample else 1
-    buf = norm.__dict__.get("_rs_sums")
-    if buf is None or buf.shape != (G, cout, 2) or buf.device != x.device:
-        buf = torch.zeros(G, cout, 2, device=x.device, dtype=torch.float32)
-        norm.__dict__["_rs_sums"] = buf  # plain attribute: not a buffer, not in the state dict
-    return buf, per_sample
-
-
 def _cached(norm: nn.Module, name: str, srcs, compute):
     """Per-module cache of tensors derived from ``srcs`` (eval-mode BatchNorm
     constants).  Keyed on the weight generation and the sources' version
@@ -220,14 +177,11 @@ def _eval_fused_ok(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, residual) 
     return residual is None and enc_conv.eligible_geo(conv, x)
 
 
-def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None, stats=None,
-             res_sink=None):
+def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None, bias=None, res_sink=None):
     """``bias``: the producing convolution's bias, folded into the statistics
-    (see :func:`conv_norm_act`); None if already applied.  ``stats``: the
-    (sums buffer, per_sample) the producing conv filled (:func:`_stats_request`)."""
+    (see :func:`conv_norm_act`); None if already applied.  ``res_sink``: see
+    :func:`conv_norm_act`."""
     if not _hip_ok(norm, x, residual):
-        if stats is not None:  # the conv filled the sums: consume (zero) them for its next use
-            torch.ops.raft_stir.norm_finalize(stats[0], 1, 1e-5)
         if bias is not None:
             x = x + bias.to(x.dtype).view(1, -1, 1, 1)
         y = norm(x)
@@ -242,9 +196,6 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
 
     def batch_moments(per_sample):
         with torch.no_grad():  # the stats' gradient is part of _NormAct.backward
-            if stats is not None:
-                n = x.numel() // x.shape[1] // (x.shape[0] if per_sample else 1)
-                return torch.ops.raft_stir.norm_finalize(stats[0], n, norm.eps)
             return torch.ops.raft_stir.norm_stats(xn, per_sample, norm.eps)
     if isinstance(norm, nn.InstanceNorm2d):
         mean, rstd = batch_moments(True)
@@ -324,25 +275,19 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
                                              or norm.bias.requires_grad)):
             sc, sh = _eval_affine(norm, conv.bias)
             return enc_conv.stem_norm(conv, x, sc, sh, relu)
-        st = _stats_request(norm, x, conv.out_channels)
-        return norm_act(norm, enc_conv.stem(conv, x, st), relu, residual, bias=conv.bias, stats=st)
+        return norm_act(norm, enc_conv.stem(conv, x), relu, residual, bias=conv.bias)
     if enc_conv.eligible_f32_train(conv, x):  # fp32 training on the split-bf16 F32 tiles
         return norm_act(norm, enc_conv.conv_f32_train(conv, x, bias=False), relu, residual, bias=conv.bias)
     if _eval_fused_ok(conv, norm, x, residual):  # eval BatchNorm: everything in the conv epilogue
         sc, sh = _eval_affine(norm, conv.bias)
         return enc_conv.conv_norm(conv, x, sc, sh, relu, residual)
     if enc_conv.eligible_f32(conv, x):  # fp32 inference on the split-bf16 F32 tiles
-        st = _stats_request(norm, x, conv.out_channels)
-        return norm_act(norm, enc_conv.conv_f32(conv, x, bias=False, stats=st), relu, residual, bias=conv.bias,
-                        stats=st)
+        return norm_act(norm, enc_conv.conv_f32(conv, x, bias=False), relu, residual, bias=conv.bias)
     if enc_conv.eligible(conv, x):  # stride-1 3x3 on the hand-written implicit-GEMM kernels
-        st = _stats_request(norm, x, conv.out_channels)
-        return norm_act(norm, enc_conv.conv3x3(conv, x, st, sink=grad_sink), relu, residual, bias=conv.bias,
-                        stats=st, res_sink=res_sink)
+        return norm_act(norm, enc_conv.conv3x3(conv, x, sink=grad_sink), relu, residual, bias=conv.bias,
+                        res_sink=res_sink)
     if enc_conv.eligible_geo(conv, x):  # stride-2 3x3 / 1x1 (strided geometry of the same kernels)
-        st = _stats_request(norm, x, conv.out_channels)
-        return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False, stats=st), relu, residual, bias=conv.bias,
-                        stats=st)
+        return norm_act(norm, enc_conv.conv_geo(conv, x, bias=False), relu, residual, bias=conv.bias)
     y = fp32conv.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return norm_act(norm, y, relu, residual, bias=conv.bias)
 
@@ -363,9 +308,7 @@ def conv_pair_norm_act(conv1: nn.Conv2d, norm1: nn.Module, down: nn.Conv2d, norm
             scd, shd = _eval_affine(norm_d, down.bias)
             return (enc_conv.conv_norm(conv1, x, sc1, sh1, True),
                     enc_conv.conv_norm(down, x, scd, shd, False))
-        s1 = _stats_request(norm1, x, conv1.out_channels)
-        sd = _stats_request(norm_d, x, down.out_channels)
-        y1, yd = enc_conv.conv_pair(conv1, down, x, (s1, sd))
-        return (norm_act(norm1, y1, True, None, bias=conv1.bias, stats=s1),
-                norm_act(norm_d, yd, False, None, bias=down.bias, stats=sd))
+        y1, yd = enc_conv.conv_pair(conv1, down, x)
+        return (norm_act(norm1, y1, True, None, bias=conv1.bias),
+                norm_act(norm_d, yd, False, None, bias=down.bias))
     return conv_norm_act(conv1, norm1, x), conv_norm_act(down, norm_d, x, relu=False)

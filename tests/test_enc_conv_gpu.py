@@ -57,7 +57,7 @@ def test_ineligible_shapes(cuda):
     assert not enc_conv.eligible(nn.Conv2d(64, 24, 3, padding=1).to(cuda), x)
 
 
-@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (64, 128), (96, 32), (128, 128), (128, 96)])
+@pytest.mark.parametrize("cin,cout", [(64, 64), (96, 96), (64, 128), (96, 32)])
 @pytest.mark.parametrize("shape", [(2, 37, 45), (1, 8, 32), (3, 13, 70)])
 def test_conv3x3_halo_kernel(cuda, cin, cout, shape):
     """csrc/enc_halo.hip (persistent halo-tile 3x3 conv) vs the fp32 PyTorch conv:
