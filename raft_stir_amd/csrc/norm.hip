@@ -198,11 +198,27 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, i
   const int b0 = G == 1 ? 0 : g, nb = G == 1 ? B : 1;
   double t0 = 0.0, t1 = 0.0;
   if (c < C) {
-    for (int i = part; i < nb * S; i += 32) {
-      const int b = b0 + i / S, s = i % S;
-      const float* w = ws + (((size_t)b * S + s) * C + c) * 2;
-      t0 += w[0];
-      t1 += w[1];
+    // 4 independent partial loads in flight per thread: the chain of one
+    // dependent load per partial made this kernel latency-bound (8 us per
+    // batch-norm call at 512 partials); the summation order is unchanged
+    // within each thread's strided share, so the result stays deterministic
+    const int n = nb * S;
+    for (int i = part; i < n; i += 32 * 4) {
+      float2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = i + 32 * u;
+        v[u] = make_float2(0.f, 0.f);
+        if (k < n) {
+          const int b = b0 + k / S, s = k % S;
+          v[u] = *reinterpret_cast<const float2*>(ws + (((size_t)b * S + s) * C + c) * 2);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        t0 += v[u].x;
+        t1 += v[u].y;
+      }
     }
   }
   __shared__ double sm[2][256];
