@@ -531,8 +531,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 // and db[co] += sum_p dF[p][co].  K = 98 per output: a VALU kernel.
 // Block = ROWS image rows of one image; the flow rows they touch (ROWS + 6,
 // zero-padded by 3 columns) are staged in LDS; thread (co, ci) walks each
-// row with a 7-wide sliding window in registers (1 LDS read + 1 dF read per
-// 7 FMAs) and keeps 49 tap accumulators; one atomic per output per block.
+// row with a 7-wide sliding window in registers (7 LDS reads + 1 dF read per
+// 49 FMAs) and keeps 49 tap accumulators; one atomic per output per block.
 constexpr int FROWS = 8;
 template <typename T>  // dF: bf16, or fp32 (the fp32 training engine)
 __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict__ coords, int Bp, int H, int W,
@@ -561,27 +561,39 @@ __global__ __launch_bounds__(256) void flow_wgrad_kernel(const float* __restrict
     float bsum = 0.f;
     for (int r = 0; r < FROWS && y0 + r < H; ++r) {
       const T* grow = df + ((size_t)b * HW + (size_t)(y0 + r) * W) * fstr + co;
-      // x outer, taps inner: each dY value is loaded once and feeds 49 FMAs;
-      // the 7 padded flow rows slide through registers (win[ky][kx] = flow
-      // at (y0 + r + ky - 3, x + kx - 3))
+      // x outer, taps inner: each dY value is loaded once and feeds 49 FMAs.
+      // The 7 padded flow rows slide through a register ring: column c of the
+      // window lives in slot c % 7, and x advances in chunks of 7 (fully
+      // unrolled, so every slot index is a constant: no register shuffling,
+      // and the chunk's 7 dF loads are issued together)
       float win[7][7];
 #pragma unroll
       for (int ky = 0; ky < 7; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 6; ++kx) win[ky][kx] = F[(r + ky) * WP + kx];
-      for (int x = 0; x < W; ++x) {
-        const float g = io<T>::ld(grow + (size_t)x * fstr);
-        bsum += g;
+      int x = 0;
+      for (; x + 7 <= W; x += 7) {
+        float g[7];
 #pragma unroll
-        for (int ky = 0; ky < 7; ++ky) win[ky][6] = F[(r + ky) * WP + x + 6];
+        for (int u = 0; u < 7; ++u) g[u] = io<T>::ld(grow + (size_t)(x + u) * fstr);
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+          bsum += g[u];
+#pragma unroll
+          for (int ky = 0; ky < 7; ++ky) win[ky][(u + 6) % 7] = F[(r + ky) * WP + x + u + 6];
+#pragma unroll
+          for (int ky = 0; ky < 7; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 7; ++kx) acc[ky * 7 + kx] += g[u] * win[ky][(kx + u) % 7];
+        }
+      }
+      for (; x < W; ++x) {  // the last W % 7 columns: window straight from LDS
+        const float g1 = io<T>::ld(grow + (size_t)x * fstr);
+        bsum += g1;
 #pragma unroll
         for (int ky = 0; ky < 7; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 7; ++kx) acc[ky * 7 + kx] += g * win[ky][kx];
-#pragma unroll
-        for (int ky = 0; ky < 7; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 6; ++kx) win[ky][kx] = win[ky][kx + 1];
+          for (int kx = 0; kx < 7; ++kx) acc[ky * 7 + kx] += g1 * F[(r + ky) * WP + x + kx];
       }
     }
     if (part) {  // deterministic mode: this block's [98 * Cout | Cout] partial, reduced in order later
