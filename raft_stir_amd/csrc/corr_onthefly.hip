@@ -428,8 +428,8 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
                                                            float* __restrict__ df1, LvlMut df2) {
   constexpr int C = CQ * 32;
   __shared__ float Gs[16][MAXC];
-  __shared__ float f2s[MAXC][33];
-  __shared__ float f1s[16][C];
+  __shared__ __attribute__((aligned(16))) float f2s[MAXC][36];  // 16-B rows: one ds_read_b128 per 4 channels
+  __shared__ __attribute__((aligned(16))) float f1s[16][C];
   __shared__ int qX0[16], qY0[16], qn[16];
   __shared__ float qfx[16], qfy[16];
   const int t = threadIdx.x;
@@ -518,10 +518,7 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
           const int X = bx0 + cell % bw, Y = by0 + cell / bw;
           float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
           if (X >= 0 && X < W && Y >= 0 && Y < H) v = ld4<T>(f2b + ((size_t)Y * W + X) * C + 32 * k + 4 * pc);
-          f2s[cell][4 * pc + 0] = v.x;
-          f2s[cell][4 * pc + 1] = v.y;
-          f2s[cell][4 * pc + 2] = v.z;
-          f2s[cell][4 * pc + 3] = v.w;
+          *reinterpret_cast<float4*>(&f2s[cell][4 * pc]) = v;
         }
         __syncthreads();
         if (t < 128) {  // df1[q][32 k + 4 cg ..] += sum_cell G[q][cell] f2[cell][..]
@@ -529,10 +526,11 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
           float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
           for (int cell = 0; cell < nc; ++cell) {
             const float gv = Gs[dq][cell];
-            s0 += gv * f2s[cell][4 * cg + 0];
-            s1 += gv * f2s[cell][4 * cg + 1];
-            s2 += gv * f2s[cell][4 * cg + 2];
-            s3 += gv * f2s[cell][4 * cg + 3];
+            const float4 fv = *reinterpret_cast<const float4*>(&f2s[cell][4 * cg]);
+            s0 += gv * fv.x;
+            s1 += gv * fv.y;
+            s2 += gv * fv.z;
+            s3 += gv * fv.w;
           }
           a1[k][0] += s0;
           a1[k][1] += s1;
@@ -546,15 +544,14 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
             float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
             bool any = false;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
+            for (int q = 0; q < 16; ++q) {  // zero G entries (queries whose window misses the cell) add 0
               const float gv = Gs[q][cell];
-              if (gv != 0.f) {
-                any = true;
-                s0 += gv * f1s[q][32 * k + 4 * cg + 0];
-                s1 += gv * f1s[q][32 * k + 4 * cg + 1];
-                s2 += gv * f1s[q][32 * k + 4 * cg + 2];
-                s3 += gv * f1s[q][32 * k + 4 * cg + 3];
-              }
+              const float4 fv = *reinterpret_cast<const float4*>(&f1s[q][32 * k + 4 * cg]);
+              any = any || gv != 0.f;
+              s0 += gv * fv.x;
+              s1 += gv * fv.y;
+              s2 += gv * fv.z;
+              s3 += gv * fv.w;
             }
             if (!any) continue;
             const size_t off = ((size_t)b * H * W + (size_t)Y * W + X) * C + 32 * k + 4 * cg;
