@@ -275,10 +275,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(Args a, float* __restrict__ 
 //    the 32-B column block with (row & 3) instead, applied to the per-lane
 //    SOURCE chunk and to the tr16 read address.
 // The bias gradient of the first N tile is summed from the staged dY tile in
-// LDS.  NS = LDS stages: 2 keeps one K step in flight behind the one being
-// multiplied; 3 keeps two (the wait before each step then leaves the newest
-// step's DMA outstanding), for the LDS-fill-bound shapes.
-template <int BM, int BN, int WGM, int WGN, int NS = 2>
+// LDS.
+template <int BM, int BN, int WGM, int WGN>
 __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float* __restrict__ db) {
   constexpr int RA = BM * 2, RB_ = BN * 2;               // bytes per staged pixel row
   constexpr int CA = BM / 8, CB = BN / 8;                // 16-B chunks per row
@@ -286,11 +284,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
   constexpr int NA = BK * CA / NT, NB = BK * CB / NT;    // DMA instructions per thread
   constexpr int WM = BM / WGM / 16, WN = BN / WGN / 16;  // MFMA tiles per wave
   static_assert(NA * NT == BK * CA && NB * NT == BK * CB && NT % CA == 0, "tile / thread split");
-  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
   constexpr int kFar = 0x7ffffff0;
   constexpr int STAGE = BK * (RA + RB_);
-  static_assert(NS * STAGE <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NS * STAGE];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave % WGM, wn = wave / WGM;
   const int nkb = a.Ktot / BN;
@@ -396,14 +392,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void wgrad_dma_kernel(Args a, float
     baddr[nt] = lds0 + BK * RA + (8 * g + tq) * RB_ + ch * 16 + (tp & 1) * 8;
   }
   RS_WD_ISSUE(0, 0);
-  if (NS == 3 && nsteps > 1) RS_WD_ISSUE(1, 1);
   for (int s = 0; s < nsteps; ++s) {
-    const int buf = NS == 2 ? (s & 1) : s % 3;
-    if (NS == 3 && s + 1 < nsteps)  // tile s landed (tile s+1 may still be in flight); buffer s-1 free
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NA + NB) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (s + NS - 1 < nsteps) RS_WD_ISSUE(s + NS - 1, NS == 2 ? (buf ^ 1) : (s + 2) % 3);
+    const int buf = s & 1;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // tile s landed; buffer s-1 free
+    if (s + 1 < nsteps) RS_WD_ISSUE(s + 1, buf ^ 1);
     const uint32_t so = buf * STAGE;
     if (do_bias) {
       u32x4_t bv[BK * CA / NT];
@@ -649,19 +641,17 @@ struct WgradPlan {
 WgradPlan wgrad_plan(const WgradLaunch& L, bool det) {
   WgradPlan pl{};
   // tile variant (L.bn128): 0 = 128x64 (64x64 for Cout <= 64), 1 = 128x128,
-  // 8-wave DMA tiles: 2 = 128x128, 3 = 256x128, 4 = 256x64, 5 = 64x128 (4 waves);
-  // three-stage DMA twins: 6 = 128x64 (4 waves), 7 = 256x64, 8 = 128x128, 9 = 256x128
+  // 8-wave DMA tiles: 2 = 128x128, 3 = 256x128, 4 = 256x64, 5 = 64x128 (4 waves)
   bool seg128 = true;  // a 128-wide N tile must stay inside one segment
   for (int s = 0; s < L.nseg; ++s) seg128 = seg128 && (L.seg_C[s] % 128 == 0);
   int var = L.bn128;
-  if (var < 0 || var > 9 || (!L.dma && var > 1)) var = 0;
-  if ((var == 1 || var == 2 || var == 3 || var == 5 || var == 8 || var == 9) && !seg128) var = 0;
+  if (var < 0 || var > 5 || (!L.dma && var > 1)) var = 0;
+  if ((var == 1 || var == 2 || var == 3 || var == 5) && !seg128) var = 0;
   if (var == 1 && L.Cout <= 64) var = 0;
   pl.var = var;
-  pl.bm = (var == 3 || var == 4 || var == 7 || var == 9) ? 256
-          : (var == 5 ? 64 : (var == 0 && L.Cout <= 64 ? 64 : 128));
-  pl.bn = (var == 0 || var == 4 || var == 6 || var == 7) ? 64 : 128;
-  pl.nthr = (var >= 2 && var <= 4) || var >= 7 ? 512 : 256;
+  pl.bm = var == 3 || var == 4 ? 256 : (var == 5 ? 64 : (var == 0 && L.Cout <= 64 ? 64 : 128));
+  pl.bn = var == 0 || var == 4 ? 64 : 128;
+  pl.nthr = var >= 2 && var <= 4 ? 512 : 256;
   const int taps = L.KH * L.KW, P = L.Bp * L.H * L.W;
   pl.ntiles = taps * (L.Ktot / pl.bn);
   pl.mtiles = cdiv(L.Cout, pl.bm);
@@ -737,10 +727,6 @@ static void wgrad_kernels(const WgradLaunch& L, const wgrad::Args& a, int var, i
       case 3: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 128, 4, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
       case 4: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 64, 4, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
       case 5: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<64, 128, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db); break;
-      case 6: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 64, 2, 2, 3>), grid, dim3(nthr), 0, stream, a, L.db); break;
-      case 7: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 64, 4, 2, 3>), grid, dim3(nthr), 0, stream, a, L.db); break;
-      case 8: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 128, 2, 4, 3>), grid, dim3(nthr), 0, stream, a, L.db); break;
-      case 9: hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<256, 128, 4, 2, 3>), grid, dim3(nthr), 0, stream, a, L.db); break;
       default:
         if (bm == 128)
           hipLaunchKernelGGL((wgrad::wgrad_dma_kernel<128, 64, 2, 2>), grid, dim3(nthr), 0, stream, a, L.db);

@@ -487,7 +487,7 @@ void conv_wgrad_impl(const Tensor& dy, int64_t yoff, int64_t Cout, const std::ve
   const int bm = Cout > 64 ? 128 : 64;
   TORCH_CHECK(yoff >= 0 && yoff % 8 == 0 && yoff + (dma_env ? Cout : (Cout + bm - 1) / bm * bm) <= dy.size(3),
               "conv_wgrad: dy channel window out of bounds");
-  TORCH_CHECK(bn128 >= 0 && bn128 <= 9, "conv_wgrad: tile variant 0..9");
+  TORCH_CHECK(bn128 >= 0 && bn128 <= 5, "conv_wgrad: tile variant 0..5");
   if (db) TORCH_CHECK(db->is_cuda() && db->scalar_type() == at::kFloat && db->numel() >= Cout, "conv_wgrad: db fp32");
   TORCH_CHECK(!segs.empty() && segs.size() <= 3 && seg_off.size() == segs.size() && seg_C.size() == segs.size() &&
                   seg_period.size() == segs.size(),

@@ -57,7 +57,6 @@ instantiations.
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -446,20 +445,12 @@ def _split_bf16(t: torch.Tensor):
     return hi, (t - hi.float()).to(torch.bfloat16)
 
 
-# RS_WGRAD_NS3=1: the three-stage DMA twins of the weight-gradient tiles
-# (csrc/conv_wgrad.hip variants 6-9: two K steps in flight instead of one)
-_WGRAD_NS3 = os.environ.get("RS_WGRAD_NS3", "0") == "1"
-_NS3_TWIN = {0: 6, 4: 7, 2: 8, 3: 9}
-
-
 def _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128=0):
     """``pc.dw += dY^T X`` (+ ``pc.db += colsum dY``) over every iteration's
     pixels on csrc/conv_wgrad.hip.  fp32 engine: the bf16 GEMM on the split
     operands, dYh.Xh + dYl.Xh + dYh.Xl (the bias sums of the first two give
     colsum(dYh + dYl))."""
     per = [s[0].shape[0] * H * W for s in segs]
-    if _WGRAD_NS3:
-        bn128 = _NS3_TWIN.get(bn128, bn128)
     if not eng.f32:
         R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
                      per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
@@ -729,7 +720,7 @@ class FusedTrainLoop(torch.autograd.Function):
         for p in range(2):
             wg(eng.zr[p], S["d_zr"][p], 0, [(hins[p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)], 4)
             wg(eng.q[p], S["d_q"][p], 0, [(S["rh"][p], 0, HD), (inpb, 0, 128), (hxs, HD, 128)])
-        wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)])
+        wg(eng.cv, S["d_conv"], 0, [(S["mot"], 0, 256)], 2)  # 8-wave 128x128: 238 vs 258 us (profiles/r4/wgrad_bench_s21.log)
         wg(eng.c2, S["d_c2f2"], 0, [(S["c1"], 0, 256)], 4)
         wg(eng.f2, S["d_c2f2"], 192, [(S["f1"], 0, 128)])
         wg(eng.c1, S["d_c1"], 0, [(S["corr"], 0, CORR_PAD)])

@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of one hipGraph")
-    ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9],
+    ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5],
                     help="wgrad tile variants (csrc/conv_wgrad.hip wgrad_launch)")
     a = ap.parse_args()
     global GRAPH

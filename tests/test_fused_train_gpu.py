@@ -46,11 +46,10 @@ def test_wgrad_batched_with_broadcast_segment(cuda, k):
     torch.testing.assert_close(dw3[:cout], want, atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("var", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("cout,k", [(70, (3, 3)), (200, (1, 5)), (320, (1, 1))])
 def test_wgrad_tile_variants(cuda, var, cout, k):
-    """Every wgrad tile variant (4- and 8-wave DMA tiles, 64..256 x 64..128,
-    two- and three-stage LDS rings)
+    """Every wgrad tile variant (4- and 8-wave DMA tiles, 64..256 x 64..128)
     vs fp32 PyTorch, ragged Cout against the M tile, multi-segment input,
     ragged pixel count against the 64-pixel K step, fused bias gradient."""
     torch.manual_seed(var)
