@@ -578,7 +578,7 @@ def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residu
     out = torch.empty(N, Ho, Wo, cout, device=x.device, dtype=torch.bfloat16)
     torch.ops.raft_stir.conv_geo([xn], [0], [cin], _fwd_weight(conv.weight), shift, kh, kw, pad[0], pad[1],
                                  stride[0], stride[1], Ho, Wo, cout, out, 0, 1, 1, 0, 0, _geo_tile(cout, [cin]),
-                                 None, False, scale, bool(relu))
+                                 scale, bool(relu))
     return out.permute(0, 3, 1, 2)
 
 
