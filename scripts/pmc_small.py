@@ -15,12 +15,12 @@ def main():
     dev = torch.device("cuda", 0)
     which = sys.argv[1]
     B, H, W, IT = 8, 46, 62, 12
-    if which == "wgrad":
-        hs = torch.relu(torch.randn(IT * B, H, W, 512, device=dev)).to(torch.bfloat16)
-        dfs = torch.randn(IT * B, 2, H, W, device=dev)
-        dw = torch.zeros(128, 9, 256, device=dev)
-        db = torch.zeros(2, device=dev)
-        fn = lambda: R.flow_head_wgrad(dfs, hs, 0, dw, db)
+    if which == "wgrad":  # convf1 weight gradient over all iterations (csrc/conv_wgrad.hip flow_wgrad_kernel)
+        crd = torch.randn(IT * B, 2, H, W, device=dev) * 4
+        dfs = torch.randn(IT * B, H, W, 128, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(49, 2, 128, device=dev)
+        db = torch.zeros(128, device=dev)
+        fn = lambda: R.flow_wgrad(crd, dfs, dw, db)
     elif which in ("fwd", "dgrad"):
         head = torch.relu(torch.randn(B, H, W, 512, device=dev)).to(torch.bfloat16)
         w2 = torch.randn(2, 3, 3, 256, device=dev)
