@@ -16,6 +16,8 @@ import os
 import torch
 import torch.optim as optim
 
+from ..runtime import weights
+
 _FUSED_ADAMW = os.environ.get("RS_FUSED_ADAMW", "1") != "0"
 
 
@@ -87,9 +89,16 @@ class FusedClipAdamW(optim.Optimizer):
         lr = g["lr"]
         lr_t = lr if isinstance(lr, torch.Tensor) else None
         b1, b2 = g["betas"]
-        return torch.ops.raft_stir.clip_adamw_(params, grads, self._m, self._v, self._partial, moff, lr_t,
+        norm = torch.ops.raft_stir.clip_adamw_(params, grads, self._m, self._v, self._partial, moff, lr_t,
                                                0.0 if lr_t is not None else float(lr), b1, b2, g["eps"],
                                                g["weight_decay"], float(max_norm), self._state)
+        # the parameters changed behind autograd's back (a custom mutable op
+        # bumps no _version) and clip_and_step bypasses the wrapped step() whose
+        # global post-hook advances the weight generation: advance it here, or
+        # every packed-weight cache (ops/wpack.py, the fused engines) would keep
+        # serving the previous weights to the HIP kernels
+        weights.bump()
+        return norm
 
     def clip_and_step(self, max_norm: float):
         return self._run(max_norm)

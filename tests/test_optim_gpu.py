@@ -121,3 +121,39 @@ def test_fetch_optimizer_uses_fused_clip_adamw(cuda):
     sched.step()
     assert not torch.equal(w0, m[0].weight.detach())
     assert opt.param_groups[0]["lr"] != 4e-4 / 25  # OneCycle moved the lr
+
+
+def test_clip_and_step_refreshes_packed_weights(cuda):
+    """clip_and_step bypasses the wrapped Optimizer.step (whose global post-hook
+    advances runtime/weights.generation) and its custom op bumps no _version:
+    it must advance the generation itself, or the HIP kernels keep reading the
+    packed weights of the previous step.  After one large-lr step the HIP
+    forward must agree with the stock-op forward on the UPDATED weights."""
+    from raft_stir_amd.config import make_args
+    from raft_stir_amd.data.synthetic import make_batch
+    from raft_stir_amd.models import RAFT
+    from raft_stir_amd.ops import _ext
+    from raft_stir_amd.runtime import weights
+
+    torch.manual_seed(0)
+    model = RAFT(make_args(mixed_precision=True)).to(cuda).to(memory_format=torch.channels_last).train()
+    opt = FusedClipAdamW([p for p in model.parameters() if p.requires_grad], lr=2e-2, weight_decay=0.0)
+    i1, i2, flow, valid = make_batch(1, 96, 128, seed=3, device=cuda)
+
+    def infer():
+        model.eval()
+        with torch.no_grad():
+            out = model(i1, i2, iters=3, test_mode=True)[1].float()
+        model.train()
+        return out
+
+    infer()  # pack every weight cache at the initial weights
+    model(i1, i2, iters=3)[-1].float().sub(flow).abs().mean().backward()
+    gen = weights.generation()
+    opt.clip_and_step(1.0)
+    assert weights.generation() > gen
+    hip = infer()
+    with _ext.reference_mode():
+        ref = infer()
+    rel = ((hip - ref).norm() / ref.norm()).item()
+    assert rel < 5e-2, rel  # stale packed weights give O(1) differences after this step
