@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Small-ensemble version of the 200-step training-fidelity check
 (tests/test_train_fidelity_gpu.py setup): for each weight-init seed, fp32
-(fused HIP engine, deterministic mode), bf16 default and bf16 deterministic
-mode.  Prints each run's first / last 50-step mean loss and the per-arm
+(fused HIP engine, deterministic mode), bf16 default, bf16 deterministic
+mode and fp32 on stock PyTorch ops.  Prints each run's first / last 50-step mean loss and the per-arm
 ensemble means, to separate bf16 / determinism effects from the trajectory
 chaos of a single run.
 
@@ -45,7 +45,7 @@ def main():
         return torch.stack(out).float().cpu()
 
     w = 50
-    arms = {"fp32_det": [], "bf16": [], "bf16_det": []}
+    arms = {"fp32_det": [], "bf16": [], "bf16_det": [], "fp32_stock": []}
     for seed in range(a.seeds):
         torch.manual_seed(seed)
         base = RAFT(make_args()).to(dev).to(memory_format=torch.channels_last).train()
@@ -55,6 +55,10 @@ def main():
                 m.cfg = m.cfg.__class__(**{**m.cfg.to_dict(), "mixed_precision": True})
             if arm.endswith("det"):
                 with deterministic(True):
+                    l = run(m, a.steps)
+            elif arm == "fp32_stock":  # the model on stock PyTorch ops (reference semantics), same optimizer
+                from raft_stir_amd.ops import _ext
+                with _ext.reference_mode():
                     l = run(m, a.steps)
             else:
                 l = run(m, a.steps)
