@@ -9,5 +9,6 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -5 gpurun_out/s24/gates.log
 if [[ $rc -ne 0 ]]; then exit $rc; fi
 timeout -k 10 1000 python -u scripts/fidelity_ensemble.py --seeds 3 > gpurun_out/s24/fid_ens.log 2>&1; rc=$?
-grep -v "amdgpu\|Warning\|sched.step" gpurun_out/s24/fid_ens.log | tail -14
-exit $rc
+grep -v "amdgpu\|Warning\|sched.step" gpurun_out/s24/fid_ens.log | tail -16
+if [[ $rc -ne 0 ]]; then exit $rc; fi
+timeout -k 10 300 python bench.py --steps 30 --warmup 5 --infer-reps 50 > gpurun_out/s24/bench.log 2>&1 && tail -1 gpurun_out/s24/bench.log | cut -c1-900
