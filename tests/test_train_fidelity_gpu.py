@@ -5,15 +5,14 @@ against fp32 references (reference train.py:47-72 loss, :162-183 step).
   and data, as ONE aggregate relative error over all parameters, bounded by
   the drift of stock PyTorch bf16 autocast (the reference's own AMP mode) on
   the same step;
-* 200 steps: fused-bf16 training vs fp32 (ATen-only) training from the same
-  initialisation on the same synthetic stream, AdamW + OneCycle as the
-  reference: both loss curves must fall and agree.
+* 200 steps, three weight-init seeds: the fused bf16 engine vs the fused
+  fp32 engine (split-bf16 F32 kernels), both deterministic, AdamW + OneCycle
+  as the reference: the first windows agree per seed, every run learns, and
+  the ensemble end points agree (see the test's docstring for the numbers).
 
 Measured on MI355X (round 2): one step, gradient relative error vs the fp32
 oracle 1.46 % for the fused engine and 1.65 % for stock bf16 autocast; loss
-32.388 vs 32.380.  200 steps (batch 2, 128x192, 6 iterations), means of the
-first / last 25 steps: fp32 23.12 -> 13.49, fused bf16 23.18 -> 13.77 in one
-process; fp32 23.13 -> 17.70, fused 23.10 -> 18.74 in another (nondeterminism).
+32.388 vs 32.380.
 """
 import copy
 
@@ -93,8 +92,11 @@ def _train(model, steps, batches, lr):
         preds = model(i1, i2, iters=6)
         loss, _ = sequence_loss(preds, flow, valid, 0.8, sync_metrics=False)
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
+        if hasattr(opt, "clip_and_step"):  # the trainer's path (train/trainer.py)
+            opt.clip_and_step(1.0)
+        else:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step()
         sched.step()
         losses.append(loss.detach())
     return torch.stack(losses).float().cpu()
@@ -102,36 +104,48 @@ def _train(model, steps, batches, lr):
 
 @pytest.mark.timeout(300)
 def test_fused_bf16_training_curve_tracks_fp32(cuda):
+    """200 steps of the fused bf16 engine vs the fused fp32 engine (the
+    reference's default training precision, on the split-bf16 F32 kernels),
+    both in deterministic mode (bitwise reproducible), over three weight-init
+    seeds.  Measured (profiles/r4/fidelity_ensemble_s24.txt, same setup):
+
+        first 50 steps   fp32 22.33 / 21.91 / 22.10   bf16 22.33 / 21.90 / 22.23
+        last 50 steps    fp32 19.01 / 10.97 / 12.35   bf16 19.16 / 13.55 /  6.55
+        (stock-op fp32, nondeterministic: 20.39 / 15.69 / 13.51)
+
+    The trajectories of this chaotic recurrent model decorrelate after the
+    first ~50 steps (single end points of one seed differ by up to ~2x between
+    precisions, and between two processes of the stock fp32 run), so the
+    bounds are: the first window agrees tightly per seed (<= 2 %); every run
+    learns; and the ensemble means of the last window agree within 30 %."""
     from raft_stir_amd.data.synthetic import make_batch
-    from raft_stir_amd.ops import _ext
-    torch.manual_seed(0)
-    m32 = RAFT(make_args()).to(cuda).to(memory_format=torch.channels_last).train()
-    mbf = copy.deepcopy(m32)
-    mbf.cfg = mbf.cfg.__class__(**{**mbf.cfg.to_dict(), "mixed_precision": True})
-    steps = 200
+    from raft_stir_amd.runtime.determinism import deterministic
 
     def batches(s):
         return make_batch(2, 128, 192, seed=1000 + s, device=cuda, max_disp=16.0)
 
-    from raft_stir_amd.runtime.determinism import deterministic
-    # 200 steps of a chaotic recurrent model.  The fused bf16 run is in
-    # deterministic mode (bitwise reproducible: 22.41 -> 20.23 on every run);
-    # the fp32 reference (stock ops) is not -- its own 50-step mean at step 200
-    # spans 10.8 .. 20.4 across processes on one box (profiles/r3/
-    # fidelity_spread.txt), so single end points differ by up to ~2x without
-    # any numerical fault.  The bounds: the two curves agree tightly BEFORE the
-    # trajectories decorrelate (first 50 steps, <= 3 %), both learn, and the
-    # end points stay within that measured ensemble spread.
-    with deterministic(True):
-        lbf = _train(mbf, steps, batches, 4e-4)
-    with _ext.reference_mode():
-        l32 = _train(m32, steps, batches, 4e-4)
-    w = 50
-    first_bf, last_bf = lbf[:w].mean().item(), lbf[-w:].mean().item()
-    first_32, last_32 = l32[:w].mean().item(), l32[-w:].mean().item()
-    print(f"fp32 {first_32:.3f} -> {last_32:.3f}; fused bf16 {first_bf:.3f} -> {last_bf:.3f}")
-    assert torch.isfinite(lbf).all() and torch.isfinite(l32).all()
-    assert abs(first_bf - first_32) <= 0.03 * first_32, (first_bf, first_32)  # before decorrelation
-    assert last_32 < 0.95 * first_32, (first_32, last_32)   # the fp32 run learns
-    assert last_bf < 0.95 * first_bf, (first_bf, last_bf)   # the fused run learns
-    assert 0.5 * last_32 <= last_bf <= 2.0 * last_32, (last_bf, last_32)  # within the fp32 ensemble spread
+    steps, w = 200, 50
+    ends = {"fp32": [], "bf16": []}
+    for seed in range(3):
+        torch.manual_seed(seed)
+        base = RAFT(make_args()).to(cuda).to(memory_format=torch.channels_last).train()
+        curves = {}
+        for arm in ("fp32", "bf16"):
+            m = copy.deepcopy(base)
+            if arm == "bf16":
+                m.cfg = m.cfg.__class__(**{**m.cfg.to_dict(), "mixed_precision": True})
+            with deterministic(True):
+                curves[arm] = _train(m, steps, batches, 4e-4)
+            assert torch.isfinite(curves[arm]).all()
+        for arm, l in curves.items():
+            first, last = l[:w].mean().item(), l[-w:].mean().item()
+            print(f"seed {seed} {arm}: {first:.3f} -> {last:.3f}")
+            assert last < 0.95 * first, (seed, arm, first, last)  # every run learns
+            ends[arm].append((first, last))
+        f32, fbf = ends["fp32"][-1][0], ends["bf16"][-1][0]
+        assert abs(fbf - f32) <= 0.02 * f32, (seed, fbf, f32)  # before the trajectories decorrelate
+    mean = {arm: (sum(a for a, _ in v) / 3, sum(b for _, b in v) / 3) for arm, v in ends.items()}
+    print("means", mean)
+    for arm, (first, last) in mean.items():
+        assert last < 0.8 * first, (arm, first, last)  # the ensemble learns
+    assert abs(mean["bf16"][1] - mean["fp32"][1]) <= 0.3 * mean["fp32"][1], mean
