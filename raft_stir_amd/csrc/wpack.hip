@@ -36,14 +36,14 @@ __global__ __launch_bounds__(256) void gather_kernel(const int* __restrict__ cod
       const long long* t = tab + (long long)((c >> 24) & 63) * kTabCols;
       const long long ptr = t[0];
       if (ptr != 0) {
-        long long li = c & 0xffffff;
-        const long long i3 = li % t[5];
-        li /= t[5];
-        const long long i2 = li % t[4];
-        li /= t[4];
-        const long long i1 = li % t[3];
-        const long long i0 = li / t[3];
-        const long long off = i0 * t[6] + i1 * t[7] + i2 * t[8] + i3 * t[9];
+        // 32-bit unravel (li < 2^24, every dim < 2^24): 64-bit division is a
+        // long software sequence on CDNA
+        unsigned li = (unsigned)(c & 0xffffff);
+        const unsigned s3 = (unsigned)t[5], s2 = (unsigned)t[4], s1 = (unsigned)t[3];
+        const unsigned q3 = li / s3, i3 = li - q3 * s3;
+        const unsigned q2 = q3 / s2, i2 = q3 - q2 * s2;
+        const unsigned i0 = q2 / s1, i1 = q2 - i0 * s1;
+        const long long off = (long long)i0 * t[6] + (long long)i1 * t[7] + (long long)i2 * t[8] + (long long)i3 * t[9];
         v = t[1] ? bf2f(reinterpret_cast<const bf16_t*>(ptr)[off]) : reinterpret_cast<const float*>(ptr)[off];
         if (c & (1 << 30)) v -= bf2f(f2bf(v));  // the lo half of a split (F32-tile) weight
       }
