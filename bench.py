@@ -53,8 +53,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
     ap.add_argument("--train-graph", action="store_true",
                     help="one GPU: replay the whole training step (forward, loss, backward, clip, AdamW) "
-                         "from one hipGraph (runtime/graph.py GraphedTrainStep).  Measured equal to the "
-                         "eager step (22.30 vs 22.47 ms: the step is GPU-bound), so off by default")
+                         "from one hipGraph (runtime/graph.py GraphedTrainStep).  Measured slower than the "
+                         "eager step (357 vs 390 pairs/s, profiles/r4/ab_train_graph_s27.txt), so off by default")
     ap.add_argument("--corr-dtype", default="auto", choices=["auto", "float32", "bfloat16"],
                     help="all-pairs pyramid storage; auto = bf16 under bf16 autocast (EPE-drift gate: "
                          "tests/test_model_gpu.py::test_bf16_pyramid_epe_drift)")

@@ -101,11 +101,13 @@ class GraphedTrainStep:
     ``step(batch)`` copies the batch into the static buffers, replays and
     returns the static loss tensor (valid until the next replay).
 
-    Measured on MI355X (RAFT, batch 8, 368x496, bench.py --train-graph): 22.30
-    ms/step graphed vs 22.47 ms eager -- the eager step is already GPU-bound
-    (its main-queue gaps are waits on the side streams, not on the host), so
-    the bench keeps the eager step and this stays an opt-in.  One GPU only:
-    the data-parallel step stays eager under DDP.
+    Measured on MI355X (RAFT, batch 8, 368x496, bench.py --train-graph):
+    round 2, 22.30 ms/step graphed vs 22.47 ms eager; round 4, 22.37 vs
+    20.49 ms (357 vs 390 pairs/s, profiles/r4/ab_train_graph_s27.txt) -- the
+    eager step is GPU-bound, and the replay (which also repacks every weight
+    layout inside the graph) is slower, so the bench keeps the eager step and
+    this stays an opt-in.  One GPU only: the data-parallel step stays eager
+    under DDP.
     """
 
     def __init__(self, model, optimizer, loss_fn, sample_batch, clip=1.0, warmup=3, iters=12):
