@@ -1085,7 +1085,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     else hipLaunchKernelGGL((conv::conv_halo_kernel<128, 4, 128>), grid, dim3(256), 0, stream, a);
     return;
   }
-  if (L.tile >= 42 && L.tile <= 53) {  // lean unrolled-tap tiles (conv_v2.hip)
+  if (L.tile >= 42 && L.tile <= 54) {  // lean unrolled-tap tiles (conv_v2.hip)
     conv_v2_launch(a, L.tile, stream);
     return;
   }

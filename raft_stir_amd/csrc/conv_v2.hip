@@ -380,11 +380,13 @@ bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream) {
   // 48 / 49: 2x2 waves of 64 Cout x 2x32 px (two A fragments per wave, 128 Cout x 4x32 px
   // per block; 3 / 2-slot ring); 50: 4x1 waves of 64 x 2x32 (256 Cout x 2x32 px, 3 slots)
   // 51 / 52: 4x2 waves of 64 Cout x 2x32 px (256 Cout x 4x32 px per block, 8 waves; 2 / 3-slot ring,
-  // 5x1: 2 slots -- its 8-row halo leaves no room for a third); 53: 4x2 waves of 32 x 2x32 (128 x 4x32, 2 slots).
+  // 5x1: 2 slots -- its 8-row halo leaves no room for a third); 53: 4x2 waves of 32 x 2x32 (128 x 4x32, 2 slots);
+  // 54: 3x2 waves of 64 x 2x32 (192 Cout x 4x32 px, 6 waves, 3 / 2-slot ring) for the 192-channel convs
+  // (convc2 forward and input gradients), which a 256-Cout tile pads by a third.
   // 51-53 stage each weight tile once for 128 pixels x all (or 128) output channels: the fewest staged bytes
   // per MAC of the family at the training grid (8 x 46 x 62: 192 blocks, one round on 256 CUs)
-  const int mw = (tile >= 48 && tile <= 52) ? 2 : 1;
-  const int nwm = tile == 43 ? 1 : (tile == 44 || tile >= 50) ? 4 : 2;
+  const int mw = ((tile >= 48 && tile <= 52) || tile == 54) ? 2 : 1;
+  const int nwm = tile == 43 ? 1 : tile == 54 ? 3 : (tile == 44 || tile >= 50) ? 4 : 2;
   const int nwn = tile == 43 ? 4 : (tile == 44 || tile == 50) ? 1 : 2;
   const int BM = 32 * nwm * mw, TH = 2 * nwn;
   const dim3 grid(cdiv(a.Cout, BM) * a.B * cdiv(a.H, TH) * cdiv(a.W, 32));
@@ -402,6 +404,7 @@ bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream) {
     case 51: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 4, 2, 2, 2>), grid, block, 0, stream, a); break; \
     case 52: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 4, 2, (KH_ == 5 ? 2 : 3), 2>), grid, block, 0, stream, a); break; \
     case 53: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 4, 2, 2, 1>), grid, block, 0, stream, a); break; \
+    case 54: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 3, 2, (KH_ == 5 ? 2 : 3), 2>), grid, block, 0, stream, a); break; \
     default: hipLaunchKernelGGL((conv::conv_v2_kernel<KH_, KW_, 2, 2, 3>), grid, block, 0, stream, a); break; \
   }
   if (a.KH == 3 && a.KW == 3) {

@@ -201,10 +201,10 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK(tile >= 0 && tile <= 53, "conv_fused: tile must be in [0,53]");
-  if (tile >= 42 && tile <= 53)
+  TORCH_CHECK(tile >= 0 && tile <= 54, "conv_fused: tile must be in [0,54]");
+  if (tile >= 42 && tile <= 54)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
-                "conv_fused: tiles 42-53 are instantiated for 3x3, 1x5 and 5x1 kernels only");
+                "conv_fused: tiles 42-54 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
   TORCH_CHECK(!(tile >= 38 && tile <= 40) || f32, "conv_fused: tiles 38-40 are the fp32 split-K tiles");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
@@ -217,6 +217,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                      tile == 39;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
   const int tileM = (tile == 48 || tile == 49 || tile == 53) ? 128 : (tile == 50 || tile == 51 || tile == 52) ? 256
+                    : tile == 54 ? 192
                     : (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
                     : tile == 0 ? 32
                     : (tile == 27 || tile == 30 || tile == 32) ? 256
@@ -292,7 +293,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
   if (nx.chs)
-    TORCH_CHECK(!(tile >= 42 && tile <= 53), "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-53)");
+    TORCH_CHECK(!(tile >= 42 && tile <= 54), "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54)");
   L.chs = nx.chs;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();

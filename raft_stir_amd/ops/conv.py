@@ -127,7 +127,9 @@ def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
 # variant with the lowest graph-timed latency for every conv_fused call of the
 # training step and of inference at the benchmark shapes, keyed by
 # tune_key().  Calls not in the table use the choose_tile heuristic.
-_TUNED_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "conv_tuning.json")
+# RS_CONV_TUNING_FILE: another tile table (A/B of a retune against the shipped one)
+_TUNED_PATH = os.environ.get("RS_CONV_TUNING_FILE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "conv_tuning.json")
 _TUNED: dict | None = None
 _RECORD: list | None = None  # scripts/tune_conv.py: conv_fused calls are appended here
 
