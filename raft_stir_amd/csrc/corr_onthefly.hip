@@ -20,6 +20,13 @@
 // decomposition as corr_lookup's backward), then df1 accumulates in registers
 // (plain store once per pixel: every pixel owns its df1 row) and df2_l
 // receives g * f1 through float atomics (cells are shared between pixels).
+// Default kernels (per-query ones above as fallback / RS_OTF_TILE=0): 4 x 4
+// query TILES -- the forward gathers the bounding box of the tile's 16
+// windows once per level and computes the cell dots as a small GEMM on MFMA
+// (otf_tile_kernel); the backward gathers the tile's cell gradients over the
+// same box into LDS, accumulates df1 in registers and sums each box cell's
+// df2 over the 16 queries before ONE atomic per (cell, channel)
+// (otf_tile_bwd_kernel).
 // Deterministic mode (DET): the df2 contributions are rounded to 32.32
 // fixed point and summed with 64-bit integer atomics -- integer addition is
 // associative, so the sums do not depend on the order the waves arrive in
