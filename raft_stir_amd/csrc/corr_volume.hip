@@ -298,7 +298,7 @@ constexpr int FB = 128;  // targets (M) and queries (N) per block tile
 
 // vol_l[b, i, n] = scale * <f1[b, i, :], f2_l[b, n, :]>: M = targets, N = queries,
 // so an MFMA accumulator lane holds 4 CONSECUTIVE targets of one query row.
-template <bool OB, bool DB>  // DB: two operand stages, one barrier per K step (RS_CORR_FLAT_DB=0: one stage)
+template <bool OB, bool DB>  // DB: two operand stages, one barrier per K step (RS_CORR_FLAT_DB=1)
 __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
   // two A | B operand stages (64-channel K step, 2 x 32 KiB: the next step is
   // stored while this one is multiplied, one barrier per step), then reused by
@@ -443,10 +443,10 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
   }
 }
 
-static bool flat_db() {
+static bool flat_db() {  // RS_CORR_FLAT_DB=1: the two-stage variant (pending its in-situ A/B)
   static const bool on = [] {
     const char* e = getenv("RS_CORR_FLAT_DB");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
