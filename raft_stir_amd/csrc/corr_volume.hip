@@ -298,13 +298,14 @@ constexpr int FB = 128;  // targets (M) and queries (N) per block tile
 
 // vol_l[b, i, n] = scale * <f1[b, i, :], f2_l[b, n, :]>: M = targets, N = queries,
 // so an MFMA accumulator lane holds 4 CONSECUTIVE targets of one query row.
-template <bool OB, bool DB>  // DB: two operand stages, one barrier per K step (RS_CORR_FLAT_DB=1)
+template <bool OB>
 __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
-  // two A | B operand stages (64-channel K step, 2 x 32 KiB: the next step is
-  // stored while this one is multiplied, one barrier per step), then reused by
-  // the epilogue transpose: 4 wave-private 64 x (64+4) fp32 tiles (68 KiB)
-  constexpr int OPND = 2 * 2 * FB * 8, EPI = 4 * 64 * 68 / 4;
+  // A | B operand tiles (64-channel K step, 32 KiB), then reused by the epilogue
+  // transpose: 4 wave-private 64 x (64+4) fp32 tiles (68 KiB)
+  constexpr int OPND = 2 * FB * 8, EPI = 4 * 64 * 68 / 4;
   __shared__ __attribute__((aligned(16))) uint4 lds[OPND > EPI ? OPND : EPI];
+  uint4* As = lds;
+  uint4* Bs = lds + FB * 8;
   // level / tile decode with constant kernarg indices only (a runtime index
   // into FlatArgs' arrays copied the struct to scratch: 160 B per lane)
   const int per_b = a.levels == 1 ? a.tstart[1] : a.levels == 2 ? a.tstart[2] : a.levels == 3 ? a.tstart[3] : a.tstart[4];
@@ -335,14 +336,12 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
       rb[q] = q0 + r < N1 ? vb_ : make_uint4(0, 0, 0, 0);                              \
     }                                                                                    \
   } while (0)
-#define RS_FL_STORE(ST)                                                                  \
+#define RS_FL_STORE()                                                                    \
   do {                                                                                   \
-    uint4* As_ = lds + (ST) * 2 * FB * 8;                                                \
-    uint4* Bs_ = As_ + FB * 8;                                                           \
     _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                      \
       const int idx = tid + 256 * q;                                                     \
-      As_[swz(idx >> 3, idx & 7)] = ra[q];                                               \
-      Bs_[swz(idx >> 3, idx & 7)] = rb[q];                                               \
+      As[swz(idx >> 3, idx & 7)] = ra[q];                                                \
+      Bs[swz(idx >> 3, idx & 7)] = rb[q];                                                \
     }                                                                                    \
   } while (0)
 
@@ -354,12 +353,10 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
   const int lr = lane & 15, lg = lane >> 4;
   const int nk = C / 64;
   RS_FL_LOAD(0);
-  RS_FL_STORE(0);
+  RS_FL_STORE();
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     if (ks + 1 < nk) RS_FL_LOAD((ks + 1) * 64);
-    const uint4* As = lds + (DB ? (ks & 1) : 0) * 2 * FB * 8;
-    const uint4* Bs = As + FB * 8;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8_t af[4], bfr[4];
@@ -380,14 +377,8 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
     }
     if (ks + 1 < nk) {
-      if constexpr (DB) {
-        // the other stage was last read in step ks - 1, which every wave
-        // finished before the barrier that ended it
-        RS_FL_STORE((ks + 1) & 1);
-      } else {
-        __syncthreads();
-        RS_FL_STORE(0);
-      }
+      __syncthreads();
+      RS_FL_STORE();
       __syncthreads();
     }
   }
@@ -442,21 +433,6 @@ __global__ __launch_bounds__(256) void corr_flat_kernel(FlatArgs a) {
     }
   }
 }
-
-static bool flat_db() {  // RS_CORR_FLAT_DB=1: the two-stage variant (pending its in-situ A/B)
-  static const bool on = [] {
-    const char* e = getenv("RS_CORR_FLAT_DB");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-#define RS_FLAT_LAUNCH(OB_)                                                                              \
-  do {                                                                                                   \
-    if (corrvol::flat_db())                                                                              \
-      hipLaunchKernelGGL((corrvol::corr_flat_kernel<OB_, true>), grid, dim3(256), 0, stream, fa);        \
-    else                                                                                                 \
-      hipLaunchKernelGGL((corrvol::corr_flat_kernel<OB_, false>), grid, dim3(256), 0, stream, fa);       \
-  } while (0)
 
 // fp32 feature maps on the bf16 flat GEMM by operand splitting (as the F32
 // conv tiles): x = xh + xl, xh = bf16(x), xl = bf16(x - xh), and
@@ -546,9 +522,9 @@ static void flat_launch(const bf16_t* f1, const bf16_t* const* f2l, int B, int N
   fa.tstart[levels] = acc_t;
   const dim3 grid((unsigned)(acc_t * B));
   if (out_bf16)
-    RS_FLAT_LAUNCH(true);
+    hipLaunchKernelGGL(corrvol::corr_flat_kernel<true>, grid, dim3(256), 0, stream, fa);
   else
-    RS_FLAT_LAUNCH(false);
+    hipLaunchKernelGGL(corrvol::corr_flat_kernel<false>, grid, dim3(256), 0, stream, fa);
 }
 
 // bytes of the fp32 split path's workspace (corr_volume_launch with bf16 = false, ws != null)
@@ -622,9 +598,9 @@ void corr_volume_launch(const void* f1, const void* f2, bool bf16, int B, int N1
     fa.tstart[levels] = acc_t;
     const dim3 grid((unsigned)(acc_t * B));
     if (out_bf16)
-      RS_FLAT_LAUNCH(true);
+      hipLaunchKernelGGL(corrvol::corr_flat_kernel<true>, grid, dim3(256), 0, stream, fa);
     else
-      RS_FLAT_LAUNCH(false);
+      hipLaunchKernelGGL(corrvol::corr_flat_kernel<false>, grid, dim3(256), 0, stream, fa);
     return;
   }
   corrvol::PyrOut po;
