@@ -67,15 +67,30 @@ def _sources():
     return [os.path.join(CSRC, s) for s in srcs]
 
 
+def _local_includes(path: str, seen=None) -> list:
+    """The csrc/ headers ``path`` includes, transitively (``#include "x"``)."""
+    seen = set() if seen is None else seen
+    with open(path, "rb") as f:
+        for line in f.read().decode("utf-8", "replace").splitlines():
+            line = line.strip()
+            if line.startswith("#include") and '"' in line:
+                name = line.split('"')[1]
+                hdr = os.path.join(CSRC, name)
+                if name not in seen and os.path.exists(hdr):
+                    seen.add(name)
+                    _local_includes(hdr, seen)
+    return sorted(seen)
+
+
 def _digest(path: str, flags) -> str:
     h = hashlib.sha1()
     h.update(json.dumps(flags).encode())
     with open(path, "rb") as f:
         h.update(f.read())
-    for hdr in sorted(os.listdir(CSRC)):
-        if hdr.endswith(".h"):
-            with open(os.path.join(CSRC, hdr), "rb") as f:
-                h.update(f.read())
+    for hdr in _local_includes(path):
+        h.update(hdr.encode())
+        with open(os.path.join(CSRC, hdr), "rb") as f:
+            h.update(f.read())
     return h.hexdigest()
 
 

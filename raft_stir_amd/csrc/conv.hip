@@ -1089,6 +1089,10 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     conv_v2_launch(a, L.tile, stream);
     return;
   }
+  if (L.tile >= 60) {  // weight-streaming tiles (conv_v3.hip), fragment-major weights
+    conv_v3_launch(a, L.tile, stream);
+    return;
+  }
   if (L.tile == 5) {
     hipLaunchKernelGGL(conv::conv_smalln_kernel, dim3(cdiv(a.P, 16)), dim3(256), 0, stream, a);
   } else if (L.tile >= 2) {

@@ -35,57 +35,6 @@
 namespace rs {
 namespace conv {
 
-template <int N>
-__device__ __forceinline__ void wait_lgkm() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// 32x32x16 accumulator -> the shared epilogue (4 consecutive channels per call)
-template <int E>
-__device__ __forceinline__ void epi32(const Args& a, const f32x16_t& acc, int m0, int lane, int p, int pb, int py,
-                                      int px, bool vec) {
-  if (pb < 0) return;
-  const int HW = a.H * a.W;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int cb = m0 + 8 * g + 4 * (lane >> 5);
-    if (cb >= a.Cout) continue;
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = acc[4 * g + j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
-    epi_frag<E>(a, v, cb, p, pb, py, px, HW, vec);
-  }
-}
-
-template <int NB>
-__device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[NB], int m0, int lane,
-                                           const int (&pp)[NB], const int (&pb)[NB], const int (&py)[NB],
-                                           const int (&px)[NB]) {
-  const bool vec =
-      ((a.ooff | a.ostr | a.o2off | a.o2str | a.o3off | a.o3str | a.a1off | a.a1str | a.a2off | a.a2str) & 3) == 0 &&
-      (((uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.out3 | (uintptr_t)a.aux1 | (uintptr_t)a.aux2) & 15) == 0;
-  switch (a.epi) {
-#define RS_E2(E)                                                                      \
-  case E:                                                                             \
-    _Pragma("unroll") for (int nb = 0; nb < NB; ++nb)                                 \
-      epi32<E>(a, acc[nb], m0, lane, pp[nb], pb[nb], py[nb], px[nb], vec);            \
-    break
-    RS_E2(EPI_FLOW);
-    RS_E2(EPI_GRU_ZR);
-    RS_E2(EPI_GRU_Q);
-    RS_E2(EPI_RELU_BWD);
-    RS_E2(EPI_ACC_F32);
-    RS_E2(EPI_GRU_QBWD);
-    RS_E2(EPI_RELU);
-    RS_E2(EPI_SCALE);
-#undef RS_E2
-    default:
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) epi32<EPI_BIAS>(a, acc[nb], m0, lane, pp[nb], pb[nb], py[nb], px[nb], vec);
-      break;
-  }
-}
-
 template <int KH, int KW, int NWM, int NWN, int S, int MW = 1>
 struct V2 {
   static constexpr int T = KH * KW;

@@ -127,6 +127,7 @@ class MpiSintel(FlowDataset):
 
 
 _CHAIRS_INDEX = osp.join(osp.dirname(osp.abspath(__file__)), "chairs_val_index.txt")
+_PACKAGED_SPLIT_NOTED = False
 
 
 def load_chairs_split(split_file="chairs_split.txt", root=None) -> np.ndarray:
@@ -141,6 +142,10 @@ def load_chairs_split(split_file="chairs_split.txt", root=None) -> np.ndarray:
     for c in cands:
         if c and osp.exists(c):
             return np.loadtxt(c, dtype=np.int32).reshape(-1)
+    global _PACKAGED_SPLIT_NOTED
+    if not _PACKAGED_SPLIT_NOTED:
+        _PACKAGED_SPLIT_NOTED = True
+        print(f"FlyingChairs: {split_file} not found; using the packaged 22,872-pair split table", flush=True)
     total, idx = None, []
     with open(_CHAIRS_INDEX) as f:
         for line in f:
@@ -165,6 +170,9 @@ class FlyingChairs(FlowDataset):
         if not flows:
             return
         split_list = load_chairs_split(split_file, root)
+        # a split table for a different release would silently mislabel pairs
+        assert len(split_list) == len(flows), (
+            f"FlyingChairs: split table has {len(split_list)} entries for {len(flows)} flow files")
         want = {"training": 1, "validation": 2}.get(split)
         for i in range(len(flows)):
             if split_list[i] == want:

@@ -63,6 +63,23 @@ def pack_weight_split(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: i
     return split_weight(pack_weight(weight, segs, cout_pad, torch.float32))
 
 
+V3_TILES = (60, 61, 62, 63, 64)
+
+
+@torch.no_grad()
+def frag_weight(w: torch.Tensor) -> torch.Tensor:
+    """A packed weight [Cout_pad][taps][Ktot] in the fragment-major layout of
+    the weight-streaming tiles 60-64 (csrc/conv_v3.h): per 32-row block, per
+    64-channel K chunk, per tap, per 16-channel slice, the 1 KB A fragment of a
+    32x32x16 MFMA (lane h*32 + r holds row r, channels 16 ks + 8 h .. + 8), so
+    each wave's weight stream is one contiguous run of 1 KB loads.  Same shape
+    and element count as the input (a permutation of it)."""
+    cp, taps, k = w.shape
+    assert cp % 32 == 0 and k % 64 == 0, (cp, k)
+    v = w.view(cp // 32, 32, taps, k // 64, 4, 2, 8)  # rb, r, t, c, ks, h, j
+    return v.permute(0, 3, 2, 4, 5, 1, 6).contiguous().view(cp, taps, k)
+
+
 F32_TILES = (6, 7, 8)
 
 

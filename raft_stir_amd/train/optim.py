@@ -85,7 +85,7 @@ class FusedClipAdamW(optim.Optimizer):
             grads.append(gr)
             moff.append(o)
         if not params:
-            return None
+            return torch.zeros((), device=self._m.device)
         lr = g["lr"]
         lr_t = lr if isinstance(lr, torch.Tensor) else None
         b1, b2 = g["betas"]
@@ -93,22 +93,28 @@ class FusedClipAdamW(optim.Optimizer):
                                                0.0 if lr_t is not None else float(lr), b1, b2, g["eps"],
                                                g["weight_decay"], float(max_norm), self._state)
         # the parameters changed behind autograd's back (a custom mutable op
-        # bumps no _version) and clip_and_step bypasses the wrapped step() whose
-        # global post-hook advances the weight generation: advance it here, or
-        # every packed-weight cache (ops/wpack.py, the fused engines) would keep
-        # serving the previous weights to the HIP kernels
+        # bumps no _version): advance the weight generation here as well as in
+        # the global step post-hook, so every packed-weight cache (ops/wpack.py,
+        # the fused engines) re-packs even for a direct _run
         weights.bump()
         return norm
 
     def clip_and_step(self, max_norm: float):
-        return self._run(max_norm)
+        """Clip + update through the hooked :meth:`step` (step pre/post hooks,
+        the LR scheduler's step-order bookkeeping); returns the total norm."""
+        self._clip = float(max_norm)
+        try:
+            self.step()
+        finally:
+            self._clip = 0.0
+        return self._last_norm
 
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        self._run(0.0)
+        self._last_norm = self._run(getattr(self, "_clip", 0.0))
         return loss
 
     def state_dict(self):

@@ -26,6 +26,13 @@ SHAPES = [
     ("head", 128, 512, 3, 3),
     ("flow", 256, 2, 3, 3),
     ("mask2", 256, 576, 1, 1),
+    # input gradients of the training step (Cout = the forward's Cin)
+    ("zr_dg", 256, 384, 1, 5),
+    ("q_dg", 128, 384, 1, 5),
+    ("head_dg", 512, 128, 3, 3),
+    ("c2_dg", 192, 256, 3, 3),
+    ("cv_dg", 128, 256, 3, 3),
+    ("f2_dg", 64, 128, 3, 3),
 ]
 
 
@@ -80,7 +87,7 @@ def main():
     global GRAPH
     GRAPH = not a.no_graph
     from raft_stir_amd.ops import _ext
-    from raft_stir_amd.ops.conv import EPI_RELU, conv_fused, pack_bias, pack_weight, pad_to
+    from raft_stir_amd.ops.conv import EPI_RELU, V3_TILES, conv_fused, frag_weight, pack_bias, pack_weight, pad_to
     _ext.load(raise_on_error=True)
     dev = torch.device("cuda", 0)
     B, (H, W) = a.batch, a.hw
@@ -94,6 +101,7 @@ def main():
         b = torch.randn(cout, device=dev)
         out = torch.empty(B, H, W, pad_to(cout, 8), device=dev, dtype=torch.bfloat16)
         wp = pack_weight(w, [(cin, [(0, cin, 0)])], pad_to(cout, 256))
+        wf = frag_weight(wp) if cin % 64 == 0 else None
         bp = pack_bias(b)
         flop = 2.0 * P * cout * cin * kh * kw
         line = f"{name:8s} P={P:6d} K={cin * kh * kw:5d} N={cout:4d} GF={flop / 1e9:6.2f} |"
@@ -101,8 +109,11 @@ def main():
         for t in a.tiles:
             if (t == 5) != (cout <= 16) or (t >= 6 and t not in (12, 13, 14) and cin % 64):
                 continue
+            if t in V3_TILES and kh * kw not in (5, 9):
+                continue
+            wt = wf if t in V3_TILES else wp
             try:
-                us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
+                us = timeit(lambda: conv_fused([(x, 0, cin)], wt, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
             except RuntimeError as e:  # tile constraint (e.g. kernel too large for a halo tile)
                 line += f" tile{t} n/a |"
                 continue

@@ -315,6 +315,15 @@ def test_packaged_chairs_split(tmp_path, monkeypatch):
         assert np.array_equal(s, np.loadtxt(ref, dtype=np.int32))
 
 
+def test_packaged_chairs_split_rejects_other_release(fake_root, tmp_path, monkeypatch):
+    """A Chairs copy whose pair count differs from the packaged table's 22,872
+    fails loudly instead of mislabelling train / validation pairs."""
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(AssertionError, match="split table has 22872 entries for 3 flow files"):
+        datasets.FlyingChairs(split="training", root=f"{fake_root}/FlyingChairs_release/data",
+                              split_file="no_such_split.txt")
+
+
 def test_fused_resize_crop_matches_resize_then_crop(monkeypatch):
     """FlowAugmentor.spatial_transform's native crop-window resize
     (csrc_host resize_crop) is bitwise the full resize + flips + crop."""

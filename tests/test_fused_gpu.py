@@ -8,8 +8,9 @@ import torch.nn.functional as F
 
 from raft_stir_amd.config import make_args
 from raft_stir_amd.models import RAFT
-from raft_stir_amd.ops.conv import (EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE,
-                                    conv_fused, pack_bias, pack_weight, pad_to)
+from raft_stir_amd.ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR,
+                                    EPI_RELU, EPI_RELU_BWD, EPI_SCALE, V3_TILES, conv_fused, frag_weight,
+                                    pack_bias, pack_weight, pad_to)
 
 pytestmark = pytest.mark.gpu
 
@@ -79,6 +80,79 @@ def test_conv_v2_tiles_vs_conv2d(cuda, k, tile, shape):
     got = out[..., :cout].float().permute(0, 3, 1, 2)
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
     assert (out[..., cout:] == 7).all()
+
+
+@pytest.mark.parametrize("k", [(3, 3), (1, 5), (5, 1)])
+@pytest.mark.parametrize("tile", list(V3_TILES))
+@pytest.mark.parametrize("shape", [(2, 11, 19), (1, 9, 70), (1, 14, 33)])
+def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
+    """csrc/conv_v3.h (weight-streaming tiles: per-wave A fragments global ->
+    VGPR from the fragment-major layout, halo per 64-channel chunk in LDS, one
+    barrier per chunk): every tile 60-64 on partial patches in both
+    directions, three input segments (4 chunks: the halo double buffer flips
+    an even and an odd number of times), Cout not a multiple of the block's
+    (the row blocks past the packed weight read as zeros)."""
+    torch.manual_seed(5)
+    B, H, W = shape
+    kh, kw = k
+    chans = (64, 64, 128) if H != 14 else (64, 128, 128)  # 4 / 5 chunks
+    segs = [torch.randn(B, H, W, c, device=cuda).to(torch.bfloat16) for c in chans]
+    cin = sum(chans)
+    cout = 200
+    w = torch.randn(cout, cin, kh, kw, device=cuda) * 0.05
+    b = torch.randn(cout, device=cuda)
+    pieces, o = [], 0
+    for c in chans:
+        pieces.append((c, [(o, c, 0)]))
+        o += c
+    wp = frag_weight(pack_weight(w, pieces, pad_to(cout, 32)))
+    out = torch.full((B, H, W, cout + 8), 7.0, device=cuda, dtype=torch.bfloat16)
+    conv_fused([(s, 0, s.shape[-1]) for s in segs], wp, pack_bias(b), kh, kw, cout, EPI_RELU, out, 0, tile=tile)
+    x = torch.cat(segs, -1).float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2)).relu()
+    got = out[..., :cout].float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
+    assert (out[..., cout:] == 7).all()
+
+
+@pytest.mark.parametrize("epi", [EPI_GRU_ZR, EPI_GRU_Q, EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_SCALE])
+def test_conv_v3_epilogues_match_v2(cuda, epi):
+    """Every epilogue kind the training step runs on the update-block convs:
+    tile 60 (fragment-major weights) against tile 52 (conv_v2, the standard
+    layout) on the same inputs -- same fused epilogue code, different K
+    accumulation order."""
+    torch.manual_seed(6)
+    B, H, W, hd = 2, 13, 37, 64
+    segs = [torch.randn(B, H, W, 128, device=cuda).to(torch.bfloat16) for _ in range(2)]
+    cout = 2 * hd if epi == EPI_GRU_ZR else (hd if epi == EPI_GRU_Q else 192)
+    w = torch.randn(cout, 256, 1, 5, device=cuda) * 0.05
+    b = torch.randn(cout, device=cuda) * 0.1
+    wp = pack_weight(w, [(128, [(0, 128, 0)]), (128, [(128, 128, 0)])], pad_to(cout, 256))
+    wf = frag_weight(wp)
+    aux1 = torch.rand(B, H, W, 256, device=cuda).to(torch.bfloat16) - 0.3
+    aux2 = torch.rand(B, H, W, 256, device=cuda).to(torch.bfloat16)
+    f32out = epi in (EPI_ACC_F32, EPI_GRU_QBWD)
+    outs = []
+    for tile, wt in ((52, wp), (60, wf)):
+        torch.manual_seed(7)
+        out = torch.randn(B, H, W, 256, device=cuda)
+        out = out if f32out else out.to(torch.bfloat16)
+        out2 = torch.zeros(B, H, W, 256, device=cuda, dtype=torch.bfloat16)
+        out3 = torch.zeros_like(out2)
+        kw_ = dict(scale=0.25, tile=tile)
+        if epi == EPI_GRU_ZR:
+            kw_.update(hd=hd, out2=out2, out3=out3, aux1=aux1, a1off=8)
+        elif epi == EPI_GRU_Q:
+            kw_.update(out2=out2, aux1=aux1, a1off=0, aux2=aux2, a2off=64)
+        elif epi == EPI_RELU_BWD:
+            kw_.update(aux1=aux1, a1off=16)
+        elif epi == EPI_GRU_QBWD:
+            kw_.update(hd=hd, out2=out2, aux1=aux1, aux2=aux2)
+        bias = None if epi in (EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD) else pack_bias(b)
+        conv_fused([(s, 0, 128) for s in segs], wt, bias, 1, 5, cout, epi, out, 0, **kw_)
+        outs.append((out.float(), out2.float(), out3.float()))
+    for x, y in zip(*outs):
+        torch.testing.assert_close(y, x, atol=2e-2, rtol=2e-2)
 
 
 def test_gru_epilogues(cuda):

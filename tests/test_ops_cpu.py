@@ -138,3 +138,15 @@ def test_sequence_loss_formula():
     epe = (preds[-1] - gt).pow(2).sum(1).sqrt()[v[:, 0] > 0]
     assert abs(metrics["epe"] - epe.mean().item()) < 1e-5
     assert abs(metrics["1px"] - (epe < 1).float().mean().item()) < 1e-6
+
+
+def test_frag_weight_layout():
+    """ops/conv.py frag_weight: element (rb, c, t, ks, lane, j) of the
+    fragment-major layout (csrc/conv_v3.h) is weight[rb*32 + lane%32][t][c*64 +
+    16 ks + 8 (lane // 32) + j]."""
+    from raft_stir_amd.ops.conv import frag_weight
+    cp, taps, k = 64, 5, 128
+    w = torch.arange(cp * taps * k, dtype=torch.float32).view(cp, taps, k)
+    f = frag_weight(w).reshape(cp // 32, k // 64, taps, 4, 64, 8)
+    for rb, c, t, ks, lane, j in [(0, 0, 0, 0, 0, 0), (1, 1, 4, 3, 63, 7), (0, 1, 2, 1, 37, 5), (1, 0, 3, 2, 12, 1)]:
+        assert f[rb, c, t, ks, lane, j] == w[rb * 32 + lane % 32, t, c * 64 + 16 * ks + 8 * (lane // 32) + j]

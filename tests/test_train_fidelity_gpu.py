@@ -8,7 +8,9 @@ against fp32 references (reference train.py:47-72 loss, :162-183 step).
 * 200 steps, three weight-init seeds: the fused bf16 engine vs the fused
   fp32 engine (split-bf16 F32 kernels), both deterministic, AdamW + OneCycle
   as the reference: the first windows agree per seed, every run learns, and
-  the ensemble end points agree (see the test's docstring for the numbers).
+  the ensemble end points agree (see the test's docstring for the numbers);
+  for seed 0 the fused fp32 engine's first window also tracks an independent
+  stock-op arm (ATen module graph + torch.optim.AdamW).
 
 Measured on MI355X (round 2): one step, gradient relative error vs the fp32
 oracle 1.46 % for the fused engine and 1.65 % for stock bf16 autocast; loss
@@ -80,11 +82,11 @@ def test_fused_bf16_step_vs_fp32_oracle(cuda):
     assert rel_f < 0.1, rel_f
 
 
-def _train(model, steps, batches, lr):
+def _train(model, steps, batches, lr, num_steps=None, stock=False):
     from raft_stir_amd.train.loss import sequence_loss
     from raft_stir_amd.train.optim import fetch_optimizer
-    args = make_args(lr=lr, wdecay=1e-5, epsilon=1e-8, num_steps=steps)
-    opt, sched = fetch_optimizer(args, model)
+    args = make_args(lr=lr, wdecay=1e-5, epsilon=1e-8, num_steps=num_steps or steps)
+    opt, sched = fetch_optimizer(args, model, fused=False if stock else None)
     losses = []
     for s in range(steps):
         i1, i2, flow, valid = batches(s)
@@ -144,6 +146,18 @@ def test_fused_bf16_training_curve_tracks_fp32(cuda):
             ends[arm].append((first, last))
         f32, fbf = ends["fp32"][-1][0], ends["bf16"][-1][0]
         assert abs(fbf - f32) <= 0.02 * f32, (seed, fbf, f32)  # before the trajectories decorrelate
+        if seed == 0:
+            # independent arm: the stock-op module graph (ATen convs, grid_sample,
+            # matmul volume) with torch.optim.AdamW, no fused kernel or optimizer
+            # in common with the two engines; the fused fp32 engine must track it
+            # over the first window (same schedule: OneCycle over 200 steps)
+            from raft_stir_amd.ops import _ext
+            m = copy.deepcopy(base)
+            with _ext.reference_mode():
+                stock = _train(m, w, batches, 4e-4, num_steps=steps, stock=True)
+            s_first, f_first = stock.mean().item(), curves["fp32"][:w].mean().item()
+            print(f"seed 0 stock-op fp32 first {w}: {s_first:.3f} (fused fp32 {f_first:.3f})")
+            assert abs(f_first - s_first) <= 0.03 * s_first, (f_first, s_first)
     mean = {arm: (sum(a for a, _ in v) / 3, sum(b for _, b in v) / 3) for arm, v in ends.items()}
     print("means", mean)
     for arm, (first, last) in mean.items():
