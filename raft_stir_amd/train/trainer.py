@@ -281,7 +281,9 @@ def main(argv=None):
     torch.manual_seed(args.seed)
     launched = "WORLD_SIZE" in os.environ
     ngpu = torch.cuda.device_count()  # does not initialise HIP
-    if not launched and len(args.gpus) > 1 and ngpu > 1 and args.device != "cpu":
+    # RS_SPAWN_CPU=1: the same spawn path with CPU (gloo) ranks (tests/test_distributed_cpu.py)
+    cpu_spawn = os.environ.get("RS_SPAWN_CPU") == "1" and args.device == "cpu"
+    if not launched and len(args.gpus) > 1 and ((ngpu > 1 and args.device != "cpu") or cpu_spawn):
         # the reference's `--gpus 0 1` -> one process per GPU (DDP over RCCL)
         import torch.multiprocessing as mp
         port = 29500 + (os.getpid() % 1000)
