@@ -687,6 +687,135 @@ __device__ __forceinline__ void epi32(const Args& a, const f32x16_t& acc, int m0
   }
 }
 
+// Batched form of epi32 for a whole 32-row fragment inside Cout (the common
+// case): every bias / aux / read-modify-write load of the NB accumulators is
+// issued first, unconditionally (pixels outside the image read pixel 0 and
+// store nothing), and the arithmetic + stores follow -- ONE memory round trip
+// per group of NBC accumulators instead of one dependent L2 round trip per
+// 4-channel group (the per-element form branches around every load and waits
+// vmcnt(0) after each: ~24 serial round trips for a 6-row patch).
+template <int NB, int E>
+__device__ __forceinline__ void epi32_batch(const Args& a, const f32x16_t (&acc)[NB], int m0, int lane,
+                                            const int (&pp)[NB], const int (&pb)[NB]) {
+  const int h4 = 4 * (lane >> 5);
+  float bz[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bz[i] = a.bias ? a.bias[m0 + 8 * (i >> 2) + h4 + (i & 3)] : 0.f;
+  // GRU_ZR / GRU_QBWD: the fragment lies wholly on one side of hd (host: hd % 32 == 0 on this path)
+  const bool lo = m0 < a.hd;
+  constexpr int NBC = NB > 3 ? 3 : NB;
+#pragma unroll
+  for (int n0 = 0; n0 < NB; n0 += NBC) {
+    uint2 l1[NBC][4], l2[NBC][4];
+    float4 lf[NBC][4];
+    // ---- phase 1: loads
+#pragma unroll
+    for (int k = 0; k < NBC; ++k) {
+      if (n0 + k >= NB) break;
+      const size_t p = (size_t)(pb[n0 + k] >= 0 ? pp[n0 + k] : 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int cb = m0 + 8 * g + h4;
+        if constexpr (E == EPI_GRU_ZR) {
+          if (!lo) l1[k][g] = *reinterpret_cast<const uint2*>(a.aux1 + p * a.a1str + a.a1off + cb - a.hd);
+        } else if constexpr (E == EPI_GRU_Q) {
+          l1[k][g] = *reinterpret_cast<const uint2*>(a.aux1 + p * a.a1str + a.a1off + cb);
+          l2[k][g] = *reinterpret_cast<const uint2*>(a.aux2 + p * a.a2str + a.a2off + cb);
+        } else if constexpr (E == EPI_RELU_BWD) {
+          l1[k][g] = *reinterpret_cast<const uint2*>(a.aux1 + p * a.a1str + a.a1off + cb);
+        } else if constexpr (E == EPI_ACC_F32) {
+          lf[k][g] = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out) + p * a.ostr + a.ooff + cb);
+        } else if constexpr (E == EPI_GRU_QBWD) {
+          lf[k][g] = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out) + p * a.ostr + a.ooff + cb);
+          if (lo) {
+            l1[k][g] = *reinterpret_cast<const uint2*>(a.aux1 + p * a.a1str + a.a1off + cb);
+            l2[k][g] = *reinterpret_cast<const uint2*>(a.aux2 + p * a.a2str + a.a2off + cb);
+          }
+        }
+      }
+    }
+    // ---- phase 2: arithmetic + stores
+#pragma unroll
+    for (int k = 0; k < NBC; ++k) {
+      if (n0 + k >= NB) break;
+      if (pb[n0 + k] < 0) continue;
+      const size_t p = (size_t)pp[n0 + k];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int cb = m0 + 8 * g + h4;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[n0 + k][4 * g + j] + bz[4 * g + j];
+        auto unpack = [](uint2 u, float (&f)[4]) {
+          f[0] = bf2f((bf16_t)(u.x & 0xffffu));
+          f[1] = bf2f((bf16_t)(u.x >> 16));
+          f[2] = bf2f((bf16_t)(u.y & 0xffffu));
+          f[3] = bf2f((bf16_t)(u.y >> 16));
+        };
+        if constexpr (E == EPI_GRU_ZR) {
+          float r[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = sigmoidf_(v[j]);
+          if (lo) {
+            st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, r);
+          } else {
+            const int c = cb - a.hd;
+            float hv[4], rh[4];
+            unpack(l1[k][g], hv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rh[j] = r[j] * hv[j];
+            st4(static_cast<bf16_t*>(a.out2) + p * a.o2str + a.o2off + c, rh);
+            if (a.out3) st4(static_cast<bf16_t*>(a.out3) + p * a.o3str + a.o3off + c, r);
+          }
+        } else if constexpr (E == EPI_GRU_Q) {
+          float hv[4], zv[4], q[4], nv[4];
+          unpack(l1[k][g], hv);
+          unpack(l2[k][g], zv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            q[j] = tanhf_(v[j]);
+            nv[j] = (1.f - zv[j]) * hv[j] + zv[j] * q[j];
+          }
+          st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, nv);
+          if (a.out2) st4(static_cast<bf16_t*>(a.out2) + p * a.o2str + a.o2off + cb, q);
+        } else if constexpr (E == EPI_RELU_BWD) {
+          float av[4];
+          unpack(l1[k][g], av);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = av[j] > 0.f ? v[j] : 0.f;
+          st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, v);
+        } else if constexpr (E == EPI_ACC_F32) {
+          const float4 o = lf[k][g];
+          *reinterpret_cast<float4*>(static_cast<float*>(a.out) + p * a.ostr + a.ooff + cb) =
+              make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+        } else if constexpr (E == EPI_GRU_QBWD) {
+          const float4 o = lf[k][g];
+          float* op = static_cast<float*>(a.out) + p * a.ostr + a.ooff + cb;
+          if (lo) {
+            float hv[4], rv[4], dv[4];
+            unpack(l1[k][g], hv);
+            unpack(l2[k][g], rv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dv[j] = v[j] * hv[j] * rv[j] * (1.f - rv[j]);
+            st4(static_cast<bf16_t*>(a.out2) + p * a.o2str + a.o2off + cb, dv);
+            *reinterpret_cast<float4*>(op) =
+                make_float4(o.x + v[0] * rv[0], o.y + v[1] * rv[1], o.z + v[2] * rv[2], o.w + v[3] * rv[3]);
+          } else {
+            *reinterpret_cast<float4*>(op) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+          }
+        } else {  // EPI_BIAS / EPI_RELU / EPI_SCALE
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (E == EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+            if constexpr (E == EPI_SCALE) v[j] *= a.scale;
+          }
+          st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, v);
+        }
+      }
+    }
+  }
+}
+
 template <int NB>
 __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[NB], int m0, int lane,
                                            const int (&pp)[NB], const int (&pb)[NB], const int (&py)[NB],
@@ -694,6 +823,24 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
   const bool vec =
       ((a.ooff | a.ostr | a.o2off | a.o2str | a.o3off | a.o3str | a.a1off | a.a1str | a.a2off | a.a2str) & 3) == 0 &&
       (((uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.out3 | (uintptr_t)a.aux1 | (uintptr_t)a.aux2) & 15) == 0;
+  // whole fragment inside Cout, 4-aligned epilogue tensors, GRU split on a 32-row boundary
+  const bool fast = vec && m0 + 32 <= a.Cout && (a.hd & 31) == 0;
+  if (fast) {
+    switch (a.epi) {
+#define RS_EB(E) \
+  case E: epi32_batch<NB, E>(a, acc, m0, lane, pp, pb); return
+      RS_EB(EPI_GRU_ZR);
+      RS_EB(EPI_GRU_Q);
+      RS_EB(EPI_RELU_BWD);
+      RS_EB(EPI_ACC_F32);
+      RS_EB(EPI_GRU_QBWD);
+      RS_EB(EPI_RELU);
+      RS_EB(EPI_SCALE);
+      RS_EB(EPI_BIAS);
+#undef RS_EB
+      default: break;  // EPI_FLOW: element-wise form below
+    }
+  }
   switch (a.epi) {
 #define RS_E2(E)                                                                      \
   case E:                                                                             \

@@ -32,7 +32,7 @@
 // last chunk are issued as zero-returning out-of-range loads so every slice
 // has the same compile-time VMEM count.
 #pragma once
-#define RS_V3_EXP 1  // timing-experiment tiles 70-76 (session build)
+// #define RS_V3_EXP 1  // timing-experiment tiles 70-79 (conv_v3_k15.hip)
 #include "conv_common.h"
 
 namespace rs {
@@ -223,10 +223,11 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
 #define V3_SLICE(J)                                                                            \
   if constexpr ((J) < NSL) {                                                                   \
     constexpr int sa_ = ((J) + D) % RA, sc_ = (J) % RA, fb_ = (J) & 1;                         \
-    if constexpr (EXP & 8) { V3_LDA(0, sa_); } else { V3_LDA((J) + D, sa_); }                  \
-    if constexpr (C::hcnt(J) > 0 && !(EXP & 2)) V3_ISSUE_H(cc + 1, hnxt, (J) * PPP, C::hcnt(J)); \
-    if constexpr ((J) + 1 < NSL) V3_RDB(fb_ ^ 1, dcur, (J) + 1);                               \
-    if constexpr (!(EXP & 1)) wait_vmcnt<(EXP & 2) ? D * MW : ((J) + 1 == NSL ? C::bwait() : C::nwait(J))>(); \
+    if constexpr (EXP & 16) {                                                                  \
+    } else if constexpr (EXP & 8) { V3_LDA(0, sa_); } else { V3_LDA((J) + D, sa_); }           \
+    if constexpr (C::hcnt(J) > 0 && !(EXP & 18)) V3_ISSUE_H(cc + 1, hnxt, (J) * PPP, C::hcnt(J)); \
+    if constexpr ((J) + 1 < NSL && !(EXP & 16)) V3_RDB(fb_ ^ 1, dcur, (J) + 1);                \
+    if constexpr (!(EXP & 17)) wait_vmcnt<(EXP & 2) ? D * MW : ((J) + 1 == NSL ? C::bwait() : C::nwait(J))>(); \
     V3_FENCE_A(sc_);                                                                           \
     if constexpr ((J) + 1 == NSL) {                                                            \
       if (cc + 1 < nchunks) {                                                                  \
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
   }
 #define V3_TAP(TT) V3_SLICE(4 * (TT)) V3_SLICE(4 * (TT) + 1) V3_SLICE(4 * (TT) + 2) V3_SLICE(4 * (TT) + 3)
 
-  for (int cc = 0; cc < nchunks; ++cc) {
+  for (int cc = 0; cc < ((EXP & 32) ? 0 : nchunks); ++cc) {
     const int hb = cc & 1;
     const uint32_t dcur = hb ? (uint32_t)(HSL * 16) : 0u, dnxt = hb ? 0u : (uint32_t)(HSL * 16);
     const int hnxt = hb ? 0 : HSL;  // slot base of the other halo buffer

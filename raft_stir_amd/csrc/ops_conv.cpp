@@ -201,7 +201,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 76), "conv_fused: tile must be in [0,54] or [60,64]");
+  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 79), "conv_fused: tile must be in [0,54] or [60,64]");
   const bool v3 = tile >= 60;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
   if ((tile >= 42 && tile <= 54) || v3)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),

@@ -62,7 +62,8 @@ import torch
 
 from ..ops import _ext
 from ..ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR, EPI_RELU,
-                        EPI_RELU_BWD, EPI_SCALE, conv_fused, pack_bias, pack_weight, pad_to)
+                        EPI_RELU_BWD, EPI_SCALE, conv_fused, frag_eligible, frag_weight, pack_bias, pack_weight,
+                        pad_to)
 
 R = torch.ops.raft_stir
 HD = 128          # hidden dim (full RAFT)
@@ -90,10 +91,12 @@ class _PConv:
         self.ktot = sum(c for c, _ in segs)
         self.wktot = sum(c for c, _ in self.wsegs)
 
-    def index_maps(self, pidx, fill):
+    def index_maps(self, pidx, fill, frag=False):
         """Index maps (into the flat parameter vector) of the packed forward
         weight [Cout_pad128][taps][Ktot], the bias, and the dgrad weight
-        Wd[k][tap'][co] = W[co][taps-1-tap'][k] ([pad128(Ktot)][taps][pad32(Cout)])."""
+        Wd[k][tap'][co] = W[co][taps-1-tap'][k] ([pad128(Ktot)][taps][pad32(Cout)]);
+        with ``frag`` also the fragment-major copies of both (ops/conv.py
+        frag_weight; None where the weight-streaming tiles cannot serve them)."""
         weight = torch.cat([pidx[id(c.weight)] for c in self.convs], 0)
         bias = torch.cat([pidx[id(c.bias)] for c in self.convs], 0)
         cout, cin, kh, kw = weight.shape
@@ -109,7 +112,9 @@ class _PConv:
         wd = torch.full((pad_to(self.ktot, 128), taps, cy), fill, dtype=torch.long)
         wd[:self.ktot] = w[:cy].flip(1).permute(2, 1, 0)
         self.cy = cy
-        return w, bias, wd
+        wf = frag_weight(w) if frag and frag_eligible(w, kh, kw) else None
+        wdf = frag_weight(wd) if frag and frag_eligible(wd, kh, kw) else None
+        return w, bias, wd, wf, wdf
 
     def grad_maps(self, gidx):
         """Per original conv (weight, bias) index maps into the packed gradient
@@ -222,9 +227,10 @@ class FusedTrainEngine:
         bf_maps, f32_maps, layout = [], [], []
         nbf = 0
         for pc in self.convs:
-            w, b, wd = pc.index_maps(pidx, fill)
-            layout.append((pc, w.shape, wd.shape, b.shape))
+            w, b, wd, wf, wdf = pc.index_maps(pidx, fill, frag=not self.f32)
+            layout.append((pc, w.shape, wd.shape, b.shape, wf is not None, wdf is not None))
             bf_maps += [w.reshape(-1), wd.reshape(-1)]
+            bf_maps += [x.reshape(-1) for x in (wf, wdf) if x is not None]
             f32_maps.append(b.reshape(-1))
         f1w = pidx[id(self.f1.weight)].permute(2, 3, 1, 0).contiguous()  # [7][7][2][f1c]
         f32_maps += [f1w.reshape(-1), pidx[id(self.f1.bias)].reshape(-1)]
@@ -235,11 +241,15 @@ class FusedTrainEngine:
         gather = torch.cat(bf_maps + f32_maps)
         # scale (mask x 0.25) folded into the dgrad weights: element range in the bf16 region
         o, scaled = 0, []
-        for pc, ws, wds, bs in layout:
+        for pc, ws, wds, bs, hf, hdf in layout:
             o += ws.numel()
             if pc.scale != 1.0:
                 scaled.append((o, o + wds.numel(), pc.scale))
             o += wds.numel()
+            o += ws.numel() if hf else 0
+            if hdf and pc.scale != 1.0:
+                scaled.append((o, o + wds.numel(), pc.scale))
+            o += wds.numel() if hdf else 0
         # gradient buffer: per conv dW [Cout_pad128][taps][Ktot] + db [Cout], then flow-conv dW, db
         glayout, go = [], 0
         for pc in self.convs:
@@ -325,13 +335,24 @@ class FusedTrainEngine:
             bf = torch.cat([hi, (v32 - hi.float()).to(torch.bfloat16)], 1).view(-1)
             k = 2
         ob, of = 0, nbf
-        for pc, ws, wds, bs in M["layout"]:
+        for pc, ws, wds, bs, hf, hdf in M["layout"]:
             n = ws.numel()
             pc.w = bf[k * ob:k * (ob + n)].view(ws[0], ws[1], k * ws[2])
             ob += n
             n = wds.numel()
             pc.wd = bf[k * ob:k * (ob + n)].view(wds[0], wds[1], k * wds[2])
             ob += n
+            # fragment-major copies (bf16 engine): conv_fused finds them through
+            # the packed weight's _rs_frag attribute when a tile 60-64 is chosen
+            pc.wf = pc.wdf = None
+            if hf:
+                pc.wf = bf[ob:ob + ws.numel()].view(ws)
+                ob += ws.numel()
+                pc.w._rs_frag = pc.wf
+            if hdf:
+                pc.wdf = bf[ob:ob + wds.numel()].view(wds)
+                ob += wds.numel()
+                pc.wd._rs_frag = pc.wdf
             pc.b = vals[of:of + bs.numel()]
             of += bs.numel()
         fc = self.f1c

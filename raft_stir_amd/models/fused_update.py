@@ -48,7 +48,7 @@ import torch.nn.functional as F
 
 from ..ops import _ext
 from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, choose_tile_f32, conv_fused,
-                        pack_bias, pack_weight, pack_weight_split, pad_to)
+                        frag_eligible, frag_weight, pack_bias, pack_weight, pack_weight_split, pad_to)
 
 _F32_ENGINE = os.environ.get("RS_F32_ENGINE", "1") != "0"
 from ..ops.upsample import convex_upsample
@@ -66,6 +66,17 @@ class _Conv:
         pack = pack_weight_split if f32 else pack_weight
         self.w = pack(weight, segs, pad_to(self.cout, 128))
         self.b = pack_bias(bias)
+        # fragment-major copy for the weight-streaming tiles (bf16 3x3 / 1x5 / 5x1 only)
+        self.wf = frag_weight(self.w) if not f32 and frag_eligible(self.w, self.kh, self.kw) else None
+
+
+def _copy_conv(prev: "_Conv", new: "_Conv"):
+    prev.w.copy_(new.w)
+    prev.b.copy_(new.b)
+    if prev.wf is not None and new.wf is not None:
+        prev.wf.copy_(new.wf)
+    else:
+        prev.wf = new.wf
 
 
 class FusedUpdate:
@@ -154,14 +165,12 @@ class FusedUpdate:
         for name, new in list(self.__dict__.items()):
             prev = old.get(name)
             if isinstance(new, _Conv) and isinstance(prev, _Conv) and prev.w.shape == new.w.shape:
-                prev.w.copy_(new.w)
-                prev.b.copy_(new.b)
+                _copy_conv(prev, new)
                 self.__dict__[name] = prev
             elif name == "gru" and isinstance(prev, list) and len(prev) == len(new):
                 for (pz, pq), (nz, nq) in zip(prev, new):
                     for p_, n_ in ((pz, nz), (pq, nq)):
-                        p_.w.copy_(n_.w)
-                        p_.b.copy_(n_.b)
+                        _copy_conv(p_, n_)
                 self.gru = prev
             elif name in ("f1_w", "f1_b", "flow_w32", "flow_b32") and isinstance(prev, torch.Tensor) and prev.shape == new.shape:
                 prev.copy_(new)
@@ -227,7 +236,7 @@ class FusedUpdate:
                 with torch.cuda.stream(side):
                     torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
                     cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
-                               bufs["mot"], 192)
+                               bufs["mot"], 192, wf=self.convf2.wf)
             if st is not None:
                 torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
             else:  # memory-efficient path: correlate the pooled fmap2 pyramid on the fly
@@ -241,33 +250,33 @@ class FusedUpdate:
                 cf([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
                            bufs["mot"], 0)
                 cf([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
-                           bufs["mot"], 96)
+                           bufs["mot"], 96, wf=self.convf2.wf)
                 cf([(bufs["mot"], 0, 128)], self.conv.w, self.conv.b, 3, 3, 80, EPI_RELU,
-                           hx, self.off_mot)
+                           hx, self.off_mot, wf=self.conv.wf)
             else:
                 cf([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 256, EPI_RELU,
                            bufs["c1"], 0)
                 cf([(bufs["c1"], 0, 256)], self.convc2.w, self.convc2.b, 3, 3, 192, EPI_RELU,
-                           bufs["mot"], 0)
+                           bufs["mot"], 0, wf=self.convc2.wf)
                 if side is None:
                     cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
-                               bufs["mot"], 192)
+                               bufs["mot"], 192, wf=self.convf2.wf)
                 else:
                     main.wait_stream(side)
                 cf([(bufs["mot"], 0, 256)], self.conv.w, self.conv.b, 3, 3, 126, EPI_RELU,
-                           hx, self.off_mot)
+                           hx, self.off_mot, wf=self.conv.wf)
             for zr, q in self.gru:
                 rhc = bufs["rh"].shape[-1]
                 cf([(hx, 0, self.hx_c)], zr.w, zr.b, zr.kh, zr.kw, 2 * hd, EPI_GRU_ZR,
-                           bufs["z"], 0, hd=hd, out2=bufs["rh"], o2off=0, aux1=hx, a1off=0)
+                           bufs["z"], 0, hd=hd, out2=bufs["rh"], o2off=0, aux1=hx, a1off=0, wf=zr.wf)
                 cf([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
-                           EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0)
+                           EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0, wf=q.wf)
             if small:
-                cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0)
+                cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0, wf=self.head.wf)
                 torch.ops.raft_stir.flow_head(bufs["head"], 0, 128, self.flow_w32, self.flow_b32, coords1, None)
             else:
                 cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
-                           bufs["head"], 0)
+                           bufs["head"], 0, wf=self.head.wf)
                 torch.ops.raft_stir.flow_head(bufs["head"], 0, 256, self.flow_w32, self.flow_b32, coords1, None)
             if not want_up:
                 continue

@@ -181,19 +181,28 @@ def tuned_tiles_f32() -> dict:
     return _TUNED_F32
 
 
+def frag_eligible(w: torch.Tensor, kh: int, kw: int) -> bool:
+    """Can the weight-streaming tiles 60-64 serve this packed weight?"""
+    return kh * kw in (5, 9) and w.dim() == 3 and w.shape[0] % 32 == 0 and w.shape[2] % 64 == 0
+
+
 def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout, epi, out, ooff=0,
                scale=1.0, hd=0, out2=None, o2off=0, out3=None, o3off=0, aux1=None, a1off=0,
-               aux2=None, a2off=0, tile=None, nscale=None):
+               aux2=None, a2off=0, tile=None, nscale=None, wf=None):
     """segs: list of (NHWC bf16 buffer, channel offset, channels read).
     ``nscale`` with ``epi=EPI_NORM``: out = [relu if hd](acc * nscale + bias)
-    [then relu(. + aux1)]."""
+    [then relu(. + aux1)].  ``wf``: the same weight in the fragment-major
+    layout (:func:`frag_weight`), which the weight-streaming tiles 60-64 read;
+    without it those tiles are not chosen."""
+    if wf is None:  # the training engine tags its packed weights with their fragment-major copy
+        wf = getattr(w, "_rs_frag", None)
     tensors = [s[0] for s in segs]
     offs = [int(s[1]) for s in segs]
     chans = [int(s[2]) for s in segs]
     if _RECORD is not None:
         _RECORD.append(dict(segs=segs, w=w, bias=bias, kh=kh, kw=kw, cout=cout, epi=epi, out=out, ooff=ooff,
                             scale=scale, hd=hd, out2=out2, o2off=o2off, out3=out3, o3off=o3off, aux1=aux1,
-                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, nscale=nscale))
+                            a1off=a1off, aux2=aux2, a2off=a2off, tile=tile, nscale=nscale, wf=wf))
     if tile is None:
         t0 = tensors[0]
         key = tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi)
@@ -202,8 +211,12 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
             tile = tuned_tiles_f32().get(key) or choose_tile_f32(P, cout)
         else:
             tile = tuned_tiles().get(key)
-            if tile is None:
+            if tile is None or (tile in V3_TILES and wf is None):
                 tile = choose_tile(P, cout, chans, kh * kw)
+    if tile in V3_TILES:
+        if wf is None:
+            raise ValueError("conv_fused: tiles 60-64 read the fragment-major weight: pass wf=frag_weight(w)")
+        w = wf
     if nscale is None:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

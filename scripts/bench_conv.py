@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of one hipGraph")
+    ap.add_argument("--ksweep", type=int, nargs="*", default=None,
+                    help="instead of SHAPES: a 1x5 conv to 256 channels for each of these input widths")
     ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5],
                     help="wgrad tile variants (csrc/conv_wgrad.hip wgrad_launch)")
     a = ap.parse_args()
@@ -93,7 +95,8 @@ def main():
     B, (H, W) = a.batch, a.hw
     P = B * H * W
     tot = {}
-    for name, cin, cout, kh, kw in SHAPES:
+    shapes = SHAPES if a.ksweep is None else [(f"k{c}", c, 256, 1, 5) for c in a.ksweep]
+    for name, cin, cout, kh, kw in shapes:
         if (a.only and name not in a.only) or not a.tiles:
             continue
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
@@ -111,9 +114,9 @@ def main():
                 continue
             if t in V3_TILES and kh * kw not in (5, 9):
                 continue
-            wt = wf if t in V3_TILES else wp
             try:
-                us = timeit(lambda: conv_fused([(x, 0, cin)], wt, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t), a.reps)
+                us = timeit(lambda: conv_fused([(x, 0, cin)], wp, bp, kh, kw, cout, EPI_RELU, out, 0, tile=t, wf=wf),
+                            a.reps)
             except RuntimeError as e:  # tile constraint (e.g. kernel too large for a halo tile)
                 line += f" tile{t} n/a |"
                 continue

@@ -105,9 +105,10 @@ def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
     for c in chans:
         pieces.append((c, [(o, c, 0)]))
         o += c
-    wp = frag_weight(pack_weight(w, pieces, pad_to(cout, 32)))
+    wp = pack_weight(w, pieces, pad_to(cout, 32))
     out = torch.full((B, H, W, cout + 8), 7.0, device=cuda, dtype=torch.bfloat16)
-    conv_fused([(s, 0, s.shape[-1]) for s in segs], wp, pack_bias(b), kh, kw, cout, EPI_RELU, out, 0, tile=tile)
+    conv_fused([(s, 0, s.shape[-1]) for s in segs], wp, pack_bias(b), kh, kw, cout, EPI_RELU, out, 0, tile=tile,
+               wf=frag_weight(wp))
     x = torch.cat(segs, -1).float().permute(0, 3, 1, 2)
     ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2)).relu()
     got = out[..., :cout].float().permute(0, 3, 1, 2)
@@ -133,7 +134,7 @@ def test_conv_v3_epilogues_match_v2(cuda, epi):
     aux2 = torch.rand(B, H, W, 256, device=cuda).to(torch.bfloat16)
     f32out = epi in (EPI_ACC_F32, EPI_GRU_QBWD)
     outs = []
-    for tile, wt in ((52, wp), (60, wf)):
+    for tile in (52, 60):
         torch.manual_seed(7)
         out = torch.randn(B, H, W, 256, device=cuda)
         out = out if f32out else out.to(torch.bfloat16)
@@ -149,7 +150,7 @@ def test_conv_v3_epilogues_match_v2(cuda, epi):
         elif epi == EPI_GRU_QBWD:
             kw_.update(hd=hd, out2=out2, aux1=aux1, aux2=aux2)
         bias = None if epi in (EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD) else pack_bias(b)
-        conv_fused([(s, 0, 128) for s in segs], wt, bias, 1, 5, cout, epi, out, 0, **kw_)
+        conv_fused([(s, 0, 128) for s in segs], wp, bias, 1, 5, cout, epi, out, 0, wf=wf, **kw_)
         outs.append((out.float(), out2.float(), out3.float()))
     for x, y in zip(*outs):
         torch.testing.assert_close(y, x, atol=2e-2, rtol=2e-2)
