@@ -867,6 +867,6 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
 
 // conv_v2.hip: tiles 42-45 (3x3 / 1x5 / 5x1 only); false if the kernel size is not instantiated
 bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream);
-// conv_v3.hip: tiles 60-64 (3x3 / 1x5 / 5x1; weights in the fragment-major layout, ops/conv.py frag_weight)
+// conv_v3.hip: tiles 60-65 (3x3 / 1x5 / 5x1; weights in the fragment-major layout, ops/conv.py frag_weight)
 bool conv_v3_launch(const conv::Args& a, int tile, hipStream_t stream);
 }  // namespace rs

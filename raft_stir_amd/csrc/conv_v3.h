@@ -295,6 +295,7 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
     case 62: *nwm = 4; *mw = 2; *th = 6; return true;
     case 63: *nwm = 2; *mw = 1; *th = 6; return true;
     case 64: *nwm = 3; *mw = 1; *th = 6; return true;
+    case 65: *nwm = 2; *mw = 1; *th = 3; return true;
     default: return false;
   }
 }
@@ -312,6 +313,7 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
       case 61: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 3, R1>), grid, block, 0, stream, a); break; \
       case 62: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 2, 6, R2>), grid, block, 0, stream, a); break; \
       case 63: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 6, R1>), grid, block, 0, stream, a); break; \
+      case 65: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1>), grid, block, 0, stream, a); break; \
       default: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 3, 1, 6, R1>), grid, block, 0, stream, a); break; \
     }                                                                                              \
     return true;                                                                                   \

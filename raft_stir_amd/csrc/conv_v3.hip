@@ -1,4 +1,4 @@
-// Dispatch of the weight-streaming conv tiles 60-64 (conv_v3.h) by kernel shape.
+// Dispatch of the weight-streaming conv tiles 60-65 (conv_v3.h) by kernel shape.
 #include "conv_v3.h"
 
 namespace rs {

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, pack_weight, pad_to
+from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -60,6 +60,47 @@ def _halo_ok(cin: int, cout: int) -> bool:
     if cin == 64:
         return cout % 64 == 0
     return cin == 96 and cout % 32 == 0
+
+
+# csrc/conv_v3.h weight-streaming tiles for the encoder 3x3 convs where they
+# measured faster than the halo / implicit-GEMM kernels (scripts/bench_enc_v3.py,
+# profiles/r5/README.md: forward 360 -> 280 us over the six fnet / cnet shapes;
+# the 1/2-res 64 -> 64 conv of fnet's 16 images stays on csrc/enc_halo.hip).
+# 96 channels are read as two overlapping 64-channel windows, [0, 64) and
+# [32, 96), with zero weights on the duplicated half.
+_V3 = os.environ.get("RS_ENC_V3", "1") != "0"
+
+
+def _v3_tile(P: int, cin: int, cout: int):
+    if not _V3 or cin % 32 or cin < 64 or cout % 32:
+        return None
+    if cin == 64 and cout == 64 and P >= 600000:
+        return None
+    return 65 if cout <= 64 else 61
+
+
+def _v3_windows(cin: int):
+    """(channel windows of the input, pack_weight segment spec) for the v3 tiles."""
+    if cin % 64 == 0:
+        return [(0, cin)], [(cin, [(0, cin, 0)])]
+    return [(0, 64), (cin - 64, 64)], [(64, [(0, 64, 0)]), (64, [(64, cin - 64, 128 - cin)])]
+
+
+def _v3_weight(weight: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    cout, cin = weight.shape[:2]
+    k_in, k_out = (cout, cin) if dgrad else (cin, cout)
+    _, wsegs = _v3_windows(k_in)
+
+    def layout(ws):
+        w = ws[0].transpose(0, 1).flip(2, 3) if dgrad else ws[0]
+        return frag_weight(pack_weight(w, wsegs, pad_to(k_out, 128), _F32))
+    return wpack.packed(("v3", id(weight), dgrad), [weight], layout)
+
+
+def _conv3x3_v3(xn, weight, k_in, k_out, out, tile, dgrad):
+    wins, _ = _v3_windows(k_in)
+    wf = _v3_weight(weight, dgrad)
+    conv_fused([(xn, o, c) for o, c in wins], wf, None, 3, 3, k_out, EPI_BIAS, out, 0, tile=tile, wf=wf)
 
 
 def _conv3x3_into(xn, wp, cin, cout, out, P):
@@ -193,11 +234,15 @@ class _Conv3x3(torch.autograd.Function):
         N, H, W, cin = xn.shape
         cout = weight.shape[0]
         P = N * H * W
-        wp = _packed(weight, False)
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.bfloat16)
-        _conv3x3_into(xn, wp, cin, cout, out, P)
+        t = _v3_tile(P, cin, cout)
+        if t is not None:
+            _conv3x3_v3(xn, weight, cin, cout, out, t, False)
+        else:
+            _conv3x3_into(xn, _packed(weight, False), cin, cout, out, P)
         ctx.save_for_backward(x)
-        ctx.sink = sink if sink is not None and _halo_ok(cout, cin) else None
+        # the skip gradient is added in the halo kernel's dgrad epilogue only
+        ctx.sink = sink if sink is not None and _halo_ok(cout, cin) and _v3_tile(P, cout, cin) is None else None
         if ctx.sink is not None:
             ctx.sink.armed = True
         return out.permute(0, 3, 1, 2)
@@ -213,15 +258,18 @@ class _Conv3x3(torch.autograd.Function):
         dyn = _nhwc(dy.to(torch.bfloat16))
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            wd = _packed(weight, True)
             sink = ctx.sink
+            td = _v3_tile(P, cout, cin)
             if sink is not None and sink.dres is not None:
                 # dX = skip gradient + dgrad, accumulated in the halo kernel's epilogue
                 dxn, sink.dres = sink.dres, None
-                torch.ops.raft_stir.conv3x3_halo(dyn, wd, dxn, cout, cin, accumulate=True)
+                torch.ops.raft_stir.conv3x3_halo(dyn, _packed(weight, True), dxn, cout, cin, accumulate=True)
             else:
                 dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
-                _conv3x3_into(dyn, wd, cout, cin, dxn, P)
+                if td is not None:
+                    _conv3x3_v3(dyn, weight, cout, cin, dxn, td, True)
+                else:
+                    _conv3x3_into(dyn, _packed(weight, True), cout, cin, dxn, P)
             dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dw, = _wgrad_on(ctx.wstream, lambda: (_wgrad3x3(dyn, x, xn, weight, cin, cout, P),), [dyn, x])
