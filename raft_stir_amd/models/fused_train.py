@@ -58,6 +58,8 @@ from __future__ import annotations
 
 import contextlib
 
+import os
+
 import torch
 
 from ..ops import _ext
@@ -466,15 +468,31 @@ def _split_bf16(t: torch.Tensor):
     return hi, (t - hi.float()).to(torch.bfloat16)
 
 
+# csrc/wgrad_v3.hip (all taps per block, split-K partials reduced in order) for
+# the 3x3 / 1x5 / 5x1 convs with more than 64 outputs; measured at the
+# training shape (scripts/bench_conv.py --wgrad 12 --v3wgrad,
+# profiles/r5/README.md): GRU z|r 400 -> 302 us, q 217 -> 171, head 475 -> 348,
+# convc2 449 -> 387; the 64-output convf2 stays on conv_wgrad.hip (107 us).
+_WG3 = os.environ.get("RS_WGRAD_V3", "1") != "0"
+
+
+def _wgrad_fn(pc, segs, bn128):
+    if (_WG3 and pc.kh * pc.kw in (5, 9) and pc.cout > 64 and all(int(s[2]) % 64 == 0 for s in segs)):
+        bm = 128 if pc.cout >= 512 else 64
+        return lambda *a: R.wgrad_v3(*a, bm)
+    return lambda *a: R.conv_wgrad(*a, bn128)
+
+
 def _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128=0):
     """``pc.dw += dY^T X`` (+ ``pc.db += colsum dY``) over every iteration's
     pixels on csrc/conv_wgrad.hip.  fp32 engine: the bf16 GEMM on the split
     operands, dYh.Xh + dYl.Xh + dYh.Xl (the bias sums of the first two give
     colsum(dYh + dYl))."""
     per = [s[0].shape[0] * H * W for s in segs]
+    wg = _wgrad_fn(pc, segs, bn128)
     if not eng.f32:
-        R.conv_wgrad(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
-                     per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
+        wg(dy, yoff, pc.cout, [s[0] for s in segs], [s[1] for s in segs], [s[2] for s in segs],
+           per, pc.kh, pc.kw, pc.dw, pc.db)
         return
     cache = eng.__dict__.setdefault("_split_cache", {})
     def split(t):
@@ -486,9 +504,9 @@ def _conv_wgrad(eng, pc, dy, yoff, segs, H, W, bn128=0):
     dyh, dyl = split(dy)
     xs = [split(s[0]) for s in segs]
     offs, chans = [s[1] for s in segs], [s[2] for s in segs]
-    R.conv_wgrad(dyh, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
-    R.conv_wgrad(dyl, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db, bn128)
-    R.conv_wgrad(dyh, yoff, pc.cout, [x[1] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, None, bn128)
+    wg(dyh, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db)
+    wg(dyl, yoff, pc.cout, [x[0] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, pc.db)
+    wg(dyh, yoff, pc.cout, [x[1] for x in xs], offs, chans, per, pc.kh, pc.kw, pc.dw, None)
 
 
 class DeferGrads(torch.autograd.Function):

@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--gemm", action="store_true", help="also time the plain GEMM of the same M/N/K (hipBLASLt)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches instead of one hipGraph")
+    ap.add_argument("--v3wgrad", action="store_true", help="also time csrc/wgrad_v3.hip (64 / 128 rows per block)")
     ap.add_argument("--ksweep", type=int, nargs="*", default=None,
                     help="instead of SHAPES: a 1x5 conv to 256 channels for each of these input widths")
     ap.add_argument("--wvars", type=int, nargs="+", default=[0, 1, 2, 3, 4, 5],
@@ -153,6 +154,15 @@ def main():
             flop = 2.0 * n * H * W * cout * cin * kh * kw
             line = f"wgrad {name:8s} K(px)={n * H * W:7d} M={cout:4d} N={cin * kh * kw:5d} |"
             ref = None
+            if a.v3wgrad and kh * kw in (5, 9):
+                for bm in (64, 128):
+                    dw.zero_(); db.zero_()
+                    torch.ops.raft_stir.wgrad_v3(dy, 0, cout, [x], [0], [cin], [n * H * W], kh, kw, dw, db, bm)
+                    got = torch.cat([dw[:cout].flatten(), db[:cout]])
+                    us = timeit(lambda: torch.ops.raft_stir.wgrad_v3(dy, 0, cout, [x], [0], [cin], [n * H * W], kh,
+                                                                      kw, dw, db, bm), max(5, a.reps // 5))
+                    line += f" v3/{bm} {us:8.1f}us {flop / us / 1e6:6.1f}TF |"
+                    ref = got.clone() if ref is None else ref
             for v in a.wvars:
                 def run():
                     dw.zero_(); db.zero_()

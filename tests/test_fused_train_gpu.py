@@ -70,6 +70,41 @@ def test_wgrad_tile_variants(cuda, var, cout, k):
     torch.testing.assert_close(db, dy[..., :cout].float().sum((0, 1, 2)), atol=5e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("bm", [64, 128])
+@pytest.mark.parametrize("cout,k", [(70, (3, 3)), (200, (1, 5)), (126, (5, 1)), (64, (3, 3))])
+@pytest.mark.parametrize("shape", [(3, 2, 11, 13), (2, 2, 46, 62)])
+def test_wgrad_v3(cuda, bm, cout, k, shape):
+    """csrc/wgrad_v3.hip (all taps per block, TH x 32-pixel patches, split-K
+    partials reduced in order) vs fp32 PyTorch: three segments (one broadcast
+    over the iterations), a dY channel window at an offset, ragged Cout against
+    the block's rows, partial patches in both directions, accumulation into dW
+    and db, the fused bias gradient."""
+    torch.manual_seed(bm + cout)
+    iters, B, H, W = shape
+    kh, kw = k
+    xa = torch.randn(iters * B, H, W, 128, device=cuda).to(torch.bfloat16)
+    xb = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)            # broadcast over iterations
+    xc = torch.randn(iters * B, H, W, 192, device=cuda).to(torch.bfloat16)   # window [64, 192)
+    dy = torch.randn(iters * B, H, W, pad_to(cout, 8) + 16, device=cuda).to(torch.bfloat16)
+    dw0 = torch.randn(cout, kh * kw, 256, device=cuda)
+    db0 = torch.randn(cout, device=cuda)
+    dw, db = dw0.clone(), db0.clone()
+    torch.ops.raft_stir.wgrad_v3(dy, 8, cout, [xa, xb, xc], [0, 0, 64], [64, 64, 128],
+                                 [iters * B * H * W, B * H * W, iters * B * H * W], kh, kw, dw, db, bm)
+    x = torch.cat([xa[..., :64], xb.repeat(iters, 1, 1, 1), xc[..., 64:]], -1).float().permute(0, 3, 1, 2)
+    w = torch.zeros(cout, 256, kh, kw, device=cuda, requires_grad=True)
+    g = dy[..., 8:8 + cout].float().permute(0, 3, 1, 2)
+    F.conv2d(x, w, padding=(kh // 2, kw // 2)).backward(g)
+    want = w.grad.permute(0, 2, 3, 1).reshape(cout, kh * kw, 256)
+    torch.testing.assert_close(dw - dw0, want, atol=5e-2, rtol=1e-2)
+    torch.testing.assert_close(db - db0, g.sum((0, 2, 3)), atol=5e-2, rtol=1e-3)
+    # bitwise repeatable (ordered split reduction, no atomics)
+    dw2 = dw0.clone()
+    torch.ops.raft_stir.wgrad_v3(dy, 8, cout, [xa, xb, xc], [0, 0, 64], [64, 64, 128],
+                                 [iters * B * H * W, B * H * W, iters * B * H * W], kh, kw, dw2, None, bm)
+    assert torch.equal(dw2, dw)
+
+
 def test_flow_wgrad(cuda):
     torch.manual_seed(1)
     n, H, W = 4, 10, 13
