@@ -32,7 +32,6 @@
 // last chunk are issued as zero-returning out-of-range loads so every slice
 // has the same compile-time VMEM count.
 #pragma once
-// #define RS_V3_EXP 1  // timing-experiment tiles 70-79 (conv_v3_k15.hip)
 #include "conv_common.h"
 
 namespace rs {
@@ -51,16 +50,17 @@ __device__ __forceinline__ i32x4_t raw_rsrc(const void* p, unsigned bytes) {
   return r;
 }
 
-template <int KH, int KW, int NWM, int MW, int TH, int RA>
+template <int KH, int KW, int NWM, int MW, int THW, int RA, int NWP>
 struct V3 {
   static constexpr int T = KH * KW, NSL = 4 * T, D = RA - 1;
-  static constexpr int NT = 64 * NWM, BM = 32 * MW * NWM, TW = 32;
+  static constexpr int TH = THW * NWP, NW = NWM * NWP;  // patch rows; waves (Cout x pixel rows)
+  static constexpr int NT = 64 * NW, BM = 32 * MW * NWM, TW = 32;
   static constexpr int HH = TH + KH - 1, HWD = TW + KW - 1;
   static constexpr int PPR = (HWD * 9 + 63) / 64;   // DMA pieces (1 KB) per halo row
   static constexpr int ROWSL = PPR * 64;            // 16-B slots per halo row
   static constexpr int NHP = HH * PPR;               // halo pieces per chunk
-  static constexpr int NHPW = (NHP + NWM - 1) / NWM; // ... per wave (the last may be padding)
-  static constexpr int HSL = NHPW * NWM * 64;        // slots per halo buffer
+  static constexpr int NHPW = (NHP + NW - 1) / NW;   // ... per wave (the last may be padding)
+  static constexpr int HSL = NHPW * NW * 64;         // slots per halo buffer
   // halo pieces go at slice positions [0, LASTP): early enough that waiting
   // for the chunk's last A slice retires them, or (deep rings) all at position 0
   static constexpr int LASTP = NSL > RA ? NSL - RA : 1;
@@ -95,9 +95,12 @@ struct V3 {
   }
 };
 
-template <int KH, int KW, int NWM, int MW, int TH, int RA, int EXP = 0>
-__global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
-  using C = V3<KH, KW, NWM, MW, TH, RA>;
+// EXP: timing-experiment bits (profiles/r5/conv_v3_experiments_s3.log): 1 no A wait, 2 no halo
+// refill, 4 no chunk barrier, 8 every A load from slice 0, 16 MFMAs only, 32 no main loop
+template <int KH, int KW, int NWM, int MW, int THW, int RA, int NWP = 1, int EXP = 0>
+__global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
+  using C = V3<KH, KW, NWM, MW, THW, RA, NWP>;
+  constexpr int TH = C::TH, NW = C::NW;
   constexpr int T = C::T, NSL = C::NSL, D = C::D, BM = C::BM;
   constexpr int HWD = C::HWD, PPR = C::PPR, NHP = C::NHP, NHPW = C::NHPW, HSL = C::HSL;
   constexpr int ROWSL = C::ROWSL, PPP = C::PPP;
@@ -111,6 +114,7 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
 
   const int t_ = threadIdx.x, lane = t_ & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t_ >> 6);
+  const int cw = wave % NWM, pw = wave / NWM;  // output-channel slice, patch-row group of this wave
   const int H = a.H, W = a.W;
   const int ntx = cdiv(W, 32), npb = cdiv(H, TH) * ntx;
   const int nct = cdiv(a.Cout, BM);
@@ -133,13 +137,13 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
   const i32x4_t rsA = raw_rsrc(a.w, a.w_bytes);
   int vA[MW];
 #pragma unroll
-  for (int mw = 0; mw < MW; ++mw) vA[mw] = ((bm0 >> 5) + wave * MW + mw) * NS * 1024 + lane * 16;
+  for (int mw = 0; mw < MW; ++mw) vA[mw] = ((bm0 >> 5) + cw * MW + mw) * NS * 1024 + lane * 16;
 
-  // ---- halo: piece q of this wave = slots g*64 .. +63 of a halo buffer, g = wave + NWM q
+  // ---- halo: piece q of this wave = slots g*64 .. +63 of a halo buffer, g = wave + NW q
   int hpix[NHPW], hch[NHPW];
 #pragma unroll
   for (int q = 0; q < NHPW; ++q) {
-    const int g = wave + NWM * q;
+    const int g = wave + NW * q;
     const int hr = g / PPR, sr = (g - hr * PPR) * 64 + lane;
     const int hc = sr / 9, ch = sr - hc * 9;
     hpix[q] = -1;
@@ -163,27 +167,27 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
         si_ == 0 ? sb0 : (si_ == 1 ? sb1 : sb2), 0x00020000);                                  \
     _Pragma("unroll") for (int q = (Q0); q < (Q0) + (NQ); ++q) {                               \
       const int v_ = (live_ && hpix[q] >= 0) ? (hpix[q] * sst_ + hch[q]) * 2 : kFar;           \
-      bdma16(rb_, lds + (HBASE) + wbase + NWM * 64 * q, v_, c0_ * 2);                          \
+      bdma16(rb_, lds + (HBASE) + wbase + NW * 64 * q, v_, c0_ * 2);                            \
     }                                                                                          \
   } while (0)
 
   // ---- B fragment read bases (bytes, LDS): halo buffer 0, patch row nb, column l32, chunk h
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)&lds[0];
   const int h = lane >> 5, l32 = lane & 31;
-  uint32_t bro[TH];
+  uint32_t bro[THW];
 #pragma unroll
-  for (int nb = 0; nb < TH; ++nb) bro[nb] = lds0 + (uint32_t)((nb * ROWSL + l32 * 9 + h) * 16);
+  for (int nb = 0; nb < THW; ++nb) bro[nb] = lds0 + (uint32_t)(((pw * THW + nb) * ROWSL + l32 * 9 + h) * 16);
 
-  f32x16_t acc[MW][TH];
+  f32x16_t acc[MW][THW];
 #pragma unroll
   for (int mw = 0; mw < MW; ++mw)
 #pragma unroll
-    for (int nb = 0; nb < TH; ++nb)
+    for (int nb = 0; nb < THW; ++nb)
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[mw][nb][j] = 0.f;
 
   u32x4_t Ar[RA][MW];
-  u32x4_t Bf[2][TH];
+  u32x4_t Bf[2][THW];
 
   // A fragments of slice (chunk base + SREL) into ring slot SL (vAc: chunk base offsets)
 #define V3_LDA(SREL, SL)                                                                       \
@@ -197,14 +201,14 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
   do {                                                                                         \
     constexpr int tp_ = (J) / 4, ks_ = (J) % 4;                                                \
     constexpr int toff_ = ((tp_ / KW) * ROWSL + (tp_ % KW) * 9 + 2 * ks_) * 16;                \
-    _Pragma("unroll") for (int nb = 0; nb < TH; ++nb)                                          \
+    _Pragma("unroll") for (int nb = 0; nb < THW; ++nb)                                          \
       asm volatile("ds_read_b128 %0, %1 offset:%2"                                             \
                    : "=v"(Bf[FB][nb]) : "v"(bro[nb] + (DB)), "i"(toff_) : "memory");           \
   } while (0)
 #define V3_FENCE_A(SL)                                                                         \
   _Pragma("unroll") for (int mw = 0; mw < MW; ++mw) asm volatile("" : "+v"(Ar[SL][mw]))
 #define V3_FENCE_B(FB)                                                                         \
-  _Pragma("unroll") for (int nb = 0; nb < TH; ++nb) asm volatile("" : "+v"(Bf[FB][nb]))
+  _Pragma("unroll") for (int nb = 0; nb < THW; ++nb) asm volatile("" : "+v"(Bf[FB][nb]))
 
   // ---- prologue: chunk-0 halo into buffer 0, A slices 0 .. D-1
   int vAc[MW];
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
       }                                                                                        \
     }                                                                                          \
     __builtin_amdgcn_sched_barrier(0);                                                         \
-    _Pragma("unroll") for (int nb = 0; nb < TH; ++nb)                                          \
+    _Pragma("unroll") for (int nb = 0; nb < THW; ++nb)                                          \
       _Pragma("unroll") for (int mw = 0; mw < MW; ++mw)                                        \
         acc[mw][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                                 \
             __builtin_bit_cast(bf16x8_t, Ar[sc_][mw]), __builtin_bit_cast(bf16x8_t, Bf[fb_][nb]), \
@@ -267,10 +271,10 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
   wait_vmcnt<0>();
 
   // ---- epilogue: n-block nb = patch row nb, column l32
-  int pp[TH], pb[TH], py[TH], px[TH];
+  int pp[THW], pb[THW], py[THW], px[THW];
 #pragma unroll
-  for (int nb = 0; nb < TH; ++nb) {
-    const int y = y0 + nb, x = x0 + l32;
+  for (int nb = 0; nb < THW; ++nb) {
+    const int y = y0 + pw * THW + nb, x = x0 + l32;
     if (y < H && x < W) {
       pb[nb] = img;
       py[nb] = y;
@@ -281,21 +285,25 @@ __global__ __launch_bounds__(64 * NWM) void conv_v3_kernel(Args a) {
       py[nb] = px[nb] = pp[nb] = 0;
     }
   }
-  epilogue32<TH>(a, acc[0], bm0 + wave * MW * 32, lane, pp, pb, py, px);
-  if constexpr (MW > 1) epilogue32<TH>(a, acc[1], bm0 + (wave * MW + 1) * 32, lane, pp, pb, py, px);
+  epilogue32<THW>(a, acc[0], bm0 + cw * MW * 32, lane, pp, pb, py, px);
+  if constexpr (MW > 1) epilogue32<THW>(a, acc[1], bm0 + (cw * MW + 1) * 32, lane, pp, pb, py, px);
 }
 
 }  // namespace conv
 
-// tile -> (waves along Cout, 32-row fragments per wave, patch rows)
-inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
+// tile -> (waves along Cout, 32-row fragments per wave, patch rows per wave, waves along the patch rows)
+inline bool v3_geom(int tile, int* nwm, int* mw, int* thw, int* nwp) {
+  *nwp = 1;
   switch (tile) {
-    case 60: *nwm = 4; *mw = 1; *th = 6; return true;
-    case 61: *nwm = 4; *mw = 1; *th = 3; return true;
-    case 62: *nwm = 4; *mw = 2; *th = 6; return true;
-    case 63: *nwm = 2; *mw = 1; *th = 6; return true;
-    case 64: *nwm = 3; *mw = 1; *th = 6; return true;
-    case 65: *nwm = 2; *mw = 1; *th = 3; return true;
+    case 60: *nwm = 4; *mw = 1; *thw = 6; return true;
+    case 61: *nwm = 4; *mw = 1; *thw = 3; return true;
+    case 62: *nwm = 4; *mw = 2; *thw = 6; return true;
+    case 63: *nwm = 2; *mw = 1; *thw = 6; return true;
+    case 64: *nwm = 3; *mw = 1; *thw = 6; return true;
+    case 65: *nwm = 2; *mw = 1; *thw = 3; return true;
+    case 66: *nwm = 4; *mw = 1; *thw = 3; *nwp = 2; return true;
+    case 67: *nwm = 4; *mw = 1; *thw = 4; *nwp = 2; return true;
+    case 68: *nwm = 2; *mw = 1; *thw = 3; *nwp = 4; return true;
     default: return false;
   }
 }
@@ -303,10 +311,10 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
 // conv_v3_k{33,15,51}.hip: one translation unit per kernel shape (parallel build)
 #define RS_V3_LAUNCHER(NAME, KH_, KW_)                                                             \
   bool NAME(const conv::Args& a, int tile, hipStream_t stream) {                                   \
-    int nwm, mw, th;                                                                               \
-    if (!v3_geom(tile, &nwm, &mw, &th)) return false;                                              \
-    const dim3 grid(cdiv(a.Cout, 32 * nwm * mw) * a.B * cdiv(a.H, th) * cdiv(a.W, 32));            \
-    const dim3 block(64 * nwm);                                                                    \
+    int nwm, mw, thw, nwp;                                                                         \
+    if (!v3_geom(tile, &nwm, &mw, &thw, &nwp)) return false;                                       \
+    const dim3 grid(cdiv(a.Cout, 32 * nwm * mw) * a.B * cdiv(a.H, thw * nwp) * cdiv(a.W, 32));     \
+    const dim3 block(64 * nwm * nwp);                                                              \
     constexpr int R1 = KH_ * KW_ == 9 ? 12 : 10, R2 = KH_ * KW_ == 9 ? 9 : 5;                       \
     switch (tile) {                                                                                \
       case 60: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 6, R1>), grid, block, 0, stream, a); break; \
@@ -314,6 +322,9 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
       case 62: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 2, 6, R2>), grid, block, 0, stream, a); break; \
       case 63: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 6, R1>), grid, block, 0, stream, a); break; \
       case 65: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1>), grid, block, 0, stream, a); break; \
+      case 66: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 3, R1, 2>), grid, block, 0, stream, a); break; \
+      case 67: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 4, R1, 2>), grid, block, 0, stream, a); break; \
+      case 68: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1, 4>), grid, block, 0, stream, a); break; \
       default: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 3, 1, 6, R1>), grid, block, 0, stream, a); break; \
     }                                                                                              \
     return true;                                                                                   \
@@ -321,5 +332,4 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* th) {
 bool conv_v3_launch_k33(const conv::Args& a, int tile, hipStream_t stream);
 bool conv_v3_launch_k15(const conv::Args& a, int tile, hipStream_t stream);
 bool conv_v3_launch_k51(const conv::Args& a, int tile, hipStream_t stream);
-bool conv_v3_exp_k15(const conv::Args& a, int tile, hipStream_t stream);
 }  // namespace rs

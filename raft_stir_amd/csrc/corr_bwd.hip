@@ -1,289 +1,312 @@
-// Backward of the all-pairs correlation volume on MFMA, with the pyramid
-// gradient folded into the operand load (reference: the autograd backward of
-// core/corr.py:52-60 corr() = fmap1^T fmap2 / sqrt(C) and of the avg_pool2d
-// pyramid, core/corr.py:24-27).
+// Backward of the all-pairs correlation volume: the two feature-gradient GEMMs
+// on MFMA (reference: the autograd backward of core/corr.py:52-60,
+// corr() = fmap1^T fmap2 / sqrt(C), and of the avg_pool2d pyramid,
+// core/corr.py:24-27).
 //
-// The lookups' backward accumulated the gradient of every pyramid level
-// g_l[b][p1][cell] (fp32, one row per query pixel p1).  The gradient of the
-// level-0 volume is
-//   G[b][p1][p2] = scale * sum_l 4^-l g_l[b][p1][(y2 >> l, x2 >> l)]     (p2 = (y2, x2);
-//                  a level-l cell exists for floor-pooled sizes only)
-// and the features' gradients are two GEMMs over it:
-//   df1[b][p1][c] = sum_p2 G[b][p1][p2] f2[b][p2][c]        (TRANS = false, M = N1, K = N2)
-//   df2[b][p2][c] = sum_p1 G[b][p1][p2] f1[b][p1][c]        (TRANS = true,  M = N2, K = N1)
-// G is never materialised: each block folds its 64 x 32 tile of G per K step
-// straight from the gradient pyramid into LDS (bf16), instead of a fold pass
-// writing a 130 MB bf16 G and two library GEMMs reading it back.
+// The lookups' backward accumulated the gradient of every pyramid level; one
+// fold pass (corr_lookup.hip pyr_fold4_kernel) turns it into the bf16
+// level-0 volume gradient G[b][p1][p2] (scale and every level's avg-pool
+// adjoint applied), rows padded with zeros to a multiple of 64 (pitch Ep).
+// The features' gradients are then, per batch image b,
+//   df1[b] = G[b]   f2[b]     (M = N1, K = N2)   "NN": A = rows of G (K-contiguous)
+//   df2[b] = G[b]^T f1[b]     (M = N2, K = N1)   "TN": A = columns of G
+// with f1 / f2 pixel-major [p][C] (the B operand is K-major rows).
 //
-// Block: 64 output rows x all 256 channels, 4 waves; wave w owns channels
-// [64w, 64w+64): 4 x 4 mfma_f32_16x16x32_bf16 tiles with the MFMA's A = the
-// features (16 channels x 32 K; from fT, the features transposed to
-// [b][c][K] so a lane's 8 K values are one 16-byte load) and B = the G tile
-// (32 K x 16 rows, ds_read_b128 from the LDS image [row][K], 80-byte pitch:
-// conflict-free for 16 consecutive rows).  The accumulator then holds
-// D[channel][row]: a lane's 4 values are 4 consecutive channels of one output
-// row, one 8-byte (bf16) / 16-byte (fp32) store.
-// G tile staging: TRANS = false, thread (row m = t/4, 8 consecutive p2) reads
-// two float4 of g_0 plus the coarser levels' cells; TRANS = true, thread
-// (p2 = t%64, 8 consecutive p1) reads one g_0 value per p1 row (coalesced
-// across the wave) and the 3 coarser cells of the same (y2, x2).  Next step's
-// g loads are in flight while this step's MFMAs run (register prefetch, LDS
-// double buffer, one barrier per step).
+// One launch runs both GEMMs (the two sets of output tiles are independent;
+// together ~740 blocks of 4 waves at the training shape, two blocks per CU).
+// Block = 128 output rows x 128 channels, K step 64, 4 waves in 2 x 2, each a
+// 64 x 64 tile of four v_mfma_f32_32x32x16_bf16 accumulators:
+//  * A and B K-step tiles are copied global -> LDS by buffer_load ... lds
+//    (double-buffered: the next K step is in flight during this step's MFMAs;
+//    rows past M / K come back as zeros from the buffer range check);
+//  * NN A tile: 128 rows x 128 B, the 16-B chunk index XOR ((row >> 1) & 7)
+//    so a ds_read_b128 of 16 consecutive rows hits all 64 banks;
+//  * K-major tiles (B, and the TN A tile): 64 K rows x 256 B; fragments are
+//    gathered by ds_read_b64_tr_b16 (4 K values of one column per lane), rows
+//    XOR-swizzle their 64-B quarters by (row & 3) so the 32 lanes of a
+//    transposed read cover all 64 banks;
+//  * the next sub-step's fragments are read while this sub-step's MFMAs run
+//    (counted lgkmcnt waits; the LDS reads are inline asm so the compiler does
+//    not drain the in-flight DMA in front of them);
+//  * fp32 accumulation, bf16 output rows written once: no atomics, no
+//    split-K -- deterministic by construction.
 #include "common.h"
 
-namespace rs {
-namespace corrbwd {
+#include <algorithm>
+#include <type_traits>
 
-struct GArgs {
-  const float* g[4];
-  int H[4], W[4], S[4];
-  int levels;
-  int B, N1, N2;
-  float scale;
-  const bf16_t* fT;  // [B][256][NP] bf16, rows zero-padded to NP (a multiple of 32)
-  int NP;
-  void* out;         // [B][M][256]
-  int M, K;          // output rows, reduction length
-  int vec;           // g_0 rows 16-byte aligned (8-float loads) -- the non-transposed staging
-  int ksplit, kchunk;  // K split over ksplit blocks of kchunk (a multiple of KS) each: fp32 atomics into out
+namespace rs {
+namespace cgemm {
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+struct Args {
+  const bf16_t* G;   // [B][N1][Ep]
+  const bf16_t* f1;  // [B][N1][C]
+  const bf16_t* f2;  // [B][N2][C]
+  bf16_t* d1;        // [B][N1][C]
+  bf16_t* d2;        // [B][N2][C]
+  unsigned g_bytes, f1_bytes, f2_bytes;
+  int B, N1, N2, C, Ep;
+  int nm1, nm2, nn;  // M tiles of each GEMM, channel tiles
 };
 
-constexpr int BMR = 64, KS = 32, GP = 40;  // G tile rows, K step, LDS pitch (bf16)
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE = BK * 256;     // bytes of one operand tile (128 x 64 or 64 x 128 bf16)
+constexpr int STAGE = 2 * TILE;    // A + B
+constexpr int kFar = 0x7ffffff0;   // buffer offset past every range: reads zeros
 
-__device__ __forceinline__ uint32_t pk2(float a, float b) { return uint32_t(f2bf(a)) | (uint32_t(f2bf(b)) << 16); }
-
-// C: feature channels (256: RAFT, 128: RAFT-small); a wave owns C/4 of them (NT 16-channel tiles)
-// SPLIT: the K range is split over a.ksplit blocks (more blocks in flight for
-// the latency-bound G staging); each adds its partial tile into the zeroed
-// fp32 output with atomics (not used in deterministic mode).
-template <bool TRANS, typename OT, int C, bool SPLIT>
-__global__ __launch_bounds__(256) void corr_bwd_kernel(GArgs a_) {
-  constexpr int NT = C / 64;
-  static_assert(!SPLIT || sizeof(OT) == 4, "split-K accumulates in fp32");
-  __shared__ __attribute__((aligned(16))) bf16_t gs[2][BMR * GP];
-  const GArgs a = a_;  // a local copy: the staging lambdas capture it (not the kernarg segment)
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int mblocks = cdiv(a.M, BMR);
-  const int ks = SPLIT ? (int)(blockIdx.x % a.ksplit) : 0;
-  const int bid = SPLIT ? (int)(blockIdx.x / a.ksplit) : (int)blockIdx.x;
-  const int b = bid / mblocks, m0 = (bid - b * mblocks) * BMR;
-  const int W0 = a.W[0];
-  const size_t rowbase = (size_t)b * a.N1;  // g rows of image b
-  const int kbeg = SPLIT ? ks * a.kchunk : 0;
-  const int kend = SPLIT ? min(a.K, kbeg + a.kchunk) : a.K;
-  const int nsteps = kend > kbeg ? cdiv(kend - kbeg, KS) : 0;
-
-  // ---- G-tile staging: this thread's 8 values of the 64 x 32 tile
-  // !TRANS: row m = m0 + t/4 (p1), K = k0 + 8*(t&3) .. +7 (p2)
-  //  TRANS: row m = m0 + t%64 (p2), K = k0 + 8*(t>>6) .. +7 (p1)
-  const int sm = TRANS ? (t & 63) : (t >> 2);
-  const int sk = TRANS ? 8 * (t >> 6) : 8 * (t & 3);
-  const int mrow = m0 + sm;
-  const bool mok = mrow < a.M;
-  // TRANS: the fixed p2 of this thread -> its coarser-level cell offsets (-1: no cell)
-  int cell[4] = {0, -1, -1, -1};
-  if (TRANS && mok) {
-    const int y2 = mrow / W0, x2 = mrow - y2 * W0;
-    cell[0] = mrow;
-#pragma unroll
-    for (int l = 1; l < 4; ++l)
-      if (l < a.levels && (y2 >> l) < a.H[l] && (x2 >> l) < a.W[l]) cell[l] = (y2 >> l) * a.W[l] + (x2 >> l);
+template <int I, int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
   }
-  float v[8];
-  auto load = [&](int k0) {
-    if constexpr (TRANS) {
+}
+
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const uint8_t* lds_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+// logical 16-B chunk held by LDS slot (row r, physical chunk pc) of a tile
+__device__ __forceinline__ int chunk_rowmajor(int r, int pc) { return pc ^ ((r >> 1) & 7); }        // 8 chunks / row
+__device__ __forceinline__ int chunk_kmajor(int r, int pc) { return pc ^ ((r & 3) << 2); }          // 16 chunks / row
+
+// One K-step's fragments for sub-step KK: A (2 x 32 rows), B (2 x 32 columns).
+// TA: A from a K-major tile (transposed reads) instead of the row-major one.
+template <bool TA>
+struct Frags {
+  v4s_t a[2][2], b[2][2];  // [fragment][lo / hi 4 K values]
+};
+
+template <bool TA, int KK>
+__device__ __forceinline__ void read_frags(Frags<TA>& f, const uint32_t (&aaddr)[2][4], const uint32_t (&baddr)[2],
+                                           uint32_t so) {
+  if constexpr (TA) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int p1 = k0 + sk + i;
-        float s = 0.f;
-        if (mok && p1 < a.K) {
-          const size_t r = rowbase + p1;
-          s = a.g[0][r * a.S[0] + cell[0]];
-          float w = 1.f;
+    for (int i = 0; i < 2; ++i) {
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.a[i][0]) : "v"(aaddr[i][0] + so),
+                   "i"((16 * KK) * 256) : "memory");
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.a[i][1]) : "v"(aaddr[i][0] + so),
+                   "i"((16 * KK + 4) * 256) : "memory");
+    }
+  } else {
 #pragma unroll
-          for (int l = 1; l < 4; ++l) {
-            w *= 0.25f;
-            if (cell[l] >= 0) s += w * a.g[l][r * a.S[l] + cell[l]];
-          }
-        }
-        v[i] = s * a.scale;
-      }
+    for (int i = 0; i < 2; ++i) {
+      // one 16-B read = both 4-value halves
+      typedef short v8s_t __attribute__((ext_vector_type(8)));
+      v8s_t v;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(aaddr[i][KK] + so) : "memory");
+      f.a[i][0] = __builtin_shufflevector(v, v, 0, 1, 2, 3);
+      f.a[i][1] = __builtin_shufflevector(v, v, 4, 5, 6, 7);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.b[j][0]) : "v"(baddr[j] + so),
+                 "i"(TILE + (16 * KK) * 256) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f.b[j][1]) : "v"(baddr[j] + so),
+                 "i"(TILE + (16 * KK + 4) * 256) : "memory");
+  }
+}
+
+template <bool TA>
+__device__ __forceinline__ void mfma4(f32x16_t (&acc)[2][2], Frags<TA>& f) {
+  asm volatile("" : "+v"(f.a[0][0]), "+v"(f.a[0][1]), "+v"(f.a[1][0]), "+v"(f.a[1][1]));
+  asm volatile("" : "+v"(f.b[0][0]), "+v"(f.b[0][1]), "+v"(f.b[1][0]), "+v"(f.b[1][1]));
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16x8_t av = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(f.a[i][0], f.a[i][1], 0, 1, 2, 3, 4, 5, 6, 7));
+      const bf16x8_t bv = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(f.b[j][0], f.b[j][1], 0, 1, 2, 3, 4, 5, 6, 7));
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i][j], 0, 0, 0);
+    }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// TA = false: D1 = G F2 (A rows = G rows); TA = true: D2 = G^T F1 (A = G columns)
+template <bool TA>
+__device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, int mt, int nt) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int M = TA ? a.N2 : a.N1, K = TA ? a.N1 : a.N2;
+  const int m0 = mt * BM, n0 = nt * BN, C = a.C, Ep = a.Ep;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.G, (short)0, a.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rf = TA ? __builtin_amdgcn_make_buffer_rsrc((void*)a.f1, (short)0, a.f1_bytes, 0x00020000)
+                                       : __builtin_amdgcn_make_buffer_rsrc((void*)a.f2, (short)0, a.f2_bytes, 0x00020000);
+  const long gbase = (long)b * a.N1;   // first G row of this image
+  const long fbase = (long)b * K;      // first feature row (the K rows)
+
+  // ---- per-lane DMA roles: 4 A slots + 4 B slots (16 B each) per K step
+  // A: (row, element) of this lane's slots -- NN: G row m0+r, column k0+8c; TA: G row k0+r, column m0+8c
+  int aro[4], aco[4], bro[4], bco[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int s = (wave + 4 * i) * 64 + lane;
+    if constexpr (TA) {
+      const int r = s >> 4;
+      aro[i] = r;
+      aco[i] = 8 * chunk_kmajor(r, s & 15);
     } else {
-      const int p2 = k0 + sk;
-      const size_t r = rowbase + (mok ? mrow : 0);
-      const float* g0 = a.g[0] + r * a.S[0];
-      if (mok && a.vec && p2 + 8 <= a.K) {
-        const float4 x = *reinterpret_cast<const float4*>(g0 + p2);
-        const float4 y = *reinterpret_cast<const float4*>(g0 + p2 + 4);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+      const int r = s >> 3;
+      aro[i] = r;
+      aco[i] = 8 * chunk_rowmajor(r, s & 7);
+    }
+    const int r = s >> 4;
+    bro[i] = r;
+    bco[i] = 8 * chunk_kmajor(r, s & 15);
+  }
+  const int nk = cdiv(K, BK);
+  auto issue = [&](int kt, int st) {
+    const uint8_t* sb = lds + st * STAGE;
+    const bool live = kt < nk;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int v;
+      if constexpr (TA) {
+        v = (live && k0 + aro[i] < K) ? (int)(((gbase + k0 + aro[i]) * Ep + m0 + aco[i]) * 2) : kFar;
       } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (mok && p2 + i < a.K) ? g0[p2 + i] : 0.f;
+        // columns k0 .. k0+63 < Ep always (Ep = round_up(N2, 64), zero pad)
+        v = (live && m0 + aro[i] < M) ? (int)(((gbase + m0 + aro[i]) * Ep + k0 + aco[i]) * 2) : kFar;
       }
-      int y2 = p2 / W0, x2 = p2 - y2 * W0;
+      dma16(rg, sb + (wave + 4 * i) * 1024, v);
+    }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (mok && p2 + i < a.K) {
-          float w = 1.f;
-#pragma unroll
-          for (int l = 1; l < 4; ++l) {
-            w *= 0.25f;
-            if (l < a.levels && (y2 >> l) < a.H[l] && (x2 >> l) < a.W[l])
-              v[i] += w * a.g[l][r * a.S[l] + (y2 >> l) * a.W[l] + (x2 >> l)];
-          }
-        }
-        v[i] *= a.scale;
-        if (++x2 == W0) { x2 = 0; ++y2; }
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int v = (live && k0 + bro[i] < K) ? (int)(((fbase + k0 + bro[i]) * C + n0 + bco[i]) * 2) : kFar;
+      dma16(rf, sb + TILE + (wave + 4 * i) * 1024, v);
     }
   };
-  auto store = [&](int buf) {
-    *reinterpret_cast<uint4*>(&gs[buf][sm * GP + sk]) =
-        make_uint4(pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7]));
+
+  // ---- fragment read addresses (bytes, LDS)
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3, h = lane >> 5;
+  // K-major tile, columns col0 .. col0+31 (col0 % 32 == 0): lane (g, 4q+p) reads row 8(g>>1) + q (+4, + 16 KK),
+  // columns col0 + 16(g&1) + 4p .. +3; quarter (col0 / 32) ^ q
+  auto kmaj = [&](int col0) -> uint32_t {
+    return (uint32_t)((8 * (g >> 1) + q) * 256 + (((col0 >> 5) ^ q) << 6) + (16 * (g & 1) + 4 * p) * 2);
   };
-
-  // ---- MFMA operands
-  const int r16 = lane & 15, q = lane >> 4;
-  const bf16_t* fT = a.fT + ((size_t)b * C + wave * (C / 4) + r16) * a.NP + 8 * q;  // + nt*16 rows, + k0
-  f32x4_t acc[NT][4];  // [n-tile: 16 channels][m-tile: 16 rows]
+  uint32_t aaddr[2][4], baddr[2];
 #pragma unroll
-  for (int i = 0; i < NT; ++i)
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (TA) {
+      aaddr[i][0] = lds0 + kmaj(wm * 64 + 32 * i);
+      aaddr[i][1] = aaddr[i][2] = aaddr[i][3] = 0;
+    } else {
+      // row-major tile: row wm*64 + 32i + (lane & 31), logical chunk 2 KK + h
+      const int r = wm * 64 + 32 * i + (lane & 31);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // the features' fragments of step s + 1 are loaded during step s (a dependent
-  // global load per step otherwise exposes its full latency every K step)
-  uint4 fa[NT], fn[NT];
-  if (nsteps > 0) {
-    load(kbeg);
-    store(0);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) fa[nt] = *reinterpret_cast<const uint4*>(fT + (size_t)nt * 16 * a.NP + kbeg);
-  }
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1, k0 = kbeg + s * KS;
-    const bool more = s + 1 < nsteps;
-    if (more) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) fn[nt] = *reinterpret_cast<const uint4*>(fT + (size_t)nt * 16 * a.NP + k0 + KS);
-      load(k0 + KS);
+      for (int kk = 0; kk < 4; ++kk) aaddr[i][kk] = lds0 + r * 128 + (chunk_rowmajor(r, 2 * kk + h) << 4);
     }
-    uint4 gb[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) gb[mt] = *reinterpret_cast<const uint4*>(&gs[buf][(mt * 16 + r16) * GP + 8 * q]);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[nt]),
-                                                              __builtin_bit_cast(bf16x8_t, gb[mt]), acc[nt][mt], 0,
-                                                              0, 0);
-    if (more) {
-      store(buf ^ 1);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) fa[nt] = fn[nt];
-    }
-    __syncthreads();
+    baddr[i] = lds0 + kmaj(wn * 64 + 32 * i);
   }
-  if (SPLIT && nsteps == 0) return;
 
-  // ---- epilogue: D[channel = 4q + j][row = r16] of each tile -> out[b][row][channel]
+  f32x16_t acc[2][2];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int row = m0 + mt * 16 + r16;
-    if (row >= a.M) continue;
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int c = wave * (C / 4) + nt * 16 + 4 * q;
-      const size_t o = ((size_t)b * a.M + row) * C + c;
-      if constexpr (SPLIT) {
-        float* op = static_cast<float*>(a.out) + o;
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) atomicAdd(op + j, acc[nt][mt][j]);
-      } else if constexpr (sizeof(OT) == 2) {
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(a.out) + o) =
-            make_uint2(pk2(acc[nt][mt][0], acc[nt][mt][1]), pk2(acc[nt][mt][2], acc[nt][mt][3]));
-      } else {
-        *reinterpret_cast<float4*>(static_cast<float*>(a.out) + o) =
-            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int RPS = (TA ? 4 : 2) + 4;  // LDS reads per sub-step
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    issue(kt + 1, st ^ 1);   // zeros past the end: a static vmcnt count
+    wait_vm<8>();            // this step's own pieces have landed
+    asm volatile("s_barrier" ::: "memory");  // ... and every other wave's
+    const uint32_t so = st * STAGE;
+    Frags<TA> f0, f1;
+    read_frags<TA, 0>(f0, aaddr, baddr, so);
+    read_frags<TA, 1>(f1, aaddr, baddr, so);
+    wait_lgkm<RPS>();
+    mfma4<TA>(acc, f0);
+    read_frags<TA, 2>(f0, aaddr, baddr, so);
+    wait_lgkm<RPS>();
+    mfma4<TA>(acc, f1);
+    read_frags<TA, 3>(f1, aaddr, baddr, so);
+    wait_lgkm<RPS>();
+    mfma4<TA>(acc, f0);
+    wait_lgkm<0>();
+    mfma4<TA>(acc, f1);
+    asm volatile("s_barrier" ::: "memory");  // every wave done reading this stage
+  }
+  wait_vm<0>();
+
+  // ---- epilogue: acc[i][j] reg r -> row m0 + wm*64 + 32i + (r&3) + 8(r>>2) + 4h, channel n0 + wn*64 + 32j + lane&31
+  bf16_t* out = TA ? a.d2 : a.d1;
+  const long obase = (long)b * M;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < M) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          out[(obase + m) * C + n0 + wn * 64 + 32 * j + (lane & 31)] = f2bf(acc[i][j][r]);
       }
     }
+}
+
+__global__ __launch_bounds__(256, 2) void corr_bwd_gemm_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+  const int nblk1 = a.B * a.nm1 * a.nn;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  if (lid < nblk1) {
+    const int nt = lid % a.nn, r = lid / a.nn;
+    gemm_tile<false>(a, lds, r / a.nm1, r % a.nm1, nt);
+  } else {
+    const int l2 = lid - nblk1;
+    const int nt = l2 % a.nn, r = l2 / a.nn;
+    gemm_tile<true>(a, lds, r / a.nm2, r % a.nm2, nt);
   }
 }
 
-// x [B][N][C] bf16 -> xT [B][C][NP] bf16, columns N .. NP-1 zero (64 x 64 tiles via LDS)
-__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict__ x, int N, int NP, int C,
-                                                        bf16_t* __restrict__ xT) {
-  __shared__ bf16_t tile[64][66];
-  const int nb = cdiv(NP, 64), cb = C / 64;
-  const int b = blockIdx.x / (nb * cb), rem = blockIdx.x - b * nb * cb;
-  const int n0 = (rem / cb) * 64, c0 = (rem % cb) * 64;
-  const int t = threadIdx.x;
-  for (int i = t; i < 64 * 64; i += 256) {
-    const int n = i >> 6, c = i & 63;
-    tile[n][c] = (n0 + n < N) ? x[((size_t)b * N + n0 + n) * C + c0 + c] : (bf16_t)0;
-  }
-  __syncthreads();
-  for (int i = t; i < 64 * 64; i += 256) {
-    const int c = i >> 6, n = i & 63;
-    if (n0 + n < NP) xT[((size_t)b * C + c0 + c) * NP + n0 + n] = tile[n][c];
-  }
-}
+}  // namespace cgemm
 
-}  // namespace corrbwd
+int corr_bwd_pitch(int N2) { return round_up(N2, cgemm::BK); }
 
-// gpyr: levels of [B][N1][cells] fp32 (row pitch S[l]); f1 [B][N1][C], f2 [B][N2][C] bf16 (N2 = H0*W0 = N1)
-// -> df1 [B][N1][C], df2 [B][N2][C] (bf16, or fp32: out_f32); scratch: xT [B][C][NP] bf16, NP = round_up(N, 32)
-// ksplit > 1: df1 / df2 must be ZEROED fp32 (out_f32) -- the K-split blocks add into them
-void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
-                     const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
-                     int NP, int ksplit, hipStream_t stream) {
-  corrbwd::GArgs a{};
-  for (int l = 0; l < 4; ++l) {
-    a.g[l] = l < levels ? g[l] : g[0];
-    a.H[l] = l < levels ? H[l] : 1;
-    a.W[l] = l < levels ? W[l] : 1;
-    a.S[l] = l < levels ? S[l] : S[0];
-  }
-  a.levels = levels;
-  a.B = B;
-  a.N1 = N1;
-  a.N2 = H[0] * W[0];
-  a.scale = scale;
-  a.NP = NP;
-  a.vec = (S[0] % 4 == 0) && ((uintptr_t)g[0] % 16 == 0);
-  bf16_t* xT = static_cast<bf16_t*>(scratch);
-  const dim3 gt(B * cdiv(NP, 64) * (C / 64));
-  a.ksplit = ksplit > 1 ? ksplit : 1;
-#define RS_CB(TR, OT_)                                                                                   \
-  do {                                                                                                  \
-    a.kchunk = round_up(cdiv(a.K, a.ksplit), corrbwd::KS);                                              \
-    const dim3 g_(B * cdiv(a.M, corrbwd::BMR) * a.ksplit);                                              \
-    if (a.ksplit > 1) {                                                                                 \
-      if (C == 256) hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, float, 256, true>), g_, dim3(256), 0, stream, a); \
-      else hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, float, 128, true>), g_, dim3(256), 0, stream, a);     \
-    } else {                                                                                            \
-      if (C == 256) hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 256, false>), g_, dim3(256), 0, stream, a); \
-      else hipLaunchKernelGGL((corrbwd::corr_bwd_kernel<TR, OT_, 128, false>), g_, dim3(256), 0, stream, a);     \
-    }                                                                                                   \
-  } while (0)
-  // df1 = G f2: fT = f2^T
-  hipLaunchKernelGGL(corrbwd::transpose_kernel, gt, dim3(256), 0, stream, static_cast<const bf16_t*>(f2), a.N2, NP,
-                     C, xT);
-  a.fT = xT;
-  a.out = df1;
-  a.M = N1;
-  a.K = a.N2;
-  if (out_f32) RS_CB(false, float); else RS_CB(false, bf16_t);
-  // df2 = G^T f1: fT = f1^T (the same scratch: stream-ordered after the first GEMM)
-  hipLaunchKernelGGL(corrbwd::transpose_kernel, gt, dim3(256), 0, stream, static_cast<const bf16_t*>(f1), N1, NP, C,
-                     xT);
-  a.out = df2;
-  a.M = a.N2;
-  a.K = N1;
-  if (out_f32) RS_CB(true, float); else RS_CB(true, bf16_t);
-#undef RS_CB
+// G [B][N1][Ep] bf16 (Ep = corr_bwd_pitch(N2), zero columns past N2); f1 [B][N1][C], f2 [B][N2][C] bf16,
+// C % 128 == 0 -> df1 [B][N1][C], df2 [B][N2][C] bf16
+void corr_bwd_gemm_launch(const void* G, int Ep, const void* f1, const void* f2, int B, int N1, int N2, int C,
+                          void* df1, void* df2, hipStream_t stream) {
+  cgemm::Args a{};
+  a.G = static_cast<const bf16_t*>(G);
+  a.f1 = static_cast<const bf16_t*>(f1);
+  a.f2 = static_cast<const bf16_t*>(f2);
+  a.d1 = static_cast<bf16_t*>(df1);
+  a.d2 = static_cast<bf16_t*>(df2);
+  a.g_bytes = (unsigned)((long)B * N1 * Ep * 2);
+  a.f1_bytes = (unsigned)((long)B * N1 * C * 2);
+  a.f2_bytes = (unsigned)((long)B * N2 * C * 2);
+  a.B = B; a.N1 = N1; a.N2 = N2; a.C = C; a.Ep = Ep;
+  a.nm1 = cdiv(N1, cgemm::BM);
+  a.nm2 = cdiv(N2, cgemm::BM);
+  a.nn = C / cgemm::BN;
+  const int nblk = B * (a.nm1 + a.nm2) * a.nn;
+  if (nblk == 0) return;
+  hipLaunchKernelGGL(cgemm::corr_bwd_gemm_kernel, dim3(nblk), dim3(256), 0, stream, a);
 }
 
 }  // namespace rs

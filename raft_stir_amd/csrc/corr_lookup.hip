@@ -289,14 +289,16 @@ __global__ __launch_bounds__(256) void pyr_fold_kernel(PyrMut g, int levels, lon
 // 32-bit in-row index math only (the flat kernel above spends most of its time
 // in 64-bit div/mod per element: 469 us for the 477 MB of the training-shape
 // fold), one 16-B level-0 load, one 8-B bf16 store (or 16-B in-place store).
-// Needs S[0] % 4 == 0 (pyramid rows are padded to 128 B); the bf16 rows are
-// compact (pitch E = H0*W0), so 8-B stores need E % 4 == 0, else 2-B stores.
+// Needs S[0] % 4 == 0 (pyramid rows are padded to 128 B).  bf16 rows have
+// pitch OP >= E = H0*W0 (columns E..OP-1 are written as zeros: the padded
+// operand of the corr_bwd.hip GEMMs); 8-B stores need OP % 4 == 0.
 template <bool BF16>
 __global__ __launch_bounds__(256) void pyr_fold4_kernel(PyrMut g, int levels, int rows, float scale,
-                                                        bf16_t* __restrict__ out_bf16) {
+                                                        bf16_t* __restrict__ out_bf16, int OP) {
   const int H0 = g.H[0], W0 = g.W[0], E = H0 * W0;
-  const int E4 = (E + 3) >> 2;
-  const bool vec_out = (E & 3) == 0;
+  const int span = BF16 ? OP : E;  // elements written per row
+  const int E4 = (span + 3) >> 2;
+  const bool vec_out = (OP & 3) == 0;
   for (int row = blockIdx.y; row < rows; row += gridDim.y) {
     float* r0 = g.p[0] + (size_t)row * g.S[0];
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < E4; q += gridDim.x * blockDim.x) {
@@ -310,37 +312,39 @@ __global__ __launch_bounds__(256) void pyr_fold4_kernel(PyrMut g, int levels, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = e + j < E ? r0[e + j] : 0.f;
       }
-      int ys[4], xs[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ys[j] = (e + j) / W0;
-        xs[j] = e + j - ys[j] * W0;
-      }
-      float w = 1.f;
-#pragma unroll
-      for (int l = 1; l < 4; ++l) {
-        if (l >= levels) break;
-        w *= 0.25f;
-        const float* rl = g.p[l] + (size_t)row * g.S[l];
-        const int Hl = g.H[l], Wl = g.W[l];
+      if (e < E) {
+        int ys[4], xs[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int yl = ys[j] >> l, xl = xs[j] >> l;
-          if (e + j < E && yl < Hl && xl < Wl) v[j] += w * rl[yl * Wl + xl];
+          ys[j] = (e + j) / W0;
+          xs[j] = e + j - ys[j] * W0;
+        }
+        float w = 1.f;
+#pragma unroll
+        for (int l = 1; l < 4; ++l) {
+          if (l >= levels) break;
+          w *= 0.25f;
+          const float* rl = g.p[l] + (size_t)row * g.S[l];
+          const int Hl = g.H[l], Wl = g.W[l];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int yl = ys[j] >> l, xl = xs[j] >> l;
+            if (e + j < E && yl < Hl && xl < Wl) v[j] += w * rl[yl * Wl + xl];
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] *= scale;
       if (BF16) {
-        bf16_t* o = out_bf16 + (size_t)row * E + e;
-        if (full && vec_out) {
+        bf16_t* o = out_bf16 + (size_t)row * OP + e;
+        if (e + 4 <= OP && vec_out) {
           const uint2 pk = make_uint2(uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
                                       uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16));
           *reinterpret_cast<uint2*>(o) = pk;
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (e + j < E) o[j] = f2bf(v[j]);
+            if (e + j < OP) o[j] = f2bf(v[j]);
         }
       } else if (full) {
         *reinterpret_cast<float4*>(r0 + e) = make_float4(v[0], v[1], v[2], v[3]);
@@ -350,6 +354,86 @@ __global__ __launch_bounds__(256) void pyr_fold4_kernel(PyrMut g, int levels, in
           if (e + j < E) r0[e + j] = v[j];
       }
     }
+  }
+}
+
+// Padded bf16 fold (the operand of the corr_bwd.hip GEMMs): one block per
+// row.  The coarse levels' cells of the row (<= 1 KB at the training shape)
+// are staged in LDS first (coalesced), so each level-0 quad costs one 16-B
+// load, 3 x 4 LDS reads and one 8-B store; columns E .. OP-1 are zeros.
+// Needs OP % 4 == 0, OP <= 6144 and the coarse levels' cells <= FOLD_LDS
+// floats; vec0: 16-B aligned level-0 rows (S[0] % 4 == 0), else scalar loads.
+constexpr int FOLD_LDS = 4096;
+
+__global__ __launch_bounds__(256) void pyr_fold_rows_kernel(PyrMut g, int levels, float scale,
+                                                            bf16_t* __restrict__ out, int OP, int vec0) {
+  __shared__ float cl[FOLD_LDS];
+  const int row = blockIdx.x;
+  const int H0 = g.H[0], W0 = g.W[0], E = H0 * W0;
+  const float* r0 = g.p[0] + (size_t)row * g.S[0];
+  // level-0 quads of this thread, loads issued before the LDS staging
+  const int nq = OP >> 2;
+  constexpr int QPT = 6;  // quads per thread (OP <= 6144 elements)
+  float4 v[QPT];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int e = (threadIdx.x + 256 * j) * 4;
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e + 4 <= E && vec0) {
+      v[j] = *reinterpret_cast<const float4*>(r0 + e);
+    } else if (e + 4 <= E) {
+      v[j] = make_float4(r0[e], r0[e + 1], r0[e + 2], r0[e + 3]);
+    } else if (e < E) {
+      v[j].x = r0[e];
+      if (e + 1 < E) v[j].y = r0[e + 1];
+      if (e + 2 < E) v[j].z = r0[e + 2];
+    }
+  }
+  int off[4] = {0, 0, 0, 0};
+  {
+    int o = 0;
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      off[l] = o;
+      if (l < levels) {
+        const int n = g.H[l] * g.W[l];
+        const float* rl = g.p[l] + (size_t)row * g.S[l];
+        for (int i = threadIdx.x; i < n; i += 256) cl[o + i] = rl[i];
+        o += n;
+      }
+    }
+  }
+  __syncthreads();
+  const float inv_w = 1.f / (float)W0;
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int q = threadIdx.x + 256 * j;
+    if (q >= nq) break;
+    const int e = q * 4;
+    float f[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    if (e < E) {
+      int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (e + k < E) {
+          float w = 1.f;
+#pragma unroll
+          for (int l = 1; l < 4; ++l) {
+            if (l >= levels) break;
+            w *= 0.25f;
+            const int yl = y >> l, xl = x >> l;
+            if (yl < g.H[l] && xl < g.W[l]) f[k] += w * cl[off[l] + yl * g.W[l] + xl];
+          }
+        }
+        if (++x == W0) {
+          x = 0;
+          ++y;
+        }
+      }
+    }
+    const uint2 pk = make_uint2(uint32_t(f2bf(f[0] * scale)) | (uint32_t(f2bf(f[1] * scale)) << 16),
+                                uint32_t(f2bf(f[2] * scale)) | (uint32_t(f2bf(f[3] * scale)) << 16));
+    *reinterpret_cast<uint2*>(out + (size_t)row * OP + e) = pk;
   }
 }
 
@@ -435,7 +519,7 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
 }
 
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
-                          float scale, hipStream_t stream, void* out_bf16) {
+                          float scale, hipStream_t stream, void* out_bf16, int opitch) {
   lookup::PyrMut p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? gpyr[l] : nullptr;
@@ -446,18 +530,29 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, cons
   const long total = rows * Hs[0] * Ws[0];
   if (total == 0) return;
   const long E = (long)Hs[0] * Ws[0];
+  if (opitch <= 0) opitch = (int)E;
+  long coarse = 0;
+  for (int l = 1; l < levels; ++l) coarse += (long)Hs[l] * Ws[l];
+  if (out_bf16 && opitch % 4 == 0 && opitch <= 6144 && coarse <= lookup::FOLD_LDS && rows < (1L << 31)) {
+    const int vec0 = Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0;
+    hipLaunchKernelGGL(lookup::pyr_fold_rows_kernel, dim3((unsigned)rows), dim3(256), 0, stream, p, levels, scale,
+                       static_cast<bf16_t*>(out_bf16), opitch, vec0);
+    return;
+  }
   if (Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0 && rows < (1L << 31) &&
       E < (1L << 30)) {
-    const int bx = (int)std::min<long>((E + 4 * 256 - 1) / (4 * 256), 64);
+    const long span = out_bf16 ? opitch : E;
+    const int bx = (int)std::min<long>((span + 4 * 256 - 1) / (4 * 256), 64);
     const dim3 grid(bx, (unsigned)std::min<long>(rows, 65535));
     if (out_bf16)
       hipLaunchKernelGGL(lookup::pyr_fold4_kernel<true>, grid, dim3(256), 0, stream, p, levels, (int)rows, scale,
-                         static_cast<bf16_t*>(out_bf16));
+                         static_cast<bf16_t*>(out_bf16), opitch);
     else
       hipLaunchKernelGGL(lookup::pyr_fold4_kernel<false>, grid, dim3(256), 0, stream, p, levels, (int)rows, scale,
-                         nullptr);
+                         nullptr, opitch);
     return;
   }
+  // (the flat kernel writes compact rows: callers asking for a padded pitch check the aligned case above)
   hipLaunchKernelGGL(lookup::pyr_fold_kernel, dim3(lookup::grid_for(total)), dim3(256), 0, stream,
                      p, levels, rows, scale, static_cast<bf16_t*>(out_bf16));
 }

@@ -36,11 +36,11 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                             const float* coords, int B, int H1, int W1, int r, const void* dout,
                             bool dout_bf16, hipStream_t stream, int dstride);
 size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
-void corr_bwd_launch(float* const* g, const int* H, const int* W, const int* S, int levels, int B, int N1, int C,
-                     const void* f1, const void* f2, float scale, void* df1, void* df2, bool out_f32, void* scratch,
-                     int NP, int ksplit, hipStream_t stream);
+int corr_bwd_pitch(int N2);
+void corr_bwd_gemm_launch(const void* G, int Ep, const void* f1, const void* f2, int B, int N1, int N2, int C,
+                          void* df1, void* df2, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
-                          float scale, hipStream_t stream, void* out_bf16 = nullptr);
+                          float scale, hipStream_t stream, void* out_bf16 = nullptr, int opitch = 0);
 void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
                          const long long* lo, const long long* hi, const float* s, int nr, hipStream_t stream);
 void split_bf16_launch(const float* x, long n, uint16_t* hi, uint16_t* lo, hipStream_t s);
@@ -274,8 +274,10 @@ void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Ten
   RS_CHECK_LAUNCH();
 }
 
-// Volume backward with the pyramid-gradient fold in the operand load
-// (csrc/corr_bwd.hip): (df1, df2) from the gradient pyramid, bf16 features.
+// Volume backward (csrc/corr_bwd.hip): the gradient pyramid folded once into
+// a bf16 level-0 gradient G (rows padded to a multiple of 64 with zeros), then
+// both feature-gradient GEMMs (df1 = G f2, df2 = G^T f1) in one MFMA launch.
+// bf16 features, C % 128 == 0; deterministic (no atomics).
 std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const Tensor& f1, const Tensor& f2,
                                          double scale) {
   check_gpu(f1, "f1");
@@ -285,40 +287,27 @@ std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const 
   TORCH_CHECK(f1.dim() == 3 && f1.is_contiguous(), "corr_volume_backward: f1 must be contiguous (B, N1, C)");
   TORCH_CHECK(f2.dim() == 4 && f2.is_contiguous(), "corr_volume_backward: f2 must be contiguous (B, H2, W2, C)");
   const int B = f1.size(0), N1 = f1.size(1), C = f1.size(2);
-  TORCH_CHECK(C == 128 || C == 256, "corr_volume_backward: 128 or 256 feature channels");
+  TORCH_CHECK(C % 128 == 0, "corr_volume_backward: feature channels must be a multiple of 128");
   TORCH_CHECK(f2.size(0) == B && f2.size(3) == C, "corr_volume_backward: f1 / f2 shapes");
   int Hs[4], Ws[4], Ss[4];
   check_pyr(gpyr, B, N1, Hs, Ws, Ss);
   TORCH_CHECK(Hs[0] == f2.size(1) && Ws[0] == f2.size(2), "corr_volume_backward: level 0 must be f2's grid");
-  TORCH_CHECK(Hs[0] * Ws[0] == N1, "corr_volume_backward: square volume (N1 = H2 * W2)");
-  TORCH_CHECK((int64_t)B * N1 * Ss[0] < (int64_t(1) << 40), "corr_volume_backward: pyramid too large");
+  const int N2 = Hs[0] * Ws[0];
+  const int Ep = rs::corr_bwd_pitch(N2);
+  int64_t coarse = 0;
+  for (size_t l = 1; l < gpyr.size(); ++l) coarse += (int64_t)Hs[l] * Ws[l];
+  TORCH_CHECK(Ep <= 6144 && coarse <= 4096, "corr_volume_backward: level-0 grid too large for the row fold");
+  TORCH_CHECK((int64_t)B * N1 * Ep * 2 < (int64_t(1) << 31) && (int64_t)B * std::max(N1, N2) * C * 2 < (int64_t(1) << 31),
+              "corr_volume_backward: operands must be < 2 GiB");
   const c10::DeviceGuard guard(f1.device());
-  const int NP = (N1 + 31) / 32 * 32;
-  // K split over blocks (fp32 atomics into zeroed outputs, then one cast
-  // each): the G-tile staging is latency-bound and one block per 64 output
-  // rows gives only ~1.4 blocks per CU at the training shape.  Deterministic
-  // mode keeps one block per row range (plain stores).  RS_CORR_BWD_KSPLIT
-  // overrides the split (1: no split).
-  static const int ks_env = [] {
-    const char* e = getenv("RS_CORR_BWD_KSPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  int ksplit = ks_env > 0 ? ks_env : 4;
-  if (rs::deterministic()) ksplit = 1;
-  Tensor scratch = at::empty({(int64_t)B * C * NP}, f1.options());
+  Tensor G = at::empty({(int64_t)B * N1, Ep}, f1.options());
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
-  if (ksplit > 1) {
-    Tensor a1 = at::zeros(f1.sizes(), f1.options().dtype(at::kFloat));
-    Tensor a2 = at::zeros(f2.sizes(), f2.options().dtype(at::kFloat));
-    rs::corr_bwd_launch(ptrs, Hs, Ws, Ss, gpyr.size(), B, N1, C, f1.data_ptr(), f2.data_ptr(), (float)scale,
-                        a1.data_ptr(), a2.data_ptr(), true, scratch.data_ptr(), NP, ksplit, cur_stream());
-    RS_CHECK_LAUNCH();
-    return {a1.to(at::kBFloat16), a2.to(at::kBFloat16)};
-  }
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), G.data_ptr(), Ep);
+  RS_CHECK_LAUNCH();
   Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
-  rs::corr_bwd_launch(ptrs, Hs, Ws, Ss, gpyr.size(), B, N1, C, f1.data_ptr(), f2.data_ptr(), (float)scale,
-                      df1.data_ptr(), df2.data_ptr(), false, scratch.data_ptr(), NP, 1, cur_stream());
+  rs::corr_bwd_gemm_launch(G.data_ptr(), Ep, f1.data_ptr(), f2.data_ptr(), B, N1, N2, C, df1.data_ptr(),
+                           df2.data_ptr(), cur_stream());
   RS_CHECK_LAUNCH();
   return {df1, df2};
 }

@@ -114,7 +114,7 @@ struct StemLaunch {  // must match stem.hip
   int f32;
 };
 void stem_launch(const StemLaunch& L, hipStream_t stream);
-int stem_wgrad_blocks(long P, int* px_per_block);
+int stem_wgrad_blocks(int B, int Ho, int Wo, int* chunks_per_block);
 void stem_wgrad_launch(const void* x, bool x_bf16, int B, int Hi, int Wi, int Ho, int Wo, const uint16_t* dy, int ystr,
                        int Cout, float* part, int nblk, int px_per_block, float* dw, hipStream_t stream);
 }  // namespace rs
@@ -123,7 +123,7 @@ namespace {
 using at::Tensor;
 
 constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8,
-              EPI_NORM = 9;
+              EPI_NORM = 9, EPI_ADD_BF16 = 10;
 
 hipStream_t stream() { return rs::current_stream(); }
 
@@ -201,11 +201,11 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 65), "conv_fused: tile must be in [0,54] or [60,65]");
+  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 68), "conv_fused: tile must be in [0,54] or [60,68]");
   const bool v3 = tile >= 60;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
   if ((tile >= 42 && tile <= 54) || v3)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
-                "conv_fused: tiles 42-54 and 60-65 are instantiated for 3x3, 1x5 and 5x1 kernels only");
+                "conv_fused: tiles 42-54 and 60-68 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
   TORCH_CHECK(!(tile >= 38 && tile <= 40) || f32, "conv_fused: tiles 38-40 are the fp32 split-K tiles");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
@@ -233,7 +233,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
               "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
   if (v3) {  // fragment-major rows in 32-row blocks; blocks past the weight read as zeros
     TORCH_CHECK(w.size(0) % 32 == 0 && w.size(0) >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
-                "conv_fused: tiles 60-65 need fragment-major weights with round_up(Cout, 32) rows (< 2 GiB)");
+                "conv_fused: tiles 60-68 need fragment-major weights with round_up(Cout, 32) rows (< 2 GiB)");
   } else {
     TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
                 "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
@@ -298,9 +298,11 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
+  TORCH_CHECK(epi != EPI_ADD_BF16 || (((tile >= 42 && tile <= 54) || v3) && !f32),
+              "conv_fused: EPI_ADD_BF16 (out += v, bf16) runs on tiles 42-54 and 60-68 only");
   if (nx.chs)
     TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3,
-                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54, 60-65)");
+                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54, 60-68)");
   L.chs = nx.chs;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();
@@ -842,9 +844,8 @@ void stem_wgrad(const Tensor& x, const Tensor& dy, int64_t Cout, const Tensor& d
                   (uintptr_t)dy.data_ptr() % 16 == 0, "stem_wgrad: dy channels / alignment");
   TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.scalar_type() == at::kFloat && dw.numel() == Cout * 147,
               "stem_wgrad: dw must be fp32 [Cout][3][7][7]");
-  const long P = (long)B * Ho * Wo;
   int per = 0;
-  const int nblk = rs::stem_wgrad_blocks(P, &per);
+  const int nblk = rs::stem_wgrad_blocks(B, Ho, Wo, &per);
   const c10::DeviceGuard guard(x.device());
   Tensor part = at::empty({(int64_t)nblk * 64 * 224}, dw.options());
   rs::stem_wgrad_launch(x.data_ptr(), x.scalar_type() == at::kBFloat16, B, Hi, Wi, Ho, Wo,

@@ -160,83 +160,140 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(SArgs s, conv::Args a) {
     conv::epilogue_pix<2, 2>(a, acc, m0, lane, pp, pb, py, px);
 }
 
-// Weight gradient partials.  Block = a contiguous range of output pixels
-// (multiple of 32), all 64 channels x 8 kernel-row slots (7 live, K = 32
-// each: N = 256).  Per 32-pixel K slice: dY^T [64 co][32 px] and the im2col
-// rows transposed [256 n][32 px] are staged in LDS; wave w owns n-tiles
-// 4w .. 4w+3 for all 4 channel tiles (16 16x16x32 MFMAs per slice).
-constexpr int WKP = 32;            // pixels per K slice
-constexpr int TS = WKP + 8;        // transposed LDS row stride (bf16)
+// Weight gradient partials: dW^T tile [64 co][7 ky x 32 k] = sum over pixels
+// of dY[px][co] x im2col[px][ky][k] (k = kx * 3 + ci, 21 live), K = pixels.
+// Block = 7 waves, wave ky owns kernel row ky (2 x v_mfma_f32_32x32x16_bf16
+// accumulators: co 0-31 / 32-63 x 32 k), walking a contiguous range of
+// 64-pixel chunks (b, oy, ox0 .. ox0+63) of the output grid.  Per chunk:
+//  * dY rows (64 px x 64 co, zeros past the row / Cout) -> LDS [px][co], the
+//    64-B halves of each 128-B row swapped on (px >> 1) & 1;
+//  * the 7 input rows the chunk reads, each ONE contiguous 134-pixel run of
+//    the NHWC image (402 values), -> LDS twice: the im2col row of pixel px and
+//    kernel row ky is elements [6 px, 6 px + 32) of run ky, so the B fragment
+//    (4 pixels of one column per lane, ds_read_b64_tr_b16) reads the runs in
+//    place -- even pixels from copy A (element e at byte 2e: 8-B aligned rows),
+//    odd pixels from copy B (element e at byte 2e + 4); columns 21..31 pick up
+//    the next pixel's values and land in dW columns nobody reads;
+//  * the next chunk's global loads are in flight while this chunk's MFMAs run
+//    (register prefetch, fixed per-thread slots).
+// Each block writes its fp32 partial tile; stem_wgrad_reduce_kernel adds the
+// partials in block order (deterministic).
+constexpr int WG_WAVES = 7, WG_T = 64 * WG_WAVES;
+constexpr int WG_RAWP = 416;  // run row pitch (elements): 402 live, reads up to 6 * 63 + 31 + 2 = 411
+constexpr int WG_RJ = (7 * 402 + WG_T - 1) / WG_T;  // run elements per thread
 
-__global__ __launch_bounds__(256) void stem_wgrad_kernel(SArgs s, const bf16_t* __restrict__ dy, int ystr, int Cout,
-                                                         int px_per_block, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) bf16_t ys[64 * TS];    // [co][px]
-  __shared__ __attribute__((aligned(16))) bf16_t xs[256 * TS];   // [ky*32 + k][px]
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int lr = lane & 15, lc = lane >> 4;
-  const long P = (long)s.B * s.Ho * s.Wo;
-  const long p0 = (long)blockIdx.x * px_per_block;
-  const long p1 = p0 + px_per_block < P ? p0 + px_per_block : P;
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (long q0 = p0; q0 < p1; q0 += WKP) {
-    // dY slice, transposed: thread -> (pixel j = t / 8, channels 8 * (t % 8) .. +7)
-    {
-      const int j = t >> 3, c8 = (t & 7) * 8;
-      const long p = q0 + j;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (p < p1 && c8 < Cout) v = *reinterpret_cast<const uint4*>(dy + p * ystr + c8);
-      const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ys[(c8 + i) * TS + j] = (c8 + i < Cout) ? e[i] : (bf16_t)0;
-    }
-    // im2col slice, transposed: thread -> (pixel j = t % 32, kernel row ky = t / 32 (7: zero))
-    {
-      const int j = t & 31, ky = t >> 5;
-      const long p = q0 + j;
-      bf16_t row[KR];
-      if (ky < 7 && p < p1) {
-        const int b = (int)(p / ((long)s.Ho * s.Wo));
-        const int rem = (int)(p - (long)b * s.Ho * s.Wo);
-        const int oy = rem / s.Wo, ox = rem - oy * s.Wo;
-        im2col_row<false>(s, b, 2 * oy - 3 + ky, 2 * ox - 3, row, nullptr);
-      } else {
-#pragma unroll
-        for (int k = 0; k < KR; ++k) row[k] = 0;
-      }
-#pragma unroll
-      for (int k = 0; k < KR; ++k) xs[(ky * KR + k) * TS + j] = row[k];
-    }
-    __syncthreads();
-    uint4 fa[4], fb[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) fa[mt] = *reinterpret_cast<const uint4*>(ys + (mt * 16 + lr) * TS + lc * 8);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-      fb[nt] = *reinterpret_cast<const uint4*>(xs + ((wave * 4 + nt) * 16 + lr) * TS + lc * 8);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fa[mt]),
-                                                              __builtin_bit_cast(bf16x8_t, fb[nt]), acc[mt][nt],
-                                                              0, 0, 0);
-    __syncthreads();
+__global__ __launch_bounds__(WG_T) void stem_wgrad_kernel(SArgs s, const bf16_t* __restrict__ dy, int ystr, int Cout,
+                                                          int chunks_per_block, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint8_t ylds[64 * 128];    // [px][co] bf16
+  __shared__ __attribute__((aligned(16))) bf16_t runA[7 * WG_RAWP];  // element e at index e
+  __shared__ __attribute__((aligned(16))) bf16_t runB[7 * WG_RAWP];  // element e at index e + 2
+  const int t = threadIdx.x, lane = t & 63;
+  const int ky = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int cpr = cdiv(s.Wo, 64);
+  const int nchunk = s.B * s.Ho * cpr;
+  const int c0 = blockIdx.x * chunks_per_block, c1 = min(nchunk, c0 + chunks_per_block);
+  for (int i = t; i < 7 * 16; i += WG_T) {  // constant zeros past the live run values
+    runA[(i >> 4) * WG_RAWP + 402 + (i & 15) % 14] = 0;
+    runB[(i >> 4) * WG_RAWP + 404 + (i & 15) % 12] = 0;
   }
-  // partial tile [64 co][224 n] of this block: C[co][n], co = mt*16 + 4*lc + j, n = (4w + nt)*16 + lr
+  // fixed staging slots: dY slots t and t + 448 (< 512); run elements t + 448 j
+  int rr[WG_RJ], re[WG_RJ];
+#pragma unroll
+  for (int j = 0; j < WG_RJ; ++j) {
+    const int qq = t + WG_T * j;
+    rr[j] = qq < 7 * 402 ? qq / 402 : -1;
+    re[j] = qq - (qq / 402) * 402;
+  }
+  uint4 ypre[2];
+  float xpre[WG_RJ];
+  auto prefetch = [&](int c) {
+    const int rowid = c / cpr, ox0 = (c - rowid * cpr) * 64;
+    const int b = rowid / s.Ho, oy = rowid - b * s.Ho;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int sl = t + WG_T * u;
+      const int px = (sl >> 3) & 63, c16 = sl & 7;
+      ypre[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (sl < 512 && ox0 + px < s.Wo && c16 * 8 < Cout)
+        ypre[u] = *reinterpret_cast<const uint4*>(dy + ((size_t)rowid * s.Wo + ox0 + px) * ystr + c16 * 8);
+    }
+    const int ix0 = 2 * ox0 - 3;
+#pragma unroll
+    for (int j = 0; j < WG_RJ; ++j) {
+      const int iy = 2 * oy - 3 + rr[j], ix = ix0 + re[j] / 3;
+      xpre[j] = 0.f;
+      if (rr[j] >= 0 && iy >= 0 && iy < s.Hi && ix >= 0 && ix < s.Wi)
+        xpre[j] = ldx(s, (((size_t)b * s.Hi + iy) * s.Wi + ix) * 3 + re[j] % 3);
+    }
+  };
+
+  // fragment read roles (tr16): 16-lane group g, lane 4q + p -> row q (+ 8h, + 4, + 16 KK), columns 4p .. 4p+3
+  const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3, h = lane >> 5;
+  const uint32_t y0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)ylds;
+  // A (dY^T): row px = 16 KK + 8h + q (+4), co = 32 i + 16 (g & 1) + 4p: half i ^ ((q >> 1) & 1)
+  uint32_t aaddr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    aaddr[i] = y0 + (8 * h + q) * 128 + ((i ^ ((q >> 1) & 1)) << 6) + 32 * (g & 1) + 8 * p;
+  // B (run ky): pixel px = 8h + q (+4, + 16 KK) -> elements 6 px + 16 (g & 1) + 4p; parity of px = parity of q
+  const uint32_t rb = (q & 1) ? (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)runB + 4
+                              : (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)runA;
+  const uint32_t baddr = rb + (ky * WG_RAWP + 6 * (8 * h + q) + 16 * (g & 1) + 4 * p) * 2;
+
+  f32x16_t acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  if (c0 < c1) prefetch(c0);
+  for (int c = c0; c < c1; ++c) {
+    __syncthreads();  // the previous chunk's fragments are read
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int sl = t + WG_T * u, px = (sl >> 3) & 63, c16 = sl & 7;
+      if (sl < 512) *reinterpret_cast<uint4*>(ylds + px * 128 + ((c16 ^ (((px >> 1) & 1) << 2)) << 4)) = ypre[u];
+    }
+#pragma unroll
+    for (int j = 0; j < WG_RJ; ++j) {
+      if (rr[j] >= 0) {
+        const bf16_t v = f2bf(xpre[j]);
+        runA[rr[j] * WG_RAWP + re[j]] = v;
+        runB[rr[j] * WG_RAWP + re[j] + 2] = v;
+      }
+    }
+    __syncthreads();
+    if (c + 1 < c1) prefetch(c + 1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      v4s alo[2], ahi[2], blo, bhi;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        alo[i] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(size_t)(aaddr[i] + kk * 16 * 128));
+        ahi[i] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s*)(size_t)(aaddr[i] + (kk * 16 + 4) * 128));
+      }
+      blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(size_t)(baddr + kk * 16 * 12));
+      bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) v4s*)(size_t)(baddr + (kk * 16 + 4) * 12));
+      const bf16x8_t bv = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bf16x8_t av =
+            __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(alo[i], ahi[i], 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i], 0, 0, 0);
+      }
+    }
+  }
+  // partial tile [64 co][224 n]: acc[i] reg r -> co = 32 i + (r & 3) + 8 (r >> 2) + 4h, n = ky * 32 + lane & 31
   float* o = part + (size_t)blockIdx.x * 64 * 224;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n = (wave * 4 + nt) * 16 + lr;
-      if (n < 224)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[(size_t)(mt * 16 + 4 * lc + j) * 224 + n] = acc[mt][nt][j];
-    }
+    for (int r = 0; r < 16; ++r)
+      o[(size_t)(32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * 224 + ky * 32 + (lane & 31)] = acc[i][r];
 }
 
 // dW[co][ci][ky][kx] (fp32, the conv weight's layout) = sum over blocks of the
@@ -288,20 +345,20 @@ void stem_launch(const StemLaunch& L, hipStream_t stream) {
     hipLaunchKernelGGL(stem::stem_fwd_kernel<false>, grid, dim3(256), 0, stream, s, a);
 }
 
-int stem_wgrad_blocks(long P, int* px_per_block) {
-  // ~2 blocks per CU, whole 32-pixel K slices per block
-  long per = (P + 511) / 512;
-  per = (per + 31) / 32 * 32;
-  if (per < 32) per = 32;
-  *px_per_block = (int)per;
-  return (int)((P + per - 1) / per);
+// (B, Ho, Wo) -> blocks of chunks_per_block 64-pixel row chunks: ~2 blocks per CU
+int stem_wgrad_blocks(int B, int Ho, int Wo, int* chunks_per_block) {
+  const long nchunk = (long)B * Ho * cdiv(Wo, 64);
+  long per = (nchunk + 511) / 512;
+  if (per < 1) per = 1;
+  *chunks_per_block = (int)per;
+  return (int)((nchunk + per - 1) / per);
 }
 
 void stem_wgrad_launch(const void* x, bool x_bf16, int B, int Hi, int Wi, int Ho, int Wo, const bf16_t* dy, int ystr,
-                       int Cout, float* part, int nblk, int px_per_block, float* dw, hipStream_t stream) {
+                       int Cout, float* part, int nblk, int chunks_per_block, float* dw, hipStream_t stream) {
   stem::SArgs s{x, x_bf16 ? 1 : 0, B, Hi, Wi, Ho, Wo};
-  hipLaunchKernelGGL(stem::stem_wgrad_kernel, dim3(nblk), dim3(256), 0, stream, s, dy, ystr, Cout, px_per_block,
-                     part);
+  hipLaunchKernelGGL(stem::stem_wgrad_kernel, dim3(nblk), dim3(stem::WG_T), 0, stream, s, dy, ystr, Cout,
+                     chunks_per_block, part);
   hipLaunchKernelGGL(stem::stem_wgrad_reduce_kernel, dim3(cdiv(Cout * 147, 256)), dim3(256), 0, stream, part, nblk,
                      Cout, dw);
 }

@@ -27,7 +27,6 @@ correlation MFMA GEMM (csrc/corr_volume.hip).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -37,9 +36,9 @@ from ..ops.fp32conv import conv_module
 from ..ops.norm import conv_norm_act, conv_pair_norm_act
 
 
-# RS_RES_SINK=0: the residual blocks' skip gradient returns to autograd (a
-# separate add) instead of the first conv's input-gradient epilogue (A/B)
-_RES_SINK = os.environ.get("RS_RES_SINK", "1") != "0"
+# the residual blocks' skip gradient is added in the first conv's
+# input-gradient epilogue (ops/enc_conv.py GradSink) instead of a separate add
+_RES_SINK = True
 
 
 def make_norm(kind: str, channels: int, groups: int) -> nn.Module:

@@ -58,7 +58,6 @@ from __future__ import annotations
 
 import contextlib
 
-import os
 
 import torch
 
@@ -473,7 +472,7 @@ def _split_bf16(t: torch.Tensor):
 # training shape (scripts/bench_conv.py --wgrad 12 --v3wgrad,
 # profiles/r5/README.md): GRU z|r 400 -> 302 us, q 217 -> 171, head 475 -> 348,
 # convc2 449 -> 387; the 64-output convf2 stays on conv_wgrad.hip (107 us).
-_WG3 = os.environ.get("RS_WGRAD_V3", "1") != "0"
+_WG3 = True
 
 
 def _wgrad_fn(pc, segs, bn128):

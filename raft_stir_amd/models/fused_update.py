@@ -36,12 +36,10 @@ fp32 (the reference's default inference precision, evaluate.py:174 /
 rafttoonnx.py): the same sequence on fp32 buffers, every conv on the
 split-bf16 F32 tiles (csrc/conv.hip conv_lds_kernel<..., F32>: x.w as three
 bf16 MFMA products, ~2^-17 relative error), the flow encoder / flow head /
-lookup / upsampling in their fp32 forms.  RS_F32_ENGINE=0 sends fp32 back to
-the module graph (MIOpen convolutions).
+lookup / upsampling in their fp32 forms.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -50,7 +48,7 @@ from ..ops import _ext
 from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, choose_tile_f32, conv_fused,
                         frag_eligible, frag_weight, pack_bias, pack_weight, pack_weight_split, pad_to)
 
-_F32_ENGINE = os.environ.get("RS_F32_ENGINE", "1") != "0"
+_F32_ENGINE = True
 from ..ops.upsample import convex_upsample
 
 

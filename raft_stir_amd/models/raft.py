@@ -26,7 +26,6 @@ Engine differences (outputs unchanged):
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 import torch.nn as nn
@@ -65,13 +64,12 @@ class _StreamHandoff(torch.autograd.Function):
 
 
 _SIDE_STREAMS = {}  # (device index, slot) -> extra HIP stream
-_FUSED_PREP = os.environ.get("RS_FUSED_PREP", "1") != "0"  # one-kernel input normalisation into the fnet batch
+_FUSED_PREP = True  # one-kernel input normalisation into the fnet batch
 # per-mechanism switches of the multi-stream schedule (all gated by cfg.overlap_encoders)
 # defer_enc (encoder conv weight gradients on the deferred stream too) is off:
 # paired A/B on one box, 3 x 30 steps: 352 pairs/s on vs 366 off (the third
 # stream then ends the backward late and its GEMMs contend with the dgrads)
-OVERLAP = {"cnet": True, "flow": True, "defer": True,
-           "defer_enc": os.environ.get("RS_DEFER_ENC", "0") == "1"}
+OVERLAP = {"cnet": True, "flow": True, "defer": True, "defer_enc": False}
 
 
 class RAFT(nn.Module):
@@ -134,11 +132,7 @@ class RAFT(nn.Module):
         """slot 0: context encoder / flow branch; slot 1: deferred weight gradients."""
         st = _SIDE_STREAMS.get((dev.index, slot))
         if st is None:
-            # RS_SIDE_PRIO / RS_WGRAD_PRIO: priority of the context-encoder /
-            # flow-branch stream and of the deferred weight-gradient stream
-            # (lower = more urgent; A/B switches, default 0)
-            prio = int(os.environ.get("RS_SIDE_PRIO" if slot == 0 else "RS_WGRAD_PRIO", "0"))
-            st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev, priority=prio)
+            st = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(device=dev)
         return st
 
     def freeze_bn(self):

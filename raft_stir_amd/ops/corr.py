@@ -59,21 +59,7 @@ def from_nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 3, 1, 2)
 
 
-def _side_stream(dev):
-    """The RAFT model's slot-0 side stream (models/raft.py), if its multi-stream
-    schedule created one on this device."""
-    if dev.type != "cuda" or os.environ.get("RS_CORR_SIDE", "1") == "0":
-        return None
-    from ..models.raft import OVERLAP, _SIDE_STREAMS
-    return _SIDE_STREAMS.get((dev.index, 0)) if OVERLAP.get("cnet", False) else None
-
-
-# RS_CORR_FUSED_BWD=1: the volume backward on csrc/corr_bwd.hip (pyramid-gradient
-# fold inside the MFMA GEMMs' operand staging, K split over blocks).  Opt-in:
-# paired in-situ A/B on MI355X (profiles/r4/README.md, session s11): 368 pairs/s
-# fused vs 384 pairs/s for the default -- one fold pass (pyr_fold4, bf16 G)
-# plus two hipBLASLt bf16 GEMMs, ~0.7 ms/step against ~2 ms for the fused pair
-_FUSED_BWD = os.environ.get("RS_CORR_FUSED_BWD", "0") == "1"
+_AB_LIB = os.environ.get("RS_AB_CORR_LIB", "0") == "1"  # temporary A/B knob
 
 
 class _CorrVolume(torch.autograd.Function):
@@ -96,22 +82,22 @@ class _CorrVolume(torch.autograd.Function):
             return None, None, None
         B, N1, C = f1.shape
         _, H2, W2, _ = f2.shape
-        if (f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16 and _FUSED_BWD and C in (128, 256)
-                and N1 == H2 * W2):
-            # csrc/corr_bwd.hip: the pyramid-gradient fold in the operand load of
-            # two MFMA GEMM kernels (no 130 MB G, no library GEMMs)
+        if (f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16 and C % 128 == 0 and not _AB_LIB
+                and -(-(H2 * W2) // 64) * 64 <= 6144):
+            # csrc/corr_bwd.hip: one fold pass into a padded bf16 G, then both
+            # feature-gradient GEMMs in one MFMA launch (deterministic); the
+            # row fold holds level-0 grids up to 6144 cells (1/8 of ~768 x 512)
             df1, df2 = torch.ops.raft_stir.corr_volume_backward(state.gpyr, f1.contiguous(), f2.contiguous(),
                                                                state.scale)
         elif f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16:
-            # bf16 GEMMs (fp32 accumulation) on a bf16 copy of the folded
-            # gradient: ~5x faster than the fp32 GEMMs on MI355X
+            # other channel counts / larger grids: bf16 library GEMMs on the folded gradient
             G = torch.empty(B, N1, H2 * W2, device=f1.device, dtype=torch.bfloat16)
             torch.ops.raft_stir.pyr_grad_fold_bf16(state.gpyr, state.scale, G)
-            side = _side_stream(f1.device)
+            side = None
+            if _AB_LIB:
+                from ..models.raft import OVERLAP, _SIDE_STREAMS
+                side = _SIDE_STREAMS.get((f1.device.index, 0)) if OVERLAP.get("cnet", False) else None
             if side is not None:
-                # the two GEMMs are independent and neither fills the GPU (~180
-                # workgroups each at the training shape): df2 on the side stream,
-                # which is idle between the loop backward and the encoder backward
                 main = torch.cuda.current_stream(f1.device)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
+from .conv import EPI_ADD_BF16, EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -44,8 +44,8 @@ def choose_enc_tile(P: int, cin: int, cout: int) -> int:
     return 16 if P >= 40000 else 17
 
 
-_WGRAD_DMA = os.environ.get("RS_WGRAD_DMA", "1") != "0"
-_HALO = os.environ.get("RS_ENC_HALO", "1") != "0"
+_WGRAD_DMA = True
+_HALO = True
 
 
 def _halo_ok(cin: int, cout: int) -> bool:
@@ -64,18 +64,22 @@ def _halo_ok(cin: int, cout: int) -> bool:
 
 # csrc/conv_v3.h weight-streaming tiles for the encoder 3x3 convs where they
 # measured faster than the halo / implicit-GEMM kernels (scripts/bench_enc_v3.py,
-# profiles/r5/README.md: forward 360 -> 280 us over the six fnet / cnet shapes;
+# profiles/r5/README.md: forward 364 -> 255 us over the six fnet / cnet shapes;
 # the 1/2-res 64 -> 64 conv of fnet's 16 images stays on csrc/enc_halo.hip).
 # 96 channels are read as two overlapping 64-channel windows, [0, 64) and
 # [32, 96), with zero weights on the duplicated half.
-_V3 = os.environ.get("RS_ENC_V3", "1") != "0"
+_V3 = True
+_AB_T68 = os.environ.get("RS_AB_T68", "1") == "1"   # temporary A/B knobs
+_AB_SINK = os.environ.get("RS_AB_SINK_V3", "1") == "1"
 
 
 def _v3_tile(P: int, cin: int, cout: int):
     if not _V3 or cin % 32 or cin < 64 or cout % 32:
         return None
-    if cin == 64 and cout == 64 and P >= 600000:
-        return None
+    if cin == 64 and cout == 64:
+        # 1/2-res 64 -> 64: the 8-wave 64 x 384-px tile (68) below fnet's
+        # 16-image size, where the halo kernel ties it (profiles/r5/bench_enc_v3_s13.log)
+        return None if P >= 600000 else (68 if _AB_T68 else 65)
     return 65 if cout <= 64 else 61
 
 
@@ -97,10 +101,12 @@ def _v3_weight(weight: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wpack.packed(("v3", id(weight), dgrad), [weight], layout)
 
 
-def _conv3x3_v3(xn, weight, k_in, k_out, out, tile, dgrad):
+def _conv3x3_v3(xn, weight, k_in, k_out, out, tile, dgrad, accumulate=False):
+    """``accumulate``: out (bf16) += the conv (EPI_ADD_BF16, the GradSink path)."""
     wins, _ = _v3_windows(k_in)
     wf = _v3_weight(weight, dgrad)
-    conv_fused([(xn, o, c) for o, c in wins], wf, None, 3, 3, k_out, EPI_BIAS, out, 0, tile=tile, wf=wf)
+    conv_fused([(xn, o, c) for o, c in wins], wf, None, 3, 3, k_out, EPI_ADD_BF16 if accumulate else EPI_BIAS,
+               out, 0, tile=tile, wf=wf)
 
 
 def _conv3x3_into(xn, wp, cin, cout, out, P):
@@ -241,8 +247,10 @@ class _Conv3x3(torch.autograd.Function):
         else:
             _conv3x3_into(xn, _packed(weight, False), cin, cout, out, P)
         ctx.save_for_backward(x)
-        # the skip gradient is added in the halo kernel's dgrad epilogue only
-        ctx.sink = sink if sink is not None and _halo_ok(cout, cin) and _v3_tile(P, cout, cin) is None else None
+        # the skip gradient is added in the dgrad kernel's epilogue (halo
+        # kernel: accumulate; v3 tiles: EPI_ADD_BF16)
+        ctx.sink = sink if sink is not None and ((_halo_ok(cout, cin) and (_AB_SINK or _v3_tile(P, cout, cin) is None))
+                                                 or (_AB_SINK and _v3_tile(P, cout, cin) is not None)) else None
         if ctx.sink is not None:
             ctx.sink.armed = True
         return out.permute(0, 3, 1, 2)
@@ -261,9 +269,12 @@ class _Conv3x3(torch.autograd.Function):
             sink = ctx.sink
             td = _v3_tile(P, cout, cin)
             if sink is not None and sink.dres is not None:
-                # dX = skip gradient + dgrad, accumulated in the halo kernel's epilogue
+                # dX = skip gradient + dgrad, accumulated in the dgrad kernel's epilogue
                 dxn, sink.dres = sink.dres, None
-                torch.ops.raft_stir.conv3x3_halo(dyn, _packed(weight, True), dxn, cout, cin, accumulate=True)
+                if td is not None:
+                    _conv3x3_v3(dyn, weight, cout, cin, dxn, td, True, accumulate=True)
+                else:
+                    torch.ops.raft_stir.conv3x3_halo(dyn, _packed(weight, True), dxn, cout, cin, accumulate=True)
             else:
                 dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
                 if td is not None:
@@ -279,7 +290,7 @@ class _Conv3x3(torch.autograd.Function):
 # csrc/enc_wgrad.hip: all nine taps of a 64 x 64 channel slice per block over
 # halo tiles (deterministic); every encoder 3x3 stride-1 conv (64 / 96 / 128
 # channels; 96 as two overlapping 64-channel blocks)
-_ENC_WGRAD = os.environ.get("RS_ENC_WGRAD", "1") != "0"
+_ENC_WGRAD = True
 
 
 def _enc_wgrad_op(dy, x):
@@ -320,16 +331,11 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, sink=None) -> torch.Tensor:
 # forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
 # conv epilogues (bias, eval-BN scale / shift + ReLU) and a
 # deterministic MFMA weight gradient; the image needs no input gradient.
-# RS_STEM: "auto" (default) runs the HIP stem for fp32 inference and for
-# full RAFT's bf16 inference (64 channels: 285.6 vs 283.3 FPS paired, the
-# forward staging each input row as one coalesced run), and leaves bf16
-# training and RAFT-small's 32-channel bf16 stem (2.27 vs 2.24 ms STIR) on
-# MIOpen, whose training forward + weight gradient measured faster than the
-# HIP pair (2 x 405 us forward + 500 us weight gradient vs 2 x 73 + 2 x 111 us
-# with the first, gather-staged forward; profiles/r3/README.md);
-# "infer": all inference; "f32": fp32 inference only; "1": always; "0": never.
-_STEM_MODE = os.environ.get("RS_STEM", "auto")
-_STEM = _STEM_MODE != "0"
+# Every mode but fp32 training (which keeps the module graph) runs here:
+# bf16 training (forward + weight gradient), bf16 / fp32 inference, both
+# encoders and RAFT-small's 32-channel stem (scripts/bench_stem.py).
+_STEM = True
+_AB_STEM = os.environ.get("RS_AB_STEM", "1") == "1"  # temporary A/B knob
 
 
 def _stem_layout(ws):
@@ -355,11 +361,7 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     f32 = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32
     if f32 and torch.is_grad_enabled() and conv.weight.requires_grad:
         return False  # fp32 training: the module graph
-    if _STEM_MODE == "f32" and not f32:
-        return False
-    if _STEM_MODE in ("infer", "auto") and torch.is_grad_enabled() and conv.weight.requires_grad:
-        return False
-    if _STEM_MODE == "auto" and not f32 and conv.out_channels != 64:
+    if not _AB_STEM and torch.is_grad_enabled() and conv.weight.requires_grad:
         return False
     return x.numel() * 4 < (1 << 31)
 
@@ -419,7 +421,7 @@ def stem_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool) -> tor
 # tiles of csrc/conv.hip: every stride-1 / stride-2 3x3 and 1x1 encoder conv,
 # no autograd (fp32 training keeps the module graph).  Weights in the split
 # [wh | wl] layout through the same packed-weight registry (wpack.packed_split).
-_F32_ENC = os.environ.get("RS_F32_ENC", "1") != "0"
+_F32_ENC = True
 
 
 def _split_weight(weight: torch.Tensor) -> torch.Tensor:
@@ -492,7 +494,7 @@ def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, scale=None, sh
 #             ~2^-16 relative, the same scheme as the fused update block;
 #   bias    : column sum of dY in fp32 (the projection head only; the other
 #             convs' biases fold into their normalisation).
-_F32_TRAIN = os.environ.get("RS_F32_ENC_TRAIN", "1") != "0"
+_F32_TRAIN = True
 
 
 def _f32_shape_ok(conv: nn.Conv2d) -> bool:
@@ -647,7 +649,7 @@ def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residu
 #             the 1x1 shortcut only has the (0, 0) phase and is fused into the
 #             3x3's (0, 0) phase as a second K segment (conv_pair)
 #   wgrad   : split-K MFMA over dY pixels with strided X rows
-_GEO = os.environ.get("RS_ENC_GEO", "1") != "0"
+_GEO = True
 _GEO_SCOPE = [True]  # per-encoder switch (geo_scope): RAFT-small's encoder keeps MIOpen
 
 
@@ -910,7 +912,7 @@ def conv_pair(conv1: nn.Conv2d, down: nn.Conv2d, x: torch.Tensor):
 # 1x1 / 3x3 convs of 8-96 channels; at inference they go to csrc/sconv.hip
 # (VALU, fp32 accumulation, bias / ReLU / residual in the epilogue, bf16 or
 # fp32 NHWC) instead of MIOpen + a bias kernel + an autocast weight cast.
-_SCONV = os.environ.get("RS_SCONV", "1") != "0"
+_SCONV = True
 
 
 def sconv_eligible(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:

@@ -16,7 +16,6 @@ Everything else (CPU, export, GroupNorm, identity) takes the composite path.
 """
 from __future__ import annotations
 
-import os
 import weakref
 
 import torch
@@ -29,7 +28,7 @@ from . import fp32conv
 from ..runtime import weights
 
 _CL = torch.channels_last
-_FOLD_BIAS = os.environ.get("RS_FOLD_BIAS", "1") != "0"
+_FOLD_BIAS = True
 
 
 def _nhwc(x):

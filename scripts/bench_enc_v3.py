@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--size", type=int, nargs=2, default=[368, 496])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tiles", type=int, nargs="+", default=[60, 61, 63, 65])
+    ap.add_argument("--wgrad", action="store_true", help="also time the weight gradients (enc_wgrad vs wgrad_v3)")
     a = ap.parse_args()
     from raft_stir_amd.ops import _ext
     from raft_stir_amd.ops.conv import EPI_BIAS, conv_fused, frag_weight, pack_weight, pad_to
@@ -75,6 +76,17 @@ def main():
             line += f" t{t} {tt:7.1f}us {flop / tt / 1e6:5.0f}TF ({e:.0e}) |"
             best = tt if best is None else min(best, tt)
         tot["v3best"] = tot.get("v3best", 0.0) + best
+        if a.wgrad:
+            dy = (torch.randn(n, h, w, cout, device=dev) * 0.5).to(torch.bfloat16)
+            t_e = timeit(lambda: torch.ops.raft_stir.enc_wgrad(dy, x), a.reps)
+            line += f" enc_wgrad {t_e:7.1f}us |"
+            tot["enc_wgrad"] = tot.get("enc_wgrad", 0.0) + t_e
+            if cin % 64 == 0:
+                dw = torch.zeros(cout, 9, cin, device=dev)
+                for bm in (64, 128):
+                    t3 = timeit(lambda: torch.ops.raft_stir.wgrad_v3(dy, 0, cout, [x], [0], [cin], [P], 3, 3, dw, None, bm),
+                                a.reps)
+                    line += f" wg3/{bm} {t3:7.1f}us |"
         print(line, flush=True)
     print("sum (us):", {k: round(v, 1) for k, v in tot.items()})
 

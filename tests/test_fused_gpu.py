@@ -8,7 +8,7 @@ import torch.nn.functional as F
 
 from raft_stir_amd.config import make_args
 from raft_stir_amd.models import RAFT
-from raft_stir_amd.ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR,
+from raft_stir_amd.ops.conv import (EPI_ACC_F32, EPI_ADD_BF16, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR,
                                     EPI_RELU, EPI_RELU_BWD, EPI_SCALE, V3_TILES, conv_fused, frag_weight,
                                     pack_bias, pack_weight, pad_to)
 
@@ -114,6 +114,29 @@ def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
     got = out[..., :cout].float().permute(0, 3, 1, 2)
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
     assert (out[..., cout:] == 7).all()
+
+
+@pytest.mark.parametrize("tile", [44, 52, 61, 66, 68])
+@pytest.mark.parametrize("cout", [96, 70])
+def test_conv_add_bf16_epilogue(cuda, tile, cout):
+    """EPI_ADD_BF16 (out(bf16) += conv, the encoder GradSink dgrad): the
+    batched 32-row epilogue (cout 96) and the element-wise form (cout 70,
+    a partial last fragment) against out0 + conv2d; the channels past the
+    window keep their values."""
+    torch.manual_seed(8)
+    B, H, W = 2, 13, 37
+    x = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
+    w = torch.randn(cout, 64, 3, 3, device=cuda) * 0.05
+    wp = pack_weight(w, [(64, [(0, 64, 0)])], pad_to(cout, 256))
+    out0 = torch.randn(B, H, W, cout + 4, device=cuda).to(torch.bfloat16)
+    out = out0.clone()
+    conv_fused([(x, 0, 64)], wp, None, 3, 3, cout, EPI_ADD_BF16, out, 0, tile=tile,
+               wf=frag_weight(wp) if tile in V3_TILES else None)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), _bf(w), None, padding=1) + out0[..., :cout].float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(out[..., :cout].float().permute(0, 3, 1, 2), ref, atol=3e-2, rtol=2e-2)
+    assert torch.equal(out[..., cout:], out0[..., cout:])
+    with pytest.raises(RuntimeError, match="EPI_ADD_BF16"):
+        conv_fused([(x, 0, 64)], wp, None, 3, 3, cout, EPI_ADD_BF16, out, 0, tile=0)
 
 
 @pytest.mark.parametrize("epi", [EPI_GRU_ZR, EPI_GRU_Q, EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_SCALE])

@@ -381,9 +381,10 @@ def test_pyr_grad_fold(cuda, HW, out_bf16):
 def test_corr_volume_backward_fused(cuda, HW, C, det):
     """csrc/corr_bwd.hip: df1 = G f2 and df2 = G^T f1 with G the folded
     pyramid gradient (avg-pool adjoint of every level onto level 0, times
-    1/sqrt(C)) computed inside the GEMMs' operand staging, vs fp32 PyTorch
-    (fold by gather, then two bmm).  (11, 37): N = 407, ragged M and K tiles
-    and an odd row pitch (the scalar staging path)."""
+    1/sqrt(C), bf16 rows zero-padded to a multiple of 64), both GEMMs in one
+    MFMA launch, vs fp32 PyTorch (fold by gather, then two bmm).  (11, 37):
+    N = 407, ragged M and K tiles; deterministic in both modes (bitwise
+    repeat)."""
     H, W = HW
     N = H * W
     B, levels, scale = 2, 4, 1.0 / math.sqrt(C)
@@ -401,13 +402,11 @@ def test_corr_volume_backward_fused(cuda, HW, C, det):
     G = (G * scale).view(B, N, N)
     want1 = torch.bmm(G, f2.float().view(B, N, C))
     want2 = torch.bmm(G.transpose(1, 2), f1.float()).view(B, H, W, C)
-    # default: K split over blocks (fp32 atomics); deterministic mode: one block per row range
     torch.ops.raft_stir.set_deterministic(det)
     try:
         df1, df2 = torch.ops.raft_stir.corr_volume_backward(gpyr, f1, f2, scale)
-        if det:
-            r1, r2 = torch.ops.raft_stir.corr_volume_backward(gpyr, f1, f2, scale)
-            assert torch.equal(df1, r1) and torch.equal(df2, r2)
+        r1, r2 = torch.ops.raft_stir.corr_volume_backward(gpyr, f1, f2, scale)
+        assert torch.equal(df1, r1) and torch.equal(df2, r2)
     finally:
         torch.ops.raft_stir.set_deterministic(False)
     assert df1.dtype == torch.bfloat16 and df1.shape == f1.shape and df2.shape == f2.shape

@@ -75,10 +75,13 @@ def test_stem_eval_bn(cuda, f32):
 
 
 @pytest.mark.parametrize("cout", [64, 32])
-def test_stem_wgrad(cuda, cout):
+@pytest.mark.parametrize("shape", [(2, 75, 99), (4, 184, 300)])
+def test_stem_wgrad(cuda, cout, shape):
+    """64-pixel row chunks: one partial chunk per row (Wo = 50) and three
+    per row with a partial last one (Wo = 150); blocks span row boundaries."""
     torch.manual_seed(5)
     conv = nn.Conv2d(3, cout, 7, stride=2, padding=3).to(cuda)
-    x = _img(2, 75, 99, cuda, 5)
+    x = _img(*shape, cuda, 5)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = enc_conv.stem(conv, x)
     g = torch.randn_like(y.float()).to(torch.bfloat16)
