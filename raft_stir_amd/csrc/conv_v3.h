@@ -114,7 +114,9 @@ __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
 
   const int t_ = threadIdx.x, lane = t_ & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t_ >> 6);
-  const int cw = wave % NWM, pw = wave / NWM;  // output-channel slice, patch-row group of this wave
+  // output-channel slice, patch-row group of this wave (NWP == 1: constants,
+  // so the single-group tiles compile to the same code as before NWP existed)
+  const int cw = NWP == 1 ? wave : wave % NWM, pw = NWP == 1 ? 0 : wave / NWM;
   const int H = a.H, W = a.W;
   const int ntx = cdiv(W, 32), npb = cdiv(H, TH) * ntx;
   const int nct = cdiv(a.Cout, BM);

@@ -4,7 +4,7 @@
 // core/corr.py:24-27).
 //
 // The lookups' backward accumulated the gradient of every pyramid level; one
-// fold pass (corr_lookup.hip pyr_fold4_kernel) turns it into the bf16
+// fold pass (corr_lookup.hip pyr_fold_rows_kernel) turns it into the bf16
 // level-0 volume gradient G[b][p1][p2] (scale and every level's avg-pool
 // adjoint applied), rows padded with zeros to a multiple of 64 (pitch Ep).
 // The features' gradients are then, per batch image b,
@@ -29,7 +29,9 @@
 //    (counted lgkmcnt waits; the LDS reads are inline asm so the compiler does
 //    not drain the in-flight DMA in front of them);
 //  * fp32 accumulation, bf16 output rows written once: no atomics, no
-//    split-K -- deterministic by construction.
+//    split-K -- deterministic by construction;
+//  * fp32 training: the operands as bf16 hi / lo pairs and three K passes
+//    (hi.hi + hi.lo + lo.hi, ~2^-16 relative error), fp32 output.
 #include "common.h"
 
 #include <algorithm>
@@ -44,8 +46,13 @@ struct Args {
   const bf16_t* G;   // [B][N1][Ep]
   const bf16_t* f1;  // [B][N1][C]
   const bf16_t* f2;  // [B][N2][C]
-  bf16_t* d1;        // [B][N1][C]
-  bf16_t* d2;        // [B][N2][C]
+  void* d1;          // [B][N1][C] bf16 (fp32: split mode)
+  void* d2;          // [B][N2][C]
+  // split mode (fp32 operands as bf16 hi + lo pairs): x.y ~= xh.yh + xh.yl + xl.yh,
+  // three K passes over (G hi, f hi), (G hi, f lo), (G lo, f hi), fp32 output
+  const bf16_t* Gl;
+  const bf16_t* f1l;
+  const bf16_t* f2l;
   unsigned g_bytes, f1_bytes, f2_bytes;
   int B, N1, N2, C, Ep;
   int nm1, nm2, nn;  // M tiles of each GEMM, channel tiles
@@ -141,8 +148,9 @@ __device__ __forceinline__ void mfma4(f32x16_t (&acc)[2][2], Frags<TA>& f) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// TA = false: D1 = G F2 (A rows = G rows); TA = true: D2 = G^T F1 (A = G columns)
-template <bool TA>
+// TA = false: D1 = G F2 (A rows = G rows); TA = true: D2 = G^T F1 (A = G columns).
+// NP = 3: split mode (hi / lo K passes, fp32 output).
+template <bool TA, int NP>
 __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, int mt, int nt) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,6 +160,12 @@ __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, in
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.G, (short)0, a.g_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rf = TA ? __builtin_amdgcn_make_buffer_rsrc((void*)a.f1, (short)0, a.f1_bytes, 0x00020000)
                                        : __builtin_amdgcn_make_buffer_rsrc((void*)a.f2, (short)0, a.f2_bytes, 0x00020000);
+  // split mode: the lo halves (same shapes and byte counts)
+  const __amdgpu_buffer_rsrc_t rgl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(NP == 3 ? a.Gl : a.G), (short)0, a.g_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rfl =
+      TA ? __builtin_amdgcn_make_buffer_rsrc((void*)(NP == 3 ? a.f1l : a.f1), (short)0, a.f1_bytes, 0x00020000)
+         : __builtin_amdgcn_make_buffer_rsrc((void*)(NP == 3 ? a.f2l : a.f2), (short)0, a.f2_bytes, 0x00020000);
   const long gbase = (long)b * a.N1;   // first G row of this image
   const long fbase = (long)b * K;      // first feature row (the K rows)
 
@@ -174,11 +188,14 @@ __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, in
     bro[i] = r;
     bco[i] = 8 * chunk_kmajor(r, s & 15);
   }
-  const int nk = cdiv(K, BK);
+  const int nk1 = cdiv(K, BK), nk = NP * nk1;  // K steps of one pass, of all passes
   auto issue = [&](int kt, int st) {
     const uint8_t* sb = lds + st * STAGE;
     const bool live = kt < nk;
-    const int k0 = kt * BK;
+    const int pass = NP == 1 ? 0 : kt / nk1;  // 0: (hi, hi), 1: (hi, lo), 2: (lo, hi)
+    const int k0 = (kt - pass * nk1) * BK;
+    const __amdgpu_buffer_rsrc_t ra = pass == 2 ? rgl : rg;
+    const __amdgpu_buffer_rsrc_t rb = pass == 1 ? rfl : rf;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int v;
@@ -188,12 +205,12 @@ __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, in
         // columns k0 .. k0+63 < Ep always (Ep = round_up(N2, 64), zero pad)
         v = (live && m0 + aro[i] < M) ? (int)(((gbase + m0 + aro[i]) * Ep + k0 + aco[i]) * 2) : kFar;
       }
-      dma16(rg, sb + (wave + 4 * i) * 1024, v);
+      dma16(ra, sb + (wave + 4 * i) * 1024, v);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int v = (live && k0 + bro[i] < K) ? (int)(((fbase + k0 + bro[i]) * C + n0 + bco[i]) * 2) : kFar;
-      dma16(rf, sb + TILE + (wave + 4 * i) * 1024, v);
+      dma16(rb, sb + TILE + (wave + 4 * i) * 1024, v);
     }
   };
 
@@ -254,7 +271,6 @@ __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, in
   wait_vm<0>();
 
   // ---- epilogue: acc[i][j] reg r -> row m0 + wm*64 + 32i + (r&3) + 8(r>>2) + 4h, channel n0 + wn*64 + 32j + lane&31
-  bf16_t* out = TA ? a.d2 : a.d1;
   const long obase = (long)b * M;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -263,23 +279,29 @@ __device__ __forceinline__ void gemm_tile(const Args& a, uint8_t* lds, int b, in
       const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (m < M) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          out[(obase + m) * C + n0 + wn * 64 + 32 * j + (lane & 31)] = f2bf(acc[i][j][r]);
+        for (int j = 0; j < 2; ++j) {
+          const long o = (obase + m) * C + n0 + wn * 64 + 32 * j + (lane & 31);
+          if constexpr (NP == 3)
+            static_cast<float*>(TA ? a.d2 : a.d1)[o] = acc[i][j][r];
+          else
+            static_cast<bf16_t*>(TA ? a.d2 : a.d1)[o] = f2bf(acc[i][j][r]);
+        }
       }
     }
 }
 
-__global__ __launch_bounds__(256, 2) void corr_bwd_gemm_kernel(Args a) {
+template <int NP>
+__global__ __launch_bounds__(256) void corr_bwd_gemm_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
   const int nblk1 = a.B * a.nm1 * a.nn;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   if (lid < nblk1) {
     const int nt = lid % a.nn, r = lid / a.nn;
-    gemm_tile<false>(a, lds, r / a.nm1, r % a.nm1, nt);
+    gemm_tile<false, NP>(a, lds, r / a.nm1, r % a.nm1, nt);
   } else {
     const int l2 = lid - nblk1;
     const int nt = l2 % a.nn, r = l2 / a.nn;
-    gemm_tile<true>(a, lds, r / a.nm2, r % a.nm2, nt);
+    gemm_tile<true, NP>(a, lds, r / a.nm2, r % a.nm2, nt);
   }
 }
 
@@ -288,15 +310,19 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_gemm_kernel(Args a) {
 int corr_bwd_pitch(int N2) { return round_up(N2, cgemm::BK); }
 
 // G [B][N1][Ep] bf16 (Ep = corr_bwd_pitch(N2), zero columns past N2); f1 [B][N1][C], f2 [B][N2][C] bf16,
-// C % 128 == 0 -> df1 [B][N1][C], df2 [B][N2][C] bf16
-void corr_bwd_gemm_launch(const void* G, int Ep, const void* f1, const void* f2, int B, int N1, int N2, int C,
-                          void* df1, void* df2, hipStream_t stream) {
+// C % 128 == 0 -> df1 [B][N1][C], df2 [B][N2][C] bf16.  Gl / f1l / f2l non-null: split mode, the lo
+// halves of fp32 operands (same layouts) -> fp32 df1 / df2.
+void corr_bwd_gemm_launch(const void* G, const void* Gl, int Ep, const void* f1, const void* f1l, const void* f2,
+                          const void* f2l, int B, int N1, int N2, int C, void* df1, void* df2, hipStream_t stream) {
   cgemm::Args a{};
   a.G = static_cast<const bf16_t*>(G);
   a.f1 = static_cast<const bf16_t*>(f1);
   a.f2 = static_cast<const bf16_t*>(f2);
-  a.d1 = static_cast<bf16_t*>(df1);
-  a.d2 = static_cast<bf16_t*>(df2);
+  a.Gl = static_cast<const bf16_t*>(Gl);
+  a.f1l = static_cast<const bf16_t*>(f1l);
+  a.f2l = static_cast<const bf16_t*>(f2l);
+  a.d1 = df1;
+  a.d2 = df2;
   a.g_bytes = (unsigned)((long)B * N1 * Ep * 2);
   a.f1_bytes = (unsigned)((long)B * N1 * C * 2);
   a.f2_bytes = (unsigned)((long)B * N2 * C * 2);
@@ -306,7 +332,10 @@ void corr_bwd_gemm_launch(const void* G, int Ep, const void* f1, const void* f2,
   a.nn = C / cgemm::BN;
   const int nblk = B * (a.nm1 + a.nm2) * a.nn;
   if (nblk == 0) return;
-  hipLaunchKernelGGL(cgemm::corr_bwd_gemm_kernel, dim3(nblk), dim3(256), 0, stream, a);
+  if (Gl != nullptr)
+    hipLaunchKernelGGL(cgemm::corr_bwd_gemm_kernel<3>, dim3(nblk), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(cgemm::corr_bwd_gemm_kernel<1>, dim3(nblk), dim3(256), 0, stream, a);
 }
 
 }  // namespace rs

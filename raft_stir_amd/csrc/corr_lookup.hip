@@ -366,7 +366,8 @@ __global__ __launch_bounds__(256) void pyr_fold4_kernel(PyrMut g, int levels, in
 constexpr int FOLD_LDS = 4096;
 
 __global__ __launch_bounds__(256) void pyr_fold_rows_kernel(PyrMut g, int levels, float scale,
-                                                            bf16_t* __restrict__ out, int OP, int vec0) {
+                                                            bf16_t* __restrict__ out, bf16_t* __restrict__ out_lo,
+                                                            int OP, int vec0) {
   __shared__ float cl[FOLD_LDS];
   const int row = blockIdx.x;
   const int H0 = g.H[0], W0 = g.W[0], E = H0 * W0;
@@ -431,9 +432,21 @@ __global__ __launch_bounds__(256) void pyr_fold_rows_kernel(PyrMut g, int levels
         }
       }
     }
-    const uint2 pk = make_uint2(uint32_t(f2bf(f[0] * scale)) | (uint32_t(f2bf(f[1] * scale)) << 16),
-                                uint32_t(f2bf(f[2] * scale)) | (uint32_t(f2bf(f[3] * scale)) << 16));
-    *reinterpret_cast<uint2*>(out + (size_t)row * OP + e) = pk;
+    bf16_t hv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[k] *= scale;
+      hv[k] = f2bf(f[k]);
+    }
+    *reinterpret_cast<uint2*>(out + (size_t)row * OP + e) =
+        make_uint2(uint32_t(hv[0]) | (uint32_t(hv[1]) << 16), uint32_t(hv[2]) | (uint32_t(hv[3]) << 16));
+    if (out_lo != nullptr) {  // split-bf16 operand: lo = bf16(x - hi)
+      bf16_t lv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lv[k] = f2bf(f[k] - bf2f(hv[k]));
+      *reinterpret_cast<uint2*>(out_lo + (size_t)row * OP + e) =
+          make_uint2(uint32_t(lv[0]) | (uint32_t(lv[1]) << 16), uint32_t(lv[2]) | (uint32_t(lv[3]) << 16));
+    }
   }
 }
 
@@ -518,8 +531,9 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                        levels, coords, B, H1, W1, r, static_cast<const float*>(dout), total, dstride);
 }
 
+// out_lo (row fold only): the lo halves of a split-bf16 output
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
-                          float scale, hipStream_t stream, void* out_bf16, int opitch) {
+                          float scale, hipStream_t stream, void* out_bf16, int opitch, void* out_lo) {
   lookup::PyrMut p;
   for (int l = 0; l < 4; ++l) {
     p.p[l] = l < levels ? gpyr[l] : nullptr;
@@ -536,7 +550,7 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, cons
   if (out_bf16 && opitch % 4 == 0 && opitch <= 6144 && coarse <= lookup::FOLD_LDS && rows < (1L << 31)) {
     const int vec0 = Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0;
     hipLaunchKernelGGL(lookup::pyr_fold_rows_kernel, dim3((unsigned)rows), dim3(256), 0, stream, p, levels, scale,
-                       static_cast<bf16_t*>(out_bf16), opitch, vec0);
+                       static_cast<bf16_t*>(out_bf16), static_cast<bf16_t*>(out_lo), opitch, vec0);
     return;
   }
   if (Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0 && rows < (1L << 31) &&

@@ -86,6 +86,18 @@ struct Args {
   float inv_n;
 };
 
+// BatchNorm running-statistics update, applied by finalize_kernel<0> for
+// batch statistics (reference nn.BatchNorm2d train mode, momentum form):
+//   running_mean = (1-m) running_mean + m (mean + bias)
+//   running_var  = (1-m) running_var  + m var * n/(n-1),  var = rstd^-2 - eps
+struct Running {
+  float* rm;            // null: no update
+  float* rv;
+  long long* nbt;
+  const float* bias;
+  float mom, unb;
+};
+
 // --------------------------------------------------------------- reductions
 // MODE 0: (x, x^2).  MODE 1: (g, g * xhat) with g the gradient reaching the
 // pre-activation a = gamma * xhat + beta.
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
 // (short serial chains: batch-norm groups have B * S partials per channel).
 template <int MODE>
 __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, int S, int C, int G,
-                                                       float eps, float inv_n, float* o0, float* o1) {
+                                                       float eps, float inv_n, float* o0, float* o1, Running run) {
   const int g = blockIdx.x;
   const int c = blockIdx.y * 8 + (threadIdx.x & 7);
   const int part = threadIdx.x >> 3;
@@ -240,8 +252,16 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, i
       const double m = t0 * inv_n;
       double var = t1 * inv_n - m * m;
       var = var < 0.0 ? 0.0 : var;
+      const float r = (float)(1.0 / sqrt(var + (double)eps));
       o0[idx] = (float)m;
-      o1[idx] = (float)(1.0 / sqrt(var + (double)eps));
+      o1[idx] = r;
+      if (run.rm != nullptr) {  // G == 1 (checked by the host)
+        const float vf = fmaxf(1.f / (r * r) - eps, 0.f);
+        const float bm = (float)m + (run.bias ? run.bias[c] : 0.f);
+        run.rm[c] = (1.f - run.mom) * run.rm[c] + run.mom * bm;
+        run.rv[c] = (1.f - run.mom) * run.rv[c] + run.mom * vf * run.unb;
+        if (c == 0 && run.nbt != nullptr) run.nbt[0] += 1;
+      }
     } else {
       o0[idx] = (float)t0;
       o1[idx] = (float)t1;
@@ -401,27 +421,6 @@ int grid_elem(size_t nvec) {
   return (int)(g < 8192 ? g : 8192);
 }
 
-// BatchNorm running-statistics update from the batch statistics (reference
-// semantics of nn.BatchNorm2d in train mode, momentum form):
-//   running_mean = (1-m) running_mean + m (mean + bias)
-//   running_var  = (1-m) running_var  + m var * n/(n-1),  var = rstd^-2 - eps
-// One launch instead of ~10 elementwise ATen kernels per BN layer.
-__global__ __launch_bounds__(256) void bn_running_kernel(const float* __restrict__ mean,
-                                                         const float* __restrict__ rstd,
-                                                         const float* __restrict__ bias, int C, float eps,
-                                                         float mom, float unb, float* __restrict__ rmean,
-                                                         float* __restrict__ rvar, long long* nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < C) {
-    const float r = rstd[c];
-    const float var = fmaxf(1.f / (r * r) - eps, 0.f);
-    const float bm = mean[c] + (bias ? bias[c] : 0.f);
-    rmean[c] = (1.f - mom) * rmean[c] + mom * bm;
-    rvar[c] = (1.f - mom) * rvar[c] + mom * var * unb;
-  }
-  if (c == 0 && nbt) nbt[0] += 1;
-}
-
 }  // namespace norm
 
 // ------------------------------------------------------------------ launchers
@@ -430,8 +429,10 @@ int norm_ws_floats(int B, int P, int C, bool bf16) {
   return B * S * C * 2;
 }
 
+// rm / rv / nbt / rbias: the BatchNorm running update (G == 1; rm null: none)
 void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, float eps, float* ws,
-                       float* mean, float* rstd, hipStream_t s) {
+                       float* mean, float* rstd, float* rm, float* rv, long long* nbt, const float* rbias,
+                       float mom, float unb, hipStream_t s) {
   norm::Args a{};
   a.x = x;
   a.B = B; a.P = P; a.C = C; a.G = G;
@@ -443,8 +444,9 @@ void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, flo
   else
     hipLaunchKernelGGL((norm::reduce_kernel<float, 0>), grid, dim3(norm::THREADS), 0, s, a);
   const float inv_n = 1.f / (float)((G == 1 ? (double)B : 1.0) * P);
+  const norm::Running run{rm, rv, nbt, rbias, mom, unb};
   hipLaunchKernelGGL(norm::finalize_kernel<0>, dim3(G, cdiv(C, 8)), dim3(256), 0, s, ws, B, a.S,
-                     C, G, eps, inv_n, mean, rstd);
+                     C, G, eps, inv_n, mean, rstd, run);
 }
 
 void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mean,
@@ -474,7 +476,7 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
   else
     hipLaunchKernelGGL((norm::reduce_kernel<float, 1>), grid, dim3(norm::THREADS), 0, s, a);
   hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 8)), dim3(256), 0, s, ws, B, a.S,
-                     C, G, 0.f, 0.f, s1, s2);
+                     C, G, 0.f, 0.f, s1, s2, norm::Running{});
   a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres;
   a.inv_n = batch_stats ? 1.f / (float)((G == 1 ? (double)B : 1.0) * P) : 0.f;
   a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
@@ -482,12 +484,6 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
     hipLaunchKernelGGL(norm::apply_bwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
   else
     hipLaunchKernelGGL(norm::apply_bwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
-}
-
-void bn_running_launch(const float* mean, const float* rstd, const float* bias, int C, float eps, float mom,
-                       float unb, float* rmean, float* rvar, long long* nbt, hipStream_t s) {
-  hipLaunchKernelGGL(norm::bn_running_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, mean, rstd, bias, C, eps, mom,
-                     unb, rmean, rvar, nbt);
 }
 
 }  // namespace rs

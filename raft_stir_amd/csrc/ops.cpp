@@ -37,10 +37,11 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                             bool dout_bf16, hipStream_t stream, int dstride);
 size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
 int corr_bwd_pitch(int N2);
-void corr_bwd_gemm_launch(const void* G, int Ep, const void* f1, const void* f2, int B, int N1, int N2, int C,
-                          void* df1, void* df2, hipStream_t stream);
+void corr_bwd_gemm_launch(const void* G, const void* Gl, int Ep, const void* f1, const void* f1l, const void* f2,
+                          const void* f2l, int B, int N1, int N2, int C, void* df1, void* df2, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
-                          float scale, hipStream_t stream, void* out_bf16 = nullptr, int opitch = 0);
+                          float scale, hipStream_t stream, void* out_bf16 = nullptr, int opitch = 0,
+                          void* out_lo = nullptr);
 void wpack_gather_launch(const int* code, long long n, const long long* tab, void* out, bool out_bf16,
                          const long long* lo, const long long* hi, const float* s, int nr, hipStream_t stream);
 void split_bf16_launch(const float* x, long n, uint16_t* hi, uint16_t* lo, hipStream_t s);
@@ -277,13 +278,16 @@ void pyr_grad_fold_bf16(const std::vector<Tensor>& gpyr, double scale, const Ten
 // Volume backward (csrc/corr_bwd.hip): the gradient pyramid folded once into
 // a bf16 level-0 gradient G (rows padded to a multiple of 64 with zeros), then
 // both feature-gradient GEMMs (df1 = G f2, df2 = G^T f1) in one MFMA launch.
-// bf16 features, C % 128 == 0; deterministic (no atomics).
+// bf16 features -> bf16 gradients; fp32 features -> fp32 gradients through
+// split-bf16 operands (G and the features as hi + lo pairs, three K passes).
+// C % 128 == 0; deterministic (no atomics).
 std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const Tensor& f1, const Tensor& f2,
                                          double scale) {
   check_gpu(f1, "f1");
   check_gpu(f2, "f2");
-  check_dtype(f1, {at::kBFloat16}, "f1");
-  check_dtype(f2, {at::kBFloat16}, "f2");
+  check_dtype(f1, {at::kBFloat16, at::kFloat}, "f1");
+  TORCH_CHECK(f2.scalar_type() == f1.scalar_type(), "corr_volume_backward: f1 / f2 dtypes differ");
+  const bool split = f1.scalar_type() == at::kFloat;
   TORCH_CHECK(f1.dim() == 3 && f1.is_contiguous(), "corr_volume_backward: f1 must be contiguous (B, N1, C)");
   TORCH_CHECK(f2.dim() == 4 && f2.is_contiguous(), "corr_volume_backward: f2 must be contiguous (B, H2, W2, C)");
   const int B = f1.size(0), N1 = f1.size(1), C = f1.size(2);
@@ -296,18 +300,39 @@ std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const 
   const int Ep = rs::corr_bwd_pitch(N2);
   int64_t coarse = 0;
   for (size_t l = 1; l < gpyr.size(); ++l) coarse += (int64_t)Hs[l] * Ws[l];
-  TORCH_CHECK(Ep <= 6144 && coarse <= 4096, "corr_volume_backward: level-0 grid too large for the row fold");
+  const bool rowfold = Ep <= 6144 && coarse <= 4096;
+  // the row fold (<= 6144 cells; the only one with a split output) or, for
+  // larger bf16 grids, the quad fold (16-B aligned level-0 rows)
+  TORCH_CHECK(rowfold || (!split && Ss[0] % 4 == 0 && (uintptr_t)gpyr[0].data_ptr() % 16 == 0),
+              "corr_volume_backward: grids over 6144 cells need bf16 features and 16-B aligned level-0 rows");
   TORCH_CHECK((int64_t)B * N1 * Ep * 2 < (int64_t(1) << 31) && (int64_t)B * std::max(N1, N2) * C * 2 < (int64_t(1) << 31),
               "corr_volume_backward: operands must be < 2 GiB");
   const c10::DeviceGuard guard(f1.device());
-  Tensor G = at::empty({(int64_t)B * N1, Ep}, f1.options());
+  auto bo = f1.options().dtype(at::kBFloat16);
+  Tensor G = at::empty({(int64_t)B * N1, Ep}, bo);
+  Tensor Gl = split ? at::empty({(int64_t)B * N1, Ep}, bo) : Tensor();
   float* ptrs[4];
   for (size_t l = 0; l < gpyr.size(); ++l) ptrs[l] = gpyr[l].data_ptr<float>();
-  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), G.data_ptr(), Ep);
+  rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), G.data_ptr(), Ep,
+                           split ? Gl.data_ptr() : nullptr);
   RS_CHECK_LAUNCH();
   Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
-  rs::corr_bwd_gemm_launch(G.data_ptr(), Ep, f1.data_ptr(), f2.data_ptr(), B, N1, N2, C, df1.data_ptr(),
-                           df2.data_ptr(), cur_stream());
+  if (split) {
+    TORCH_CHECK((uintptr_t)f1.data_ptr() % 16 == 0 && (uintptr_t)f2.data_ptr() % 16 == 0,
+                "corr_volume_backward: fp32 features must be 16-B aligned");
+    Tensor h1 = at::empty(f1.sizes(), bo), l1 = at::empty(f1.sizes(), bo);
+    Tensor h2 = at::empty(f2.sizes(), bo), l2 = at::empty(f2.sizes(), bo);
+    rs::split_bf16_launch(f1.data_ptr<float>(), f1.numel(), reinterpret_cast<uint16_t*>(h1.data_ptr()),
+                          reinterpret_cast<uint16_t*>(l1.data_ptr()), cur_stream());
+    rs::split_bf16_launch(f2.data_ptr<float>(), f2.numel(), reinterpret_cast<uint16_t*>(h2.data_ptr()),
+                          reinterpret_cast<uint16_t*>(l2.data_ptr()), cur_stream());
+    RS_CHECK_LAUNCH();
+    rs::corr_bwd_gemm_launch(G.data_ptr(), Gl.data_ptr(), Ep, h1.data_ptr(), l1.data_ptr(), h2.data_ptr(),
+                             l2.data_ptr(), B, N1, N2, C, df1.data_ptr(), df2.data_ptr(), cur_stream());
+  } else {
+    rs::corr_bwd_gemm_launch(G.data_ptr(), nullptr, Ep, f1.data_ptr(), nullptr, f2.data_ptr(), nullptr, B, N1, N2, C,
+                             df1.data_ptr(), df2.data_ptr(), cur_stream());
+  }
   RS_CHECK_LAUNCH();
   return {df1, df2};
 }

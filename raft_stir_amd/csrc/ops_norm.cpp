@@ -9,7 +9,8 @@
 namespace rs {
 int norm_ws_floats(int B, int P, int C, bool bf16);
 void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, float eps, float* ws,
-                       float* mean, float* rstd, hipStream_t s);
+                       float* mean, float* rstd, float* rm, float* rv, long long* nbt, const float* rbias,
+                       float mom, float unb, hipStream_t s);
 void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, void* y, hipStream_t s);
@@ -17,8 +18,6 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
                      void* dres, hipStream_t s);
-void bn_running_launch(const float* mean, const float* rstd, const float* bias, int C, float eps, float mom,
-                       float unb, float* rmean, float* rvar, long long* nbt, hipStream_t s);
 }  // namespace rs
 
 namespace {
@@ -50,17 +49,30 @@ void check_param(const c10::optional<Tensor>& t, int64_t C, const char* n) {
 
 const float* fptr(const c10::optional<Tensor>& t) { return t ? t->data_ptr<float>() : nullptr; }
 
-std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps) {
+// running_mean / running_var / nbt (+ bias, the producing conv's bias folded
+// into the statistics): the train-mode BatchNorm running update, fused into
+// the statistics launch (batch statistics only).
+std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps, const c10::optional<Tensor>& rmean,
+                               const c10::optional<Tensor>& rvar, const c10::optional<Tensor>& nbt,
+                               const c10::optional<Tensor>& bias, double momentum, int64_t n) {
   check_x(x);
   const c10::DeviceGuard g(x.device());
   const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
   const int G = per_sample ? B : 1;
   const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bool(rmean) == bool(rvar) && (!rmean || !per_sample), "norm_stats: running stats need batch statistics");
+  check_param(rmean, C, "running_mean");
+  check_param(rvar, C, "running_var");
+  check_param(bias, C, "bias");
+  if (nbt) TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "norm_stats: nbt");
   auto fo = x.options().dtype(at::kFloat);
   Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
   Tensor mean = at::empty({G, C}, fo), rstd = at::empty({G, C}, fo);
-  rs::norm_stats_launch(bf, x.data_ptr(), B, P, C, G, (float)eps, ws.data_ptr<float>(),
-                        mean.data_ptr<float>(), rstd.data_ptr<float>(), stream());
+  const float unb = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
+  rs::norm_stats_launch(bf, x.data_ptr(), B, P, C, G, (float)eps, ws.data_ptr<float>(), mean.data_ptr<float>(),
+                        rstd.data_ptr<float>(), rmean ? rmean->data_ptr<float>() : nullptr, rvar ? rvar->data_ptr<float>() : nullptr,
+                        nbt ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr, fptr(bias),
+                        (float)momentum, unb, stream());
   RS_CHECK_LAUNCH();
   return {mean, rstd};
 }
@@ -124,35 +136,15 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
 
 }  // namespace
 
-// In-place BatchNorm running-statistics update (see bn_running_kernel).
-void bn_running_update(const Tensor& mean, const Tensor& rstd, const c10::optional<Tensor>& bias,
-                       Tensor running_mean, Tensor running_var, c10::optional<Tensor> nbt, double eps,
-                       double momentum, int64_t n) {
-  const int64_t C = running_mean.numel();
-  check_param(mean, C, "mean");
-  check_param(rstd, C, "rstd");
-  check_param(bias, C, "bias");
-  check_param(running_mean, C, "running_mean");
-  check_param(running_var, C, "running_var");
-  if (nbt) TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "bn: num_batches_tracked");
-  const c10::DeviceGuard g(mean.device());
-  const float unb = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
-  rs::bn_running_launch(mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(bias), (int)C, (float)eps,
-                        (float)momentum, unb, running_mean.data_ptr<float>(), running_var.data_ptr<float>(),
-                        nbt ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr, stream());
-  RS_CHECK_LAUNCH();
-}
-
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
-  m.def("bn_running_update(Tensor mean, Tensor rstd, Tensor? bias, Tensor(a!) running_mean, Tensor(b!) running_var, Tensor(c!)? nbt, float eps, float momentum, int n) -> ()");
-  m.def("norm_stats(Tensor x, bool per_sample, float eps) -> Tensor[]");
+  m.def("norm_stats(Tensor x, bool per_sample, float eps, Tensor(a!)? running_mean=None, "
+        "Tensor(b!)? running_var=None, Tensor(c!)? nbt=None, Tensor? bias=None, float momentum=0.1, int n=0) -> Tensor[]");
   m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu) -> Tensor");
   m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, bool batch_stats) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("norm_stats", &norm_stats);
-  m.impl("bn_running_update", &bn_running_update);
   m.impl("norm_act", &norm_act);
   m.impl("norm_act_backward", &norm_act_backward);
 }

@@ -297,17 +297,41 @@ __global__ __launch_bounds__(WG_T) void stem_wgrad_kernel(SArgs s, const bf16_t*
 }
 
 // dW[co][ci][ky][kx] (fp32, the conv weight's layout) = sum over blocks of the
-// partials, in block order; k = kx * 3 + ci of kernel row ky
-__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int Cout,
-                                                                float* __restrict__ dw) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // over Cout * 147
-  if (i >= Cout * 147) return;
-  const int co = i / 147, r = i - co * 147;
-  const int ci = r / 49, ky = (r / 7) % 7, kx = r % 7;
-  const int n = ky * KR + kx * 3 + ci;
+// partials, k = kx * 3 + ci of kernel row ky.  Block = 64 outputs x 16 partial
+// lanes: lane j sums partials j, j + 16, ... in order, then output o adds the
+// 16 lane sums in lane order (deterministic; independent loads in flight
+// instead of one serial chain of nblk loads per output).
+constexpr int RD_O = 64, RD_L = 16;
+
+__global__ __launch_bounds__(RD_O * RD_L) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblk,
+                                                                        int Cout, float* __restrict__ dw) {
+  __shared__ float red[RD_L][RD_O];
+  const int o = threadIdx.x % RD_O, j = threadIdx.x / RD_O;
+  const int i = blockIdx.x * RD_O + o;  // over Cout * 147
   float acc = 0.f;
-  for (int blk = 0; blk < nblk; ++blk) acc += part[((size_t)blk * 64 + co) * 224 + n];
-  dw[i] = acc;
+  if (i < Cout * 147) {
+    const int co = i / 147, r = i - co * 147;
+    const int ci = r / 49, ky = (r / 7) % 7, kx = r % 7;
+    const size_t n = (size_t)co * 224 + ky * KR + kx * 3 + ci;
+    int blk = j;
+    for (; blk + 3 * RD_L < nblk; blk += 4 * RD_L) {
+      const float v0 = part[(size_t)blk * 64 * 224 + n], v1 = part[(size_t)(blk + RD_L) * 64 * 224 + n];
+      const float v2 = part[(size_t)(blk + 2 * RD_L) * 64 * 224 + n], v3 = part[(size_t)(blk + 3 * RD_L) * 64 * 224 + n];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; blk < nblk; blk += RD_L) acc += part[(size_t)blk * 64 * 224 + n];
+  }
+  red[j][o] = acc;
+  __syncthreads();
+  if (j == 0 && i < Cout * 147) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < RD_L; ++l) t += red[l][o];
+    dw[i] = t;
+  }
 }
 
 }  // namespace stem
@@ -359,8 +383,8 @@ void stem_wgrad_launch(const void* x, bool x_bf16, int B, int Hi, int Wi, int Ho
   stem::SArgs s{x, x_bf16 ? 1 : 0, B, Hi, Wi, Ho, Wo};
   hipLaunchKernelGGL(stem::stem_wgrad_kernel, dim3(nblk), dim3(stem::WG_T), 0, stream, s, dy, ystr, Cout,
                      chunks_per_block, part);
-  hipLaunchKernelGGL(stem::stem_wgrad_reduce_kernel, dim3(cdiv(Cout * 147, 256)), dim3(256), 0, stream, part, nblk,
-                     Cout, dw);
+  hipLaunchKernelGGL(stem::stem_wgrad_reduce_kernel, dim3(cdiv(Cout * 147, stem::RD_O)), dim3(stem::RD_O * stem::RD_L),
+                     0, stream, part, nblk, Cout, dw);
 }
 
 }  // namespace rs

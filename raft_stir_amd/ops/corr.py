@@ -17,12 +17,12 @@ zero-filled pyramid gradient each time) and then through
   atomics) and returns a zero token gradient;
 * when autograd reaches the volume node (after all lookups, by topology) it
   folds the pyramid gradient into level 0 (avg-pool backward + 1/sqrt(C)) and
-  issues the two GEMMs  df1 = G f2,  df2 = G^T f1  once per step.
+  issues the two GEMMs  df1 = G f2,  df2 = G^T f1  once per step, both in one
+  MFMA launch (csrc/corr_bwd.hip; split-bf16 operands for fp32 features).
 """
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional
 
 import torch
@@ -59,9 +59,6 @@ def from_nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 3, 1, 2)
 
 
-_AB_LIB = os.environ.get("RS_AB_CORR_LIB", "0") == "1"  # temporary A/B knob
-
-
 class _CorrVolume(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f1, f2, state: CorrState):
@@ -82,34 +79,23 @@ class _CorrVolume(torch.autograd.Function):
             return None, None, None
         B, N1, C = f1.shape
         _, H2, W2, _ = f2.shape
-        if (f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16 and C % 128 == 0 and not _AB_LIB
-                and -(-(H2 * W2) // 64) * 64 <= 6144):
+        g0 = state.gpyr[0]
+        bf16 = f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16
+        f32 = f1.dtype == torch.float32 and f2.dtype == torch.float32
+        row_fold = -(-(H2 * W2) // 64) * 64 <= 6144  # csrc/corr_lookup.hip pyr_fold_rows_kernel
+        if C % 128 == 0 and ((bf16 and (row_fold or (g0.stride(1) % 4 == 0 and g0.data_ptr() % 16 == 0)))
+                             or (f32 and row_fold)):
             # csrc/corr_bwd.hip: one fold pass into a padded bf16 G, then both
-            # feature-gradient GEMMs in one MFMA launch (deterministic); the
-            # row fold holds level-0 grids up to 6144 cells (1/8 of ~768 x 512)
+            # feature-gradient GEMMs in one MFMA launch (deterministic); fp32
+            # features: split-bf16 operands, three K passes, fp32 gradients
             df1, df2 = torch.ops.raft_stir.corr_volume_backward(state.gpyr, f1.contiguous(), f2.contiguous(),
                                                                state.scale)
-        elif f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16:
-            # other channel counts / larger grids: bf16 library GEMMs on the folded gradient
+        elif bf16:
+            # other channel counts: bf16 library GEMMs on the folded gradient
             G = torch.empty(B, N1, H2 * W2, device=f1.device, dtype=torch.bfloat16)
             torch.ops.raft_stir.pyr_grad_fold_bf16(state.gpyr, state.scale, G)
-            side = None
-            if _AB_LIB:
-                from ..models.raft import OVERLAP, _SIDE_STREAMS
-                side = _SIDE_STREAMS.get((f1.device.index, 0)) if OVERLAP.get("cnet", False) else None
-            if side is not None:
-                main = torch.cuda.current_stream(f1.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    df2 = torch.bmm(G.transpose(1, 2), f1)
-                df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
-                main.wait_stream(side)
-                G.record_stream(side)
-                f1.record_stream(side)
-                df2.record_stream(main)
-            else:
-                df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
-                df2 = torch.bmm(G.transpose(1, 2), f1)
+            df1 = torch.bmm(G, f2.reshape(B, H2 * W2, C))
+            df2 = torch.bmm(G.transpose(1, 2), f1)
         else:
             torch.ops.raft_stir.pyr_grad_fold(state.gpyr, state.scale)
             G = state.gpyr[0].view(B, N1, H2 * W2)

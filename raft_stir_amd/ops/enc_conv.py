@@ -69,17 +69,16 @@ def _halo_ok(cin: int, cout: int) -> bool:
 # 96 channels are read as two overlapping 64-channel windows, [0, 64) and
 # [32, 96), with zero weights on the duplicated half.
 _V3 = True
-_AB_T68 = os.environ.get("RS_AB_T68", "1") == "1"   # temporary A/B knobs
-_AB_SINK = os.environ.get("RS_AB_SINK_V3", "1") == "1"
 
 
 def _v3_tile(P: int, cin: int, cout: int):
     if not _V3 or cin % 32 or cin < 64 or cout % 32:
         return None
-    if cin == 64 and cout == 64:
-        # 1/2-res 64 -> 64: the 8-wave 64 x 384-px tile (68) below fnet's
-        # 16-image size, where the halo kernel ties it (profiles/r5/bench_enc_v3_s13.log)
-        return None if P >= 600000 else (68 if _AB_T68 else 65)
+    if cin == 64 and cout == 64 and P >= 600000:
+        return None
+    # (tile 68, the 8-wave 64 x 384-px tile, wins the isolated cnet 1/2-res
+    # conv but costs 131 vs 91 us per call inside the training step, where it
+    # co-runs with fnet: profiles/r5/train_kernel_stats_s18_*.csv)
     return 65 if cout <= 64 else 61
 
 
@@ -249,8 +248,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x)
         # the skip gradient is added in the dgrad kernel's epilogue (halo
         # kernel: accumulate; v3 tiles: EPI_ADD_BF16)
-        ctx.sink = sink if sink is not None and ((_halo_ok(cout, cin) and (_AB_SINK or _v3_tile(P, cout, cin) is None))
-                                                 or (_AB_SINK and _v3_tile(P, cout, cin) is not None)) else None
+        ctx.sink = sink if sink is not None and (_halo_ok(cout, cin) or _v3_tile(P, cout, cin) is not None) else None
         if ctx.sink is not None:
             ctx.sink.armed = True
         return out.permute(0, 3, 1, 2)
@@ -335,7 +333,6 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, sink=None) -> torch.Tensor:
 # bf16 training (forward + weight gradient), bf16 / fp32 inference, both
 # encoders and RAFT-small's 32-channel stem (scripts/bench_stem.py).
 _STEM = True
-_AB_STEM = os.environ.get("RS_AB_STEM", "1") == "1"  # temporary A/B knob
 
 
 def _stem_layout(ws):
@@ -361,8 +358,6 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     f32 = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32
     if f32 and torch.is_grad_enabled() and conv.weight.requires_grad:
         return False  # fp32 training: the module graph
-    if not _AB_STEM and torch.is_grad_enabled() and conv.weight.requires_grad:
-        return False
     return x.numel() * 4 < (1 << 31)
 
 

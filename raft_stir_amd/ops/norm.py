@@ -202,19 +202,21 @@ def norm_act(norm: nn.Module, x: torch.Tensor, relu: bool = True, residual=None,
     # BatchNorm2d
     batch_stats = norm.training
     if batch_stats:
-        mean, rstd = batch_moments(False)
-        with torch.no_grad():
-            n = x.numel() // x.shape[1]
-            rm, rv = norm.running_mean, norm.running_var
-            if rm.dtype == torch.float32 and rv.dtype == torch.float32 and rm.is_contiguous() and rv.is_contiguous():
-                # one fused launch (csrc/norm.hip bn_running_kernel)
-                torch.ops.raft_stir.bn_running_update(
-                    mean.reshape(-1), rstd.reshape(-1), None if bias is None else bias.detach().float().contiguous(),
-                    rm, rv, norm.num_batches_tracked, norm.eps, norm.momentum, n)
+        n = x.numel() // x.shape[1]
+        rm, rv = norm.running_mean, norm.running_var
+        if rm.dtype == torch.float32 and rv.dtype == torch.float32 and rm.is_contiguous() and rv.is_contiguous():
+            # the running update rides on the statistics finalize (csrc/norm.hip finalize_kernel)
+            with torch.no_grad():
+                nbt = norm.num_batches_tracked
+                mean, rstd = torch.ops.raft_stir.norm_stats(
+                    xn, False, norm.eps, rm, rv, nbt if nbt is not None and nbt.dtype == torch.long else None,
+                    None if bias is None else bias.detach().float().contiguous(), norm.momentum, n)
                 # a custom mutable op does not bump the version counters: do it
                 # here so the eval-mode caches keyed on them (_cached) go stale
                 torch.autograd.graph.increment_version([rm, rv])
-            else:
+        else:
+            mean, rstd = batch_moments(False)
+            with torch.no_grad():
                 var = (rstd.reshape(-1).pow(-2) - norm.eps).clamp_min(0)
                 unbiased = var * (n / max(n - 1, 1))
                 m = norm.momentum

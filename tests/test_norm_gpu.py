@@ -115,7 +115,8 @@ def test_conv_norm_act_folds_bias(cuda, kind):
 
 def test_bn_recalibration_then_eval(cuda):
     """Train-mode forwards under no_grad (BN recalibration) update the running
-    buffers through the custom bn_running_update op; a following eval()
+    buffers inside the statistics launch (norm_stats running_mean / running_var /
+    nbt, csrc/norm.hip finalize_kernel); a following eval()
     forward must see the new buffers, not the eval-affine cache of the old ones
     (ops/norm.py bumps the version counters the cache is keyed on)."""
     from raft_stir_amd.ops.norm import conv_norm_act
@@ -139,6 +140,7 @@ def test_bn_recalibration_then_eval(cuda):
         rnorm.eval()
         torch.testing.assert_close(norm.running_mean, rnorm.running_mean, atol=1e-4, rtol=1e-4)
         torch.testing.assert_close(norm.running_var, rnorm.running_var, atol=1e-4, rtol=1e-4)
+        assert norm.num_batches_tracked.item() == rnorm.num_batches_tracked.item() == 3
         y = conv_norm_act(conv, norm, x)
         yr = F.relu(rnorm(rconv(x)))
     torch.testing.assert_close(y, yr, atol=1e-4, rtol=1e-4)
