@@ -985,6 +985,9 @@ __global__ __launch_bounds__(256) void relu_take_kernel(float* __restrict__ G, i
 }  // namespace conv
 
 // ------------------------------------------------------------------ launchers
+// conv_gemm1.hip: tile 70 (1x1, bf16, segments % 64 channels)
+bool conv_1x1_launch(const conv::Args& a, int tile, hipStream_t stream);
+
 struct ConvLaunch {
   const void* seg_ptr[3];
   int seg_C[3], seg_stride[3];
@@ -1087,6 +1090,10 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   }
   if (L.tile >= 42 && L.tile <= 54) {  // lean unrolled-tap tiles (conv_v2.hip)
     conv_v2_launch(a, L.tile, stream);
+    return;
+  }
+  if (L.tile == 70) {  // 1x1 convs as plain GEMMs (conv_gemm1.hip)
+    conv_1x1_launch(a, L.tile, stream);
     return;
   }
   if (L.tile >= 60) {  // weight-streaming tiles (conv_v3.hip), fragment-major weights

@@ -23,9 +23,6 @@ enum Epi : int {
                      // co >= hd: out(fp32)[co] += v          (h = aux1, r = aux2)
   // encoder normalisation folded into the conv (eval-mode BatchNorm):
   EPI_NORM = 9,  // v = acc * chs[co] + bias[co]; hd != 0: ReLU; aux1: v = relu(v + aux1) -> out (bf16)
-  // dgrad into a bf16 gradient that already holds another path's contribution
-  // (a residual block's skip gradient): out(bf16) = out + v   (tiles 42-54, 60-68 only)
-  EPI_ADD_BF16 = 10,
 };
 
 struct Seg {
@@ -268,19 +265,6 @@ __device__ __forceinline__ void epi_frag(const Args& a, float (&v)[4], int cb, i
         for (int j = 0; j < 4; ++j)
           if (cb + j < a.Cout) o[j] += v[j];
       }
-    }
-  } else if constexpr (E == EPI_ADD_BF16) {
-    bf16_t* o = static_cast<bf16_t*>(a.out) + (size_t)p * a.ostr + a.ooff + cb;
-    if (vec && full) {
-      float ov[4];
-      ld4(o, ov);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ov[j] += v[j];
-      st4(o, ov);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (cb + j < a.Cout) o[j] = f2bf(bf2f(o[j]) + v[j]);
     }
   } else if constexpr (E == EPI_NORM) {
     if (a.hd) {
@@ -739,8 +723,6 @@ __device__ __forceinline__ void epi32_batch(const Args& a, const f32x16_t (&acc)
           l2[k][g] = *reinterpret_cast<const uint2*>(a.aux2 + p * a.a2str + a.a2off + cb);
         } else if constexpr (E == EPI_RELU_BWD) {
           l1[k][g] = *reinterpret_cast<const uint2*>(a.aux1 + p * a.a1str + a.a1off + cb);
-        } else if constexpr (E == EPI_ADD_BF16) {
-          l1[k][g] = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(a.out) + p * a.ostr + a.ooff + cb);
         } else if constexpr (E == EPI_ACC_F32) {
           lf[k][g] = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out) + p * a.ostr + a.ooff + cb);
         } else if constexpr (E == EPI_GRU_QBWD) {
@@ -802,12 +784,6 @@ __device__ __forceinline__ void epi32_batch(const Args& a, const f32x16_t (&acc)
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = av[j] > 0.f ? v[j] : 0.f;
           st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, v);
-        } else if constexpr (E == EPI_ADD_BF16) {
-          float ov[4];
-          unpack(l1[k][g], ov);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) ov[j] += v[j];
-          st4(static_cast<bf16_t*>(a.out) + p * a.ostr + a.ooff + cb, ov);
         } else if constexpr (E == EPI_ACC_F32) {
           const float4 o = lf[k][g];
           *reinterpret_cast<float4*>(static_cast<float*>(a.out) + p * a.ostr + a.ooff + cb) =
@@ -856,7 +832,6 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
       RS_EB(EPI_GRU_ZR);
       RS_EB(EPI_GRU_Q);
       RS_EB(EPI_RELU_BWD);
-      RS_EB(EPI_ADD_BF16);
       RS_EB(EPI_ACC_F32);
       RS_EB(EPI_GRU_QBWD);
       RS_EB(EPI_RELU);
@@ -876,7 +851,6 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
     RS_E2(EPI_GRU_ZR);
     RS_E2(EPI_GRU_Q);
     RS_E2(EPI_RELU_BWD);
-    RS_E2(EPI_ADD_BF16);
     RS_E2(EPI_ACC_F32);
     RS_E2(EPI_GRU_QBWD);
     RS_E2(EPI_RELU);

@@ -123,7 +123,7 @@ namespace {
 using at::Tensor;
 
 constexpr int EPI_GRU_ZR = 3, EPI_GRU_Q = 4, EPI_FLOW = 5, EPI_RELU_BWD = 6, EPI_ACC_F32 = 7, EPI_GRU_QBWD = 8,
-              EPI_NORM = 9, EPI_ADD_BF16 = 10;
+              EPI_NORM = 9;
 
 hipStream_t stream() { return rs::current_stream(); }
 
@@ -201,8 +201,14 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 68), "conv_fused: tile must be in [0,54] or [60,68]");
-  const bool v3 = tile >= 60;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
+  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 68) || tile == 70,
+              "conv_fused: tile must be in [0,54], [60,68] or 70");
+  if (tile == 70) {  // conv_gemm1.hip: 1x1 GEMM over 64-channel K chunks
+    TORCH_CHECK(KH == 1 && KW == 1 && !f32, "conv_fused: tile 70 is the bf16 1x1 GEMM");
+    for (size_t s = 0; s < segs.size(); ++s)
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tile 70 needs segment channels % 64 == 0");
+  }
+  const bool v3 = tile >= 60 && tile <= 68;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
   if ((tile >= 42 && tile <= 54) || v3)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-54 and 60-68 are instantiated for 3x3, 1x5 and 5x1 kernels only");
@@ -217,7 +223,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
                      tile == 18 || tile == 20 || tile == 22 || tile == 24 || tile == 26 || tile == 36 ||
                      tile == 39;
   const bool bm128w = tile == 28 || tile == 31 || tile == 33;
-  const int tileM = (tile == 48 || tile == 49 || tile == 53) ? 128 : (tile == 50 || tile == 51 || tile == 52) ? 256
+  const int tileM = (tile == 48 || tile == 49 || tile == 53 || tile == 70) ? 128
+                    : (tile == 50 || tile == 51 || tile == 52) ? 256
                     : tile == 54 ? 192
                     : (tile == 42 || tile >= 45) ? 64 : tile == 43 ? 32 : tile == 44 ? 128
                     : tile == 0 ? 32
@@ -298,11 +305,10 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     opt_nhwc(aux1, a1off, hd, "aux1", &p, &L.a1str, &L.a1off); L.aux1 = p;
     opt_nhwc(aux2, a2off, hd, "aux2", &p, &L.a2str, &L.a2off); L.aux2 = p;
   }
-  TORCH_CHECK(epi != EPI_ADD_BF16 || (((tile >= 42 && tile <= 54) || v3) && !f32),
-              "conv_fused: EPI_ADD_BF16 (out += v, bf16) runs on tiles 42-54 and 60-68 only");
+  TORCH_CHECK(epi >= 0 && epi <= EPI_NORM, "conv_fused: unknown epilogue kind");
   if (nx.chs)
-    TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3,
-                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54, 60-68)");
+    TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3 && tile != 70,
+                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54, 60-70)");
   L.chs = nx.chs;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();

@@ -16,7 +16,7 @@ from typing import List, Sequence, Tuple
 import torch
 
 (EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_GRU_ZR, EPI_GRU_Q, EPI_FLOW,
- EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_NORM, EPI_ADD_BF16) = range(11)
+ EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_NORM) = range(10)
 
 Piece = Tuple[int, int, int]          # (weight in-channel start, length, segment channel offset)
 SegSpec = Tuple[int, Sequence[Piece]]  # (segment channels read (multiple of 32), pieces)
@@ -111,6 +111,21 @@ def pack_bias(bias: torch.Tensor, n: int | None = None) -> torch.Tensor:
 # bit 4 (192-wide conv on the 192x96 tile) +0.4 %, bit 1 (Cout <= 128 on 128x96)
 # -1.4 %, bit 2 (Cout > 192) neutral -- default 4.
 _WIDE = 4
+
+
+# csrc/conv_gemm1.hip: the update block's 1x1 convs (convc1, the mask head's
+# second conv; forward and input gradient) as plain MFMA GEMMs over
+# K-contiguous weight and activation rows (bf16, every segment % 64 channels,
+# packed weights with >= round_up(Cout, 128) rows, no EPI_NORM).  A tuning
+# candidate: it beats the implicit-GEMM tiles on the training shape's convc1 /
+# mask-head forward and the mask-head dgrad, not at batch 1
+# (profiles/r5/bench_conv_1x1_s22.log)
+GEMM1_TILE = 70
+
+
+def gemm1_ok(w: torch.Tensor, cout: int, chans, nscale=None) -> bool:
+    return (w.dtype == torch.bfloat16 and nscale is None and all(int(c) % 64 == 0 for c in chans)
+            and w.shape[0] >= pad_to(cout, 128))
 
 
 def choose_tile(P: int, cout: int, seg_chans, taps: int = 9) -> int:
@@ -211,7 +226,8 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
             tile = tuned_tiles_f32().get(key) or choose_tile_f32(P, cout)
         else:
             tile = tuned_tiles().get(key)
-            if tile is None or (tile in V3_TILES and wf is None):
+            if tile is None or (tile in V3_TILES and wf is None) or (tile == GEMM1_TILE and not gemm1_ok(
+                    w, cout, chans, nscale)):
                 tile = choose_tile(P, cout, chans, kh * kw)
     if tile in V3_TILES:
         if wf is None:

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_ADD_BF16, EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
+from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -100,12 +100,10 @@ def _v3_weight(weight: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wpack.packed(("v3", id(weight), dgrad), [weight], layout)
 
 
-def _conv3x3_v3(xn, weight, k_in, k_out, out, tile, dgrad, accumulate=False):
-    """``accumulate``: out (bf16) += the conv (EPI_ADD_BF16, the GradSink path)."""
+def _conv3x3_v3(xn, weight, k_in, k_out, out, tile, dgrad):
     wins, _ = _v3_windows(k_in)
     wf = _v3_weight(weight, dgrad)
-    conv_fused([(xn, o, c) for o, c in wins], wf, None, 3, 3, k_out, EPI_ADD_BF16 if accumulate else EPI_BIAS,
-               out, 0, tile=tile, wf=wf)
+    conv_fused([(xn, o, c) for o, c in wins], wf, None, 3, 3, k_out, EPI_BIAS, out, 0, tile=tile, wf=wf)
 
 
 def _conv3x3_into(xn, wp, cin, cout, out, P):
@@ -246,9 +244,10 @@ class _Conv3x3(torch.autograd.Function):
         else:
             _conv3x3_into(xn, _packed(weight, False), cin, cout, out, P)
         ctx.save_for_backward(x)
-        # the skip gradient is added in the dgrad kernel's epilogue (halo
-        # kernel: accumulate; v3 tiles: EPI_ADD_BF16)
-        ctx.sink = sink if sink is not None and (_halo_ok(cout, cin) or _v3_tile(P, cout, cin) is not None) else None
+        # the skip gradient is added in the halo kernel's dgrad epilogue only
+        # (an out += v kind in the v2 / v3 tiles' shared epilogue slowed every
+        # conv on them by 1-7%: profiles/r5/infer_kernel_stats_s21_*.csv)
+        ctx.sink = sink if sink is not None and _halo_ok(cout, cin) and _v3_tile(P, cout, cin) is None else None
         if ctx.sink is not None:
             ctx.sink.armed = True
         return out.permute(0, 3, 1, 2)
@@ -267,12 +266,9 @@ class _Conv3x3(torch.autograd.Function):
             sink = ctx.sink
             td = _v3_tile(P, cout, cin)
             if sink is not None and sink.dres is not None:
-                # dX = skip gradient + dgrad, accumulated in the dgrad kernel's epilogue
+                # dX = skip gradient + dgrad, accumulated in the halo kernel's epilogue
                 dxn, sink.dres = sink.dres, None
-                if td is not None:
-                    _conv3x3_v3(dyn, weight, cout, cin, dxn, td, True, accumulate=True)
-                else:
-                    torch.ops.raft_stir.conv3x3_halo(dyn, _packed(weight, True), dxn, cout, cin, accumulate=True)
+                torch.ops.raft_stir.conv3x3_halo(dyn, _packed(weight, True), dxn, cout, cin, accumulate=True)
             else:
                 dxn = torch.empty(N, H, W, cin, device=x.device, dtype=torch.bfloat16)
                 if td is not None:

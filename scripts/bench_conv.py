@@ -33,6 +33,8 @@ SHAPES = [
     ("c2_dg", 192, 256, 3, 3),
     ("cv_dg", 128, 256, 3, 3),
     ("f2_dg", 64, 128, 3, 3),
+    ("c1_dg", 256, 384, 1, 1),
+    ("m2_dg", 576, 256, 1, 1),
 ]
 
 

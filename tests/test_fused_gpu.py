@@ -8,8 +8,8 @@ import torch.nn.functional as F
 
 from raft_stir_amd.config import make_args
 from raft_stir_amd.models import RAFT
-from raft_stir_amd.ops.conv import (EPI_ACC_F32, EPI_ADD_BF16, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR,
-                                    EPI_RELU, EPI_RELU_BWD, EPI_SCALE, V3_TILES, conv_fused, frag_weight,
+from raft_stir_amd.ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR,
+                                    EPI_RELU, EPI_RELU_BWD, EPI_SCALE, GEMM1_TILE, V3_TILES, conv_fused, frag_weight,
                                     pack_bias, pack_weight, pad_to)
 
 pytestmark = pytest.mark.gpu
@@ -116,27 +116,45 @@ def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
     assert (out[..., cout:] == 7).all()
 
 
-@pytest.mark.parametrize("tile", [44, 52, 61, 66, 68])
-@pytest.mark.parametrize("cout", [96, 70])
-def test_conv_add_bf16_epilogue(cuda, tile, cout):
-    """EPI_ADD_BF16 (out(bf16) += conv, the encoder GradSink dgrad): the
-    batched 32-row epilogue (cout 96) and the element-wise form (cout 70,
-    a partial last fragment) against out0 + conv2d; the channels past the
-    window keep their values."""
-    torch.manual_seed(8)
-    B, H, W = 2, 13, 37
-    x = torch.randn(B, H, W, 64, device=cuda).to(torch.bfloat16)
-    w = torch.randn(cout, 64, 3, 3, device=cuda) * 0.05
-    wp = pack_weight(w, [(64, [(0, 64, 0)])], pad_to(cout, 256))
-    out0 = torch.randn(B, H, W, cout + 4, device=cuda).to(torch.bfloat16)
+@pytest.mark.parametrize("cout", [256, 576, 70])
+@pytest.mark.parametrize("epi", [EPI_RELU, EPI_SCALE, EPI_RELU_BWD, EPI_ACC_F32])
+@pytest.mark.parametrize("shape", [(2, 11, 19), (1, 9, 70), (8, 46, 62)])
+def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape):
+    """csrc/conv_gemm1.hip (tile 70): two input segments read from windows of
+    wider buffers, pixel counts that are not a multiple of the 128-pixel tile,
+    Cout a multiple of 32 (batched epilogue) or not (element-wise epilogue),
+    the epilogue kinds the update block's 1x1 convs use; channels past the
+    output window untouched."""
+    torch.manual_seed(9)
+    B, H, W = shape
+    a_buf = torch.randn(B, H, W, 192, device=cuda).to(torch.bfloat16)
+    b_buf = torch.randn(B, H, W, 256, device=cuda).to(torch.bfloat16)
+    x = torch.cat([a_buf[..., 64:192], b_buf], -1).float().permute(0, 3, 1, 2)
+    w = torch.randn(cout, 384, 1, 1, device=cuda) * 0.05
+    b = torch.randn(cout, device=cuda)
+    wp = pack_weight(w, [(128, [(0, 128, 0)]), (256, [(128, 256, 0)])], pad_to(cout, 128))
+    f32out = epi == EPI_ACC_F32
+    out0 = torch.randn(B, H, W, cout + 8, device=cuda)
+    out0 = out0 if f32out else out0.to(torch.bfloat16)
     out = out0.clone()
-    conv_fused([(x, 0, 64)], wp, None, 3, 3, cout, EPI_ADD_BF16, out, 0, tile=tile,
-               wf=frag_weight(wp) if tile in V3_TILES else None)
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2), _bf(w), None, padding=1) + out0[..., :cout].float().permute(0, 3, 1, 2)
-    torch.testing.assert_close(out[..., :cout].float().permute(0, 3, 1, 2), ref, atol=3e-2, rtol=2e-2)
+    aux = torch.randn(B, H, W, cout, device=cuda).to(torch.bfloat16)
+    kw_ = dict(scale=0.25, tile=GEMM1_TILE)
+    if epi == EPI_RELU_BWD:
+        kw_.update(aux1=aux, a1off=0)
+    bias = None if epi in (EPI_RELU_BWD, EPI_ACC_F32) else pack_bias(b)
+    conv_fused([(a_buf, 64, 128), (b_buf, 0, 256)], wp, bias, 1, 1, cout, epi, out, 0, **kw_)
+    ref = F.conv2d(x, _bf(w), None if bias is None else b)
+    if epi == EPI_RELU:
+        ref = ref.relu()
+    elif epi == EPI_SCALE:
+        ref = ref * 0.25
+    elif epi == EPI_RELU_BWD:
+        ref = ref * (aux.float().permute(0, 3, 1, 2) > 0)
+    elif epi == EPI_ACC_F32:
+        ref = ref + out0[..., :cout].permute(0, 3, 1, 2)
+    got = out[..., :cout].float().permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
     assert torch.equal(out[..., cout:], out0[..., cout:])
-    with pytest.raises(RuntimeError, match="EPI_ADD_BF16"):
-        conv_fused([(x, 0, 64)], wp, None, 3, 3, cout, EPI_ADD_BF16, out, 0, tile=0)
 
 
 @pytest.mark.parametrize("epi", [EPI_GRU_ZR, EPI_GRU_Q, EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_SCALE])
