@@ -200,6 +200,42 @@ __global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __re
   }
 }
 
+// Adjoint of RAFT-small's x8 bilinear upsampling with align_corners=True
+// (reference core/utils/utils.py:80-82 upflow8, the training loss path):
+//   dflow[n][c][i][j] = 8 * sum_{I, J} ah[I][i] aw[J][j] g[n][c][I][J]
+// ah [8H][H], aw [8W][W]: the interpolation matrices (upsample_bilinear2d's
+// float32 source-index arithmetic, models/fused_train.py _interp_matrix).
+// Gather form, one output per thread: the nonzero rows of column i lie in
+// [floor((i - 1) / r), ceil((i + 1) / r)] for r = (H - 1) / (8H - 1); the loop
+// runs a window two wider on each side (zeros outside the band add nothing)
+// -- deterministic, no atomics.
+__global__ __launch_bounds__(256) void upflow8_bwd_kernel(const float* __restrict__ g, const float* __restrict__ ah,
+                                                          const float* __restrict__ aw, int NC, int H, int W,
+                                                          float* __restrict__ out) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)NC * H * W;
+  if (idx >= total) return;
+  const int j = (int)(idx % W), i = (int)((idx / W) % H), nc = (int)(idx / ((long)H * W));
+  const int H8 = 8 * H, W8 = 8 * W;
+  const float rh = H > 1 ? (float)(H8 - 1) / (float)(H - 1) : 0.f;  // output rows per input row
+  const float rw = W > 1 ? (float)(W8 - 1) / (float)(W - 1) : 0.f;
+  // (a single input row / column: every output row / column reads it)
+  const int I0 = H > 1 ? max(0, (int)floorf((i - 1) * rh) - 2) : 0;
+  const int I1 = H > 1 ? min(H8 - 1, (int)ceilf((i + 1) * rh) + 2) : H8 - 1;
+  const int J0 = W > 1 ? max(0, (int)floorf((j - 1) * rw) - 2) : 0;
+  const int J1 = W > 1 ? min(W8 - 1, (int)ceilf((j + 1) * rw) + 2) : W8 - 1;
+  const float* gp = g + (size_t)nc * H8 * W8;
+  float acc = 0.f;
+  for (int I = I0; I <= I1; ++I) {
+    const float a = ah[(size_t)I * H + i];
+    if (a == 0.f) continue;
+    float row = 0.f;
+    for (int J = J0; J <= J1; ++J) row += aw[(size_t)J * W + j] * gp[(size_t)I * W8 + J];
+    acc += a * row;
+  }
+  out[idx] = 8.f * acc;
+}
+
 }  // namespace cvx
 
 // flow: (N,2,H,W) fp32; mask: (N,H,W,576) channels-last; out: (N,2,8H,8W) fp32
@@ -237,6 +273,14 @@ void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, c
   if (g > 65535) g = 65535;
   hipLaunchKernelGGL(cvx::convex_up_gather_kernel, dim3((unsigned)g), dim3(256), 0, stream,
                      partial, N, H, W, dflow);
+}
+
+void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* out,
+                        hipStream_t stream) {
+  const long total = (long)NC * H * W;
+  if (total > 0)
+    hipLaunchKernelGGL(cvx::upflow8_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, g, ah, aw,
+                       NC, H, W, out);
 }
 
 }  // namespace rs

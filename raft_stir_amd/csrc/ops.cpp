@@ -37,6 +37,8 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                             bool dout_bf16, hipStream_t stream, int dstride);
 size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
 int corr_bwd_pitch(int N2);
+void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* out,
+                        hipStream_t stream);
 void corr_bwd_gemm_launch(const void* G, const void* Gl, int Ep, const void* f1, const void* f1l, const void* f2,
                           const void* f2l, int B, int N1, int N2, int C, void* df1, void* df2, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
@@ -440,6 +442,26 @@ Tensor convex_upsample(const Tensor& flow, const Tensor& mask) {
   return out;
 }
 
+// Adjoint of the x8 bilinear (align_corners) upsampling: g [N, C, 8H, 8W] fp32,
+// ah [8H, H], aw [8W, W] fp32 interpolation matrices -> [N, C, H, W] fp32 (x 8)
+Tensor upflow8_backward(const Tensor& g, const Tensor& ah, const Tensor& aw) {
+  check_gpu(g, "g");
+  check_dtype(g, {at::kFloat}, "g");
+  TORCH_CHECK(g.dim() == 4 && g.is_contiguous() && g.size(2) % 8 == 0 && g.size(3) % 8 == 0,
+              "upflow8_backward: g must be contiguous (N, C, 8H, 8W)");
+  const int H = g.size(2) / 8, W = g.size(3) / 8;
+  TORCH_CHECK(ah.is_cuda() && ah.is_contiguous() && ah.scalar_type() == at::kFloat && ah.size(0) == 8 * H &&
+                  ah.size(1) == H && aw.is_cuda() && aw.is_contiguous() && aw.scalar_type() == at::kFloat &&
+                  aw.size(0) == 8 * W && aw.size(1) == W,
+              "upflow8_backward: interpolation matrices [8H, H] / [8W, W] fp32");
+  const c10::DeviceGuard guard(g.device());
+  Tensor out = at::empty({g.size(0), g.size(1), H, W}, g.options());
+  rs::upflow8_bwd_launch(g.data_ptr<float>(), ah.data_ptr<float>(), aw.data_ptr<float>(), g.size(0) * g.size(1), H, W,
+                         out.data_ptr<float>(), cur_stream());
+  RS_CHECK_LAUNCH();
+  return out;
+}
+
 std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& mask,
                                              const Tensor& dup) {
   check_gpu(flow, "flow");
@@ -634,6 +656,7 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> Tensor[]");
+  m.def("upflow8_backward(Tensor g, Tensor ah, Tensor aw) -> Tensor");
   m.def("gru_gate_zr(Tensor zr, Tensor h, Tensor x) -> Tensor[]");
   m.def("gru_gate_q(Tensor q, Tensor z, Tensor h) -> Tensor[]");
   m.def("gru_bwd_q(Tensor dhn, Tensor z, Tensor h, Tensor qt) -> Tensor[]");
@@ -655,6 +678,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("corr_otf_backward", &corr_otf_backward);
   m.impl("convex_upsample", &convex_upsample);
   m.impl("convex_upsample_backward", &convex_upsample_backward);
+  m.impl("upflow8_backward", &upflow8_backward);
   m.impl("gru_gate_zr", &gru_gate_zr);
   m.impl("gru_gate_q", &gru_gate_q);
   m.impl("gru_bwd_q", &gru_bwd_q);

@@ -50,6 +50,16 @@ struct SconvLaunch {
   bool f32;
 };
 int sconv_max_weights();
+struct SconvWgradLaunch {
+  const void* x;
+  const void* dy;
+  int xstr, ystr, Cin, Cout, B, Hi, Wi, Ho, Wo, KH, KW, S, P;
+  bool f32;
+  float* dw;
+  float* part;
+};
+int sconv_wgrad_blocks(int B, int Ho, int OUT, int* rows_per_block);
+void sconv_wgrad_launch(const SconvWgradLaunch& L, int nblk, int rows_per_block, hipStream_t stream);
 void sconv_launch(const SconvLaunch& L, hipStream_t stream);
 struct EncWgradLaunch {
   const void* x;
@@ -633,6 +643,43 @@ void sconv(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, 
   RS_CHECK_LAUNCH();
 }
 
+// Weight gradient of a narrow-channel conv (csrc/sconv_train.hip; RAFT-small
+// encoder training): dw fp32 [Cout, KH, KW, Cin] = sum over pixels of
+// dy (x) im2col(x); x / dy dense NHWC views of the same dtype (bf16 / fp32).
+void sconv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                 const Tensor& dw) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "sconv_wgrad: x bf16 / fp32 NHWC");
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == x.scalar_type(), "sconv_wgrad: dy dtype");
+  const int B = x.size(0), Hi = x.size(1), Wi = x.size(2), Cin = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Cout = dy.size(3);
+  TORCH_CHECK(x.stride(3) == 1 && x.stride(2) % 8 == 0 && x.stride(1) == Wi * x.stride(2) &&
+                  x.stride(0) == Hi * x.stride(1) && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "sconv_wgrad: x must be dense NHWC pixels with a channel stride % 8 == 0, 16-B aligned");
+  TORCH_CHECK(dy.stride(3) == 1 && dy.stride(1) == Wo * dy.stride(2) && dy.stride(0) == Ho * dy.stride(1) &&
+                  dy.stride(2) % 4 == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && Cout % 4 == 0,
+              "sconv_wgrad: dy must be dense 16-B aligned NHWC pixels, channel stride % 4 == 0, Cout % 4 == 0");
+  TORCH_CHECK(Cin % 8 == 0 && dy.size(0) == B && stride >= 1 && pad >= 0 && KH >= 1 && KW >= 1,
+              "sconv_wgrad: shapes");
+  TORCH_CHECK(Ho == (Hi + 2 * pad - KH) / stride + 1 && Wo == (Wi + 2 * pad - KW) / stride + 1,
+              "sconv_wgrad: dy grid does not match the conv geometry");
+  TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.scalar_type() == at::kFloat &&
+                  dw.numel() == (int64_t)Cout * KH * KW * Cin,
+              "sconv_wgrad: dw fp32 [Cout, KH, KW, Cin]");
+  const int OUT = Cout * KH * KW * Cin;
+  int rows = 0;
+  const int nblk = rs::sconv_wgrad_blocks(B, Ho, OUT, &rows);
+  const c10::DeviceGuard guard(x.device());
+  Tensor part = at::empty({(int64_t)nblk * OUT}, dw.options());
+  rs::SconvWgradLaunch L{};
+  L.x = x.data_ptr(); L.dy = dy.data_ptr(); L.xstr = x.stride(2); L.ystr = dy.stride(2);
+  L.Cin = Cin; L.Cout = Cout; L.B = B; L.Hi = Hi; L.Wi = Wi; L.Ho = Ho; L.Wo = Wo;
+  L.KH = KH; L.KW = KW; L.S = stride; L.P = pad; L.f32 = x.scalar_type() == at::kFloat;
+  L.dw = dw.data_ptr<float>(); L.part = part.data_ptr<float>();
+  rs::sconv_wgrad_launch(L, nblk, rows, stream());
+  RS_CHECK_LAUNCH();
+}
+
 Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
   check_nhwc_view(dy, "enc_wgrad dy");
   check_nhwc_view(x, "enc_wgrad x");
@@ -884,6 +931,7 @@ TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
         "Tensor(c!)? out3, int o3off, Tensor? aux1, int a1off, Tensor? aux2, int a2off, int tile, "
         "Tensor? nscale=None) -> ()");
   m.def("enc_wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("sconv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad, Tensor(a!) dw) -> ()");
   m.def("sconv(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool relu, Tensor(a!) out, int yoff, "
         "Tensor? res) -> ()");
   m.def("conv_geo(Tensor[] segs, int[] seg_off, int[] seg_C, Tensor w, Tensor? bias, int KH, int KW, int PH, "
@@ -897,6 +945,7 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("conv_fused", &conv_fused);
   m.impl("conv3x3_halo", &conv3x3_halo);
   m.impl("enc_wgrad", &enc_wgrad);
+  m.impl("sconv_wgrad", &sconv_wgrad);
   m.impl("sconv", &sconv);
   m.impl("stem_conv", &stem_conv);
   m.impl("stem_wgrad", &stem_wgrad);

@@ -187,6 +187,8 @@ class _Encoder(nn.Module):
             return enc_conv.conv_f32_train(self.conv2, x)
         if not self.hip_geo and enc_conv.sconv_eligible(self.conv2, x):  # RAFT-small inference
             return enc_conv.sconv(self.conv2, x)
+        if not self.hip_geo and enc_conv.sconv_train_eligible(self.conv2, x):  # RAFT-small training
+            return enc_conv.sconv_train(self.conv2, x)
         if enc_conv.eligible_geo(self.conv2, x):
             return enc_conv.conv_geo(self.conv2, x)
         return conv_module(self.conv2, x)

@@ -879,10 +879,11 @@ def _small_backward(ctx, g_up):
     if g_up is None:
         g_up = torch.zeros(n, 2, 8 * H, 8 * W, device=dev)
     # adjoint of the x8 bilinear upsampling (align_corners) of every iteration:
-    # separable, so two batched GEMMs (deterministic, unlike the atomic scatter
-    # of upsample_bilinear2d_backward)
+    # a gather kernel over the interpolation matrices' bands (csrc/convex_upsample.hip
+    # upflow8_bwd_kernel; deterministic, unlike the atomic scatter of
+    # upsample_bilinear2d_backward)
     ah, aw = _interp_matrix(H, 8 * H, dev), _interp_matrix(W, 8 * W, dev)
-    dflow = (8 * torch.matmul(torch.matmul(ah.t(), g_up.float()), aw)).contiguous()
+    dflow = torch.ops.raft_stir.upflow8_backward(g_up.float().contiguous(), ah, aw)
     S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
     zr, q = eng.zr[0], eng.q[0]
     for i in reversed(range(iters)):

@@ -974,6 +974,84 @@ def _register_sconv_refresher():
 _register_sconv_refresher()
 
 
+def sconv_train_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Training form of the narrow-channel path, inside RAFT-small's encoder
+    (geo_scope(False)): forward and input gradient on csrc/sconv.hip, weight
+    gradient on csrc/sconv_train.hip.  bf16 under autocast or fp32 without it."""
+    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x):
+        return False
+    if not torch.is_grad_enabled() or not (x.requires_grad or conv.weight.requires_grad):
+        return False
+    ac = torch.is_autocast_enabled("cuda")
+    if not ((ac and x.dtype == torch.bfloat16) or (not ac and x.dtype == torch.float32)):
+        return False
+    if not x.is_contiguous(memory_format=_CL) or conv.weight.dtype != torch.float32:
+        return False
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if k not in ((1, 1), (3, 3)) or isinstance(p, str) or p != (k[0] // 2, k[1] // 2):
+        return False
+    if s not in ((1, 1), (2, 2)) or conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    cin, cout = conv.in_channels, conv.out_channels
+    taps = k[0] * k[1]
+    if cin % 8 or cout % 8 or min(4, cout // 8) * 8 * taps * cin > 16384 or min(4, cin // 8) * 8 * taps * cout > 16384:
+        return False
+    return x.numel() * x.element_size() < (1 << 31)
+
+
+def _sconv_dgrad_weight(weight: torch.Tensor) -> torch.Tensor:
+    """The input-gradient conv's weight: flipped and transposed, fp32 [Cin, KH, KW, Cout]."""
+    return weight.detach().float().permute(1, 2, 3, 0).flip(1, 2).contiguous()
+
+
+class _SConvTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, hold):
+        conv = hold.p
+        xn = _nhwc(x)
+        N, H, W, _ = xn.shape
+        kh, kw = conv.kernel_size
+        Ho, Wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+        out = torch.empty(N, Ho, Wo, conv.out_channels, device=x.device, dtype=x.dtype)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        torch.ops.raft_stir.sconv(xn, _sconv_weight(conv), b, stride, pad, False, out, 0, None)
+        ctx.save_for_backward(x)
+        ctx.conv, ctx.stride, ctx.pad, ctx.has_bias = conv, stride, pad, bias is not None
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        conv, s, p = ctx.conv, ctx.stride, ctx.pad
+        xn = _nhwc(x)
+        N, H, W, cin = xn.shape
+        kh, kw = conv.kernel_size
+        dyn = _nhwc(dy.to(x.dtype).contiguous(memory_format=_CL))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            src = dyn
+            if s != 1:  # the transposed stride: dY on every s-th input pixel, zeros between
+                src = torch.zeros(N, H, W, dyn.shape[3], device=dy.device, dtype=dyn.dtype)
+                src[:, ::s, ::s] = dyn
+            dxn = torch.empty(N, H, W, cin, device=dy.device, dtype=x.dtype)
+            torch.ops.raft_stir.sconv(src, _sconv_dgrad_weight(conv.weight), None, 1, kh // 2 if s == 1 else p,
+                                      False, dxn, 0, None)
+            dx = dxn.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            g = torch.empty(conv.out_channels, kh, kw, cin, device=dy.device, dtype=torch.float32)
+            torch.ops.raft_stir.sconv_wgrad(dyn, xn, kh, kw, s, p, g)
+            dw = g.permute(0, 3, 1, 2).to(conv.weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dyn.float().sum((0, 1, 2)).to(conv.bias.dtype)
+        return dx, dw, db, None, None, None
+
+
+def sconv_train(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True) -> torch.Tensor:
+    """conv(x) [+ bias] with autograd on the narrow-channel kernels (:func:`sconv_train_eligible`)."""
+    b = conv.bias if bias else None
+    return _SConvTrain.apply(x, conv.weight, b, conv.stride[0], conv.padding[0], _Hold(conv))
+
+
 def sconv(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, relu: bool = False, residual=None) -> torch.Tensor:
     """[relu](conv(x) [+ bias]) [then relu(. + residual)] on csrc/sconv.hip;
     channels_last in and out (see :func:`sconv_eligible`)."""

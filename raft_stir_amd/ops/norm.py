@@ -268,7 +268,16 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
         if _norm_kind_ok(norm) and _FOLD_BIAS:
             return norm_act(norm, enc_conv.sconv(conv, x, False), relu, residual, bias=conv.bias)
         return norm_act(norm, enc_conv.sconv(conv, x, True), relu, residual)
+    if enc_conv.sconv_train_eligible(conv, x):  # narrow channels (RAFT-small encoders), training
+        fold = conv.bias is not None and _norm_kind_ok(norm)
+        return norm_act(norm, enc_conv.sconv_train(conv, x, bias=not fold), relu, residual,
+                        bias=conv.bias if fold else None)
     if conv.bias is None or not _FOLD_BIAS or not _ext.use_hip(x) or not _norm_kind_ok(norm):
+        if residual is None and conv.bias is not None and _ext.use_hip(x) and enc_conv.stem_eligible(conv, x):
+            # the 7x7 stem ahead of a norm that cannot absorb the bias (RAFT-small's
+            # norm_fn 'none' context encoder): the bias as a separate add
+            y = enc_conv.stem(conv, x)
+            return norm_act(norm, y + conv.bias.to(y.dtype).view(1, -1, 1, 1), relu, residual)
         return norm_act(norm, conv(x), relu, residual)
     if residual is None and enc_conv.stem_eligible(conv, x):  # the 7x7 / stride-2 stem (csrc/stem.hip)
         if isinstance(norm, nn.BatchNorm2d) and not norm.training and not (

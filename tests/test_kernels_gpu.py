@@ -427,3 +427,19 @@ def test_split_bf16_matches_aten(cuda, n):
     want_hi = x.to(torch.bfloat16)
     want_lo = (x - want_hi.float()).to(torch.bfloat16)
     assert torch.equal(hi, want_hi) and torch.equal(lo, want_lo)
+
+
+@pytest.mark.parametrize("HW", [(46, 62), (11, 37), (1, 5)])
+def test_upflow8_backward_matches_autograd(cuda, HW):
+    """csrc/convex_upsample.hip upflow8_bwd_kernel: the adjoint of RAFT-small's
+    x8 bilinear upsampling (align_corners=True), deterministic gather form, vs
+    the autograd of F.interpolate (fp32, the training forward's arithmetic)."""
+    from raft_stir_amd.models.fused_train import _interp_matrix
+    H, W = HW
+    g = torch.randn(3, 2, 8 * H, 8 * W, device=cuda)
+    got = torch.ops.raft_stir.upflow8_backward(g, _interp_matrix(H, 8 * H, cuda), _interp_matrix(W, 8 * W, cuda))
+    f = torch.zeros(3, 2, H, W, device=cuda, requires_grad=True)
+    (8 * F.interpolate(f, size=(8 * H, 8 * W), mode="bilinear", align_corners=True)).backward(g)
+    torch.testing.assert_close(got, f.grad, atol=1e-3, rtol=1e-4)
+    assert torch.equal(got, torch.ops.raft_stir.upflow8_backward(g, _interp_matrix(H, 8 * H, cuda),
+                                                                 _interp_matrix(W, 8 * W, cuda)))
