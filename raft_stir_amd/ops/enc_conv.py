@@ -325,9 +325,10 @@ def conv3x3(conv: nn.Conv2d, x: torch.Tensor, sink=None) -> torch.Tensor:
 # forward (bf16 under autocast, split-bf16 for fp32 inference) with the shared
 # conv epilogues (bias, eval-BN scale / shift + ReLU) and a
 # deterministic MFMA weight gradient; the image needs no input gradient.
-# Every mode but fp32 training (which keeps the module graph) runs here:
-# bf16 training (forward + weight gradient), bf16 / fp32 inference, both
-# encoders and RAFT-small's 32-channel stem (scripts/bench_stem.py).
+# Every mode runs here: bf16 training (forward + weight gradient), fp32
+# training (split-bf16 forward, three-product split weight gradient), bf16 /
+# fp32 inference, both encoders and RAFT-small's 32-channel stem
+# (scripts/bench_stem.py).
 _STEM = True
 
 
@@ -351,9 +352,6 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
         return False
     if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous(memory_format=_CL):
         return False
-    f32 = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32
-    if f32 and torch.is_grad_enabled() and conv.weight.requires_grad:
-        return False  # fp32 training: the module graph
     return x.numel() * 4 < (1 << 31)
 
 
@@ -383,13 +381,29 @@ class _Stem(torch.autograd.Function):
         weight = ctx.param
         dw = None
         if ctx.needs_input_grad[1]:
-            dyn = _nhwc(dy.to(torch.bfloat16))
+            if x.dtype == torch.float32 and dy.dtype == torch.float32:
+                # fp32 training: split-bf16 operands, dW = dYh.Xh + dYh.Xl + dYl.Xh
+                xh, xl = _split(_nhwc(x))
+                dh, dl = _split(_nhwc(dy.contiguous(memory_format=_CL)))
 
-            def wgrad():
-                g = torch.empty(weight.shape, device=dy.device, dtype=torch.float32)
-                torch.ops.raft_stir.stem_wgrad(_nhwc(x), dyn, weight.shape[0], g)
-                return (g.to(weight.dtype),)
-            dw, = _wgrad_on(ctx.wstream, wgrad, [dyn, x])
+                def wgrad():
+                    g = torch.empty(weight.shape, device=dy.device, dtype=torch.float32)
+                    t = torch.empty_like(g)
+                    torch.ops.raft_stir.stem_wgrad(xh, dh, weight.shape[0], g)
+                    torch.ops.raft_stir.stem_wgrad(xl, dh, weight.shape[0], t)
+                    g += t
+                    torch.ops.raft_stir.stem_wgrad(xh, dl, weight.shape[0], t)
+                    g += t
+                    return (g.to(weight.dtype),)
+                dw, = _wgrad_on(ctx.wstream, wgrad, [dh, dl, xh, xl])
+            else:
+                dyn = _nhwc(dy.to(torch.bfloat16))
+
+                def wgrad():
+                    g = torch.empty(weight.shape, device=dy.device, dtype=torch.float32)
+                    torch.ops.raft_stir.stem_wgrad(_nhwc(x), dyn, weight.shape[0], g)
+                    return (g.to(weight.dtype),)
+                dw, = _wgrad_on(ctx.wstream, wgrad, [dyn, x])
         return None, dw, None, None
 
 

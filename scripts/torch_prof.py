@@ -21,12 +21,16 @@ GLUE = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::cat", "aten::scatter
         "aten::copy", "aten::permute_copy", "aten::where", "aten::masked_fill", "aten::div", "aten::clamp", "aten::stack")
 
 
+VENDOR = ("aten::convolution", "aten::convolution_backward", "aten::mm", "aten::bmm", "aten::addmm", "aten::matmul",
+          "aten::baddbmm", "aten::_convolution")
+
+
 class GlueTrace:
     """TorchDispatchMode that attributes every glue aten op (GLUE) to the
     innermost repo source line on the Python stack (the profiler's own stacks
     come back empty for ops issued from autograd.Function bodies on ROCm)."""
 
-    def __init__(self):
+    def __init__(self, ops=GLUE):
         import traceback
         from torch.utils._python_dispatch import TorchDispatchMode
         agg = self.agg = {}
@@ -34,7 +38,7 @@ class GlueTrace:
         class Mode(TorchDispatchMode):
             def __torch_dispatch__(self, func, types, args=(), kwargs=None):
                 name = "aten::" + func.__name__.split(".")[0]
-                if name in GLUE:
+                if name in ops:
                     where = "(no repo frame)"
                     for fr in reversed(traceback.extract_stack()):
                         if ("raft_stir_amd" in fr.filename or "/scripts/" in fr.filename) and \
@@ -58,6 +62,9 @@ def main():
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--mode", default="both")
     ap.add_argument("--out", default="gpurun_out")
+    ap.add_argument("--fp32", action="store_true", help="fp32 (no autocast), the reference's default precision")
+    ap.add_argument("--vendor", action="store_true",
+                    help="attribute the library-backed aten ops (convolution, mm, bmm, ...) instead of the glue ops")
     ap.add_argument("--stacks", action="store_true",
                     help="also attribute the glue ops (copy_, fill_, cat, scatter, ...) to Python source lines")
     a = ap.parse_args()
@@ -69,7 +76,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = RAFT(make_args(small=a.small, mixed_precision=True)).to(dev).to(memory_format=torch.channels_last)
+    model = RAFT(make_args(small=a.small, mixed_precision=not a.fp32)).to(dev).to(memory_format=torch.channels_last)
     os.makedirs(a.out, exist_ok=True)
     if a.mode in ("train", "both"):
         model.train()
@@ -86,12 +93,12 @@ def main():
         for _ in range(3):
             step()
         torch.cuda.synchronize()
-        if a.stacks:
-            gt = GlueTrace()
+        if a.stacks or a.vendor:
+            gt = GlueTrace(VENDOR if a.vendor else GLUE)
             with gt.mode:
                 step()
             torch.cuda.synchronize()
-            gt.write(os.path.join(a.out, "torch_glue_train.txt"))
+            gt.write(os.path.join(a.out, "torch_vendor_train.txt" if a.vendor else "torch_glue_train.txt"))
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             step()
             torch.cuda.synchronize()

@@ -95,3 +95,21 @@ def test_stem_wgrad(cuda, cout, shape):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         enc_conv.stem(conv, x).backward(g)
     assert torch.equal(conv.weight.grad, g1)
+
+
+def test_stem_fp32_training(cuda):
+    """fp32 training (the reference's default precision) through the HIP stem:
+    split-bf16 forward and the three-product split weight gradient, vs fp64."""
+    torch.manual_seed(7)
+    conv = nn.Conv2d(3, 64, 7, stride=2, padding=3).to(cuda)
+    x = _img(2, 75, 99, cuda, 7)
+    assert enc_conv.stem_eligible(conv, x)
+    y = enc_conv.stem(conv, x)
+    assert y.dtype == torch.float32
+    g = torch.randn_like(y)
+    y.backward(g)
+    wr = conv.weight.detach().double().requires_grad_()
+    yr = F.conv2d(x.double(), wr, stride=2, padding=3)
+    yr.backward(g.double())
+    assert _rel(y, yr) < 2e-5, _rel(y, yr)
+    assert _rel(conv.weight.grad, wr.grad) < 5e-5, _rel(conv.weight.grad, wr.grad)
