@@ -321,6 +321,25 @@ class ResumableSampler(data.Sampler):
         return self.per_rank
 
 
+# Chairs feed on MI355X boxes (scripts/bench_dataloader.py, profiles/r5/feed_s29.jsonl):
+# ~50-70 pairs/s per worker; the engine consumes ~427 pairs/s per GPU, so 12
+# workers per rank (600 pairs/s, 1.4x the engine) when the CPUs allow it.
+FEED_WORKERS = 12
+
+
+def auto_workers(local_ranks=None) -> int:
+    """DataLoader workers per rank: FEED_WORKERS, capped by this process's CPU
+    share (CPUs in its affinity mask / ranks on the node, one kept for the
+    training process itself)."""
+    if local_ranks is None:
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = os.cpu_count() or 1
+    return max(0, min(FEED_WORKERS, cpus // max(1, local_ranks) - 1))
+
+
 def fetch_dataloader(args, TRAIN_DS="C+T+K+S+H", rank=None, world_size=None, pin_memory=None):
     """Per-stage DataLoader (reference core/datasets.py:199-234).
 
@@ -335,7 +354,8 @@ def fetch_dataloader(args, TRAIN_DS="C+T+K+S+H", rank=None, world_size=None, pin
     per_rank = max(1, args.batch_size // world_size)
     sampler = ResumableSampler(train_dataset, rank=rank, world_size=world_size,
                                seed=int(getattr(args, "seed", 1234)), batch_size=per_rank)
-    workers = int(getattr(args, "num_workers", 4))
+    workers = getattr(args, "num_workers", None)
+    workers = auto_workers() if workers is None or int(workers) < 0 else int(workers)
     if pin_memory is None:
         pin_memory = torch.cuda.is_available()
     loader = data.DataLoader(train_dataset, batch_size=per_rank, pin_memory=pin_memory,

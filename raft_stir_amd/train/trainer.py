@@ -73,7 +73,8 @@ def build_parser():
                    help="on-the-fly (memory-efficient) correlation, differentiable")
     p.add_argument("--data_root", default=None, help="parent of FlyingChairs_release/, Sintel/, ...")
     p.add_argument("--chairs_split", default="chairs_split.txt")
-    p.add_argument("--num_workers", type=int, default=4)
+    p.add_argument("--num_workers", type=int, default=None,
+                   help="DataLoader workers per rank (default: data.datasets.auto_workers, up to 12)")
     p.add_argument("--ckpt_dir", default="checkpoints")
     p.add_argument("--log_dir", default=None, help="JSONL/TensorBoard dir (default runs/<name>)")
     p.add_argument("--val_freq", type=int, default=5000)
@@ -267,7 +268,7 @@ def run_validation(model, args):
 
 def _spawn_worker(local_rank, gpus, argv, port):
     os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(len(gpus)),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      LOCAL_WORLD_SIZE=str(len(gpus)), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)
     args = build_parser().parse_args(argv)
     train(args)

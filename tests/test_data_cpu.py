@@ -352,3 +352,14 @@ def test_fused_resize_crop_matches_resize_then_crop(monkeypatch):
         monkeypatch.undo()
         for g, w in zip(got, want):
             assert g.shape == w.shape and np.array_equal(np.ascontiguousarray(g), np.ascontiguousarray(w)), seed
+
+
+def test_auto_workers_share_the_cpus(monkeypatch):
+    """DataLoader workers per rank: up to FEED_WORKERS, within this process's
+    CPU share (affinity / local ranks, one CPU kept for the trainer)."""
+    from raft_stir_amd.data import datasets as D
+    monkeypatch.setattr(D.os, "sched_getaffinity", lambda pid: set(range(64)))
+    assert D.auto_workers(1) == D.FEED_WORKERS
+    assert D.auto_workers(8) == 7
+    monkeypatch.setattr(D.os, "sched_getaffinity", lambda pid: {0})
+    assert D.auto_workers(1) == 0
