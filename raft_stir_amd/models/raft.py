@@ -69,6 +69,7 @@ _FUSED_PREP = True  # one-kernel input normalisation into the fnet batch
 # defer_enc (encoder conv weight gradients on the deferred stream too) is off:
 # paired A/B on one box, 3 x 30 steps: 352 pairs/s on vs 366 off (the third
 # stream then ends the backward late and its GEMMs contend with the dgrads)
+# defer_enc re-measured in round 5: 405 vs 427 pairs/s (profiles/r5/ab_defer_enc_s32.txt)
 OVERLAP = {"cnet": True, "flow": True, "defer": True, "defer_enc": False}
 
 
