@@ -19,6 +19,9 @@
 // pixel over its 64 sub-pixels (8 in-thread, 8 rows by xor shuffles); a
 // second tiny kernel gathers them into dflow (deterministic, no atomics).
 
+#include <algorithm>
+#include <cmath>
+
 #include "common.h"
 
 namespace rs {
@@ -202,37 +205,74 @@ __global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __re
 
 // Adjoint of RAFT-small's x8 bilinear upsampling with align_corners=True
 // (reference core/utils/utils.py:80-82 upflow8, the training loss path):
-//   dflow[n][c][i][j] = 8 * sum_{I, J} ah[I][i] aw[J][j] g[n][c][I][J]
+//   dflow[n][c][i][j] = 8 * sum_I ah[I][i] * (sum_J aw[J][j] g[n][c][I][J])
 // ah [8H][H], aw [8W][W]: the interpolation matrices (upsample_bilinear2d's
 // float32 source-index arithmetic, models/fused_train.py _interp_matrix).
-// Gather form, one output per thread: the nonzero rows of column i lie in
-// [floor((i - 1) / r), ceil((i + 1) / r)] for r = (H - 1) / (8H - 1); the loop
-// runs a window two wider on each side (zeros outside the band add nothing)
-// -- deterministic, no atomics.
-__global__ __launch_bounds__(256) void upflow8_bwd_kernel(const float* __restrict__ g, const float* __restrict__ ah,
-                                                          const float* __restrict__ aw, int NC, int H, int W,
-                                                          float* __restrict__ out) {
+// Separable, two gather passes (deterministic, no atomics):
+//   upflow8_cols_kernel: T[n][c][I][j] = sum_J aw[J][j] g[n][c][I][J]  (8W -> W)
+//   upflow8_rows_kernel: dflow[n][c][i][j] = 8 sum_I ah[I][i] T[n][c][I][j]  (8H -> H)
+// The nonzero rows of column j of aw lie in [floor((j - 1) r), ceil((j + 1) r)]
+// for r = (8W - 1) / (W - 1); the loops run a window two wider on each side
+// (zeros outside the band add nothing).
+// The column pass reads each g row once, coalesced, into LDS: the band's
+// weights differ per output column, so a direct gather from aw / g put every
+// lane of a load on its own cache line (327 us per RAFT-small step, vs the
+// 140 MB of g it has to read).  A block stages the W x L band weights once
+// (wb[t][j] = aw[J0(j) + t][j]), then walks its rows RG at a time.
+__device__ __forceinline__ void band(int j, int n, float r, int* lo, int* hi) {
+  // (a single input row / column: every output row / column reads it)
+  *lo = n > 1 ? max(0, (int)floorf((j - 1) * r) - 2) : 0;
+  *hi = n > 1 ? min(8 * n - 1, (int)ceilf((j + 1) * r) + 2) : 8 * n - 1;
+}
+
+constexpr int UP_ROWS = 64;  // rows (n, c, I) per block of the column pass
+
+__global__ __launch_bounds__(256) void upflow8_cols_kernel(const float* __restrict__ g, const float* __restrict__ aw,
+                                                           long nrows, int W, int L, float* __restrict__ T) {
+  extern __shared__ float sm[];
+  const int W8 = 8 * W, t = threadIdx.x;
+  const int RG = W >= 256 ? 1 : 256 / W;
+  float* wb = sm;          // [L][W]
+  float* gs = sm + L * W;  // [RG][8W]
+  const float rw = W > 1 ? (float)(W8 - 1) / (float)(W - 1) : 0.f;
+  for (int e = t; e < L * W; e += 256) {
+    const int k = e / W, j = e - k * W;
+    int J0, J1;
+    band(j, W, rw, &J0, &J1);
+    wb[e] = J0 + k <= J1 ? aw[(size_t)(J0 + k) * W + j] : 0.f;
+  }
+  const long rb = (long)blockIdx.x * UP_ROWS, re = min(nrows, rb + UP_ROWS);
+  for (long r0 = rb; r0 < re; r0 += RG) {
+    const int nr = (int)min((long)RG, re - r0);
+    __syncthreads();  // wb staged / the previous rows consumed
+    const float4* src = reinterpret_cast<const float4*>(g + (size_t)r0 * W8);
+    for (int e = t; e < nr * W8 / 4; e += 256) reinterpret_cast<float4*>(gs)[e] = src[e];
+    __syncthreads();
+    for (int u = t; u < nr * W; u += 256) {
+      const int rr = u / W, j = u - rr * W;
+      int J0, J1;
+      band(j, W, rw, &J0, &J1);
+      const float* gr = gs + rr * W8 + J0;
+      float acc = 0.f;
+      for (int k = 0; k <= J1 - J0; ++k) acc += wb[k * W + j] * gr[k];
+      T[(size_t)(r0 + rr) * W + j] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void upflow8_rows_kernel(const float* __restrict__ T, const float* __restrict__ ah,
+                                                           int NC, int H, int W, float* __restrict__ out) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = (long)NC * H * W;
   if (idx >= total) return;
   const int j = (int)(idx % W), i = (int)((idx / W) % H), nc = (int)(idx / ((long)H * W));
-  const int H8 = 8 * H, W8 = 8 * W;
-  const float rh = H > 1 ? (float)(H8 - 1) / (float)(H - 1) : 0.f;  // output rows per input row
-  const float rw = W > 1 ? (float)(W8 - 1) / (float)(W - 1) : 0.f;
-  // (a single input row / column: every output row / column reads it)
-  const int I0 = H > 1 ? max(0, (int)floorf((i - 1) * rh) - 2) : 0;
-  const int I1 = H > 1 ? min(H8 - 1, (int)ceilf((i + 1) * rh) + 2) : H8 - 1;
-  const int J0 = W > 1 ? max(0, (int)floorf((j - 1) * rw) - 2) : 0;
-  const int J1 = W > 1 ? min(W8 - 1, (int)ceilf((j + 1) * rw) + 2) : W8 - 1;
-  const float* gp = g + (size_t)nc * H8 * W8;
+  const int H8 = 8 * H;
+  const float rh = H > 1 ? (float)(H8 - 1) / (float)(H - 1) : 0.f;
+  int I0, I1;
+  band(i, H, rh, &I0, &I1);
+  const float* tp = T + (size_t)nc * H8 * W + j;
   float acc = 0.f;
-  for (int I = I0; I <= I1; ++I) {
-    const float a = ah[(size_t)I * H + i];
-    if (a == 0.f) continue;
-    float row = 0.f;
-    for (int J = J0; J <= J1; ++J) row += aw[(size_t)J * W + j] * gp[(size_t)I * W8 + J];
-    acc += a * row;
-  }
+  for (int I = I0; I <= I1; ++I) acc += ah[(size_t)I * H + i] * tp[(size_t)I * W];
   out[idx] = 8.f * acc;
 }
 
@@ -275,12 +315,26 @@ void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, c
                      partial, N, H, W, dflow);
 }
 
-void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* out,
-                        hipStream_t stream) {
-  const long total = (long)NC * H * W;
-  if (total > 0)
-    hipLaunchKernelGGL(cvx::upflow8_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, g, ah, aw,
-                       NC, H, W, out);
+// tmp: NC * 8H * W floats (the column pass)
+int upflow8_band(int W) {  // band width bound of the column pass (cvx::band)
+  if (W <= 1) return 8;
+  const float rw = (float)(8 * W - 1) / (float)(W - 1);
+  return std::min(8 * W, (int)std::ceil(2.f * rw) + 8);
+}
+
+size_t upflow8_cols_lds(int W) {
+  const int RG = W >= 256 ? 1 : 256 / W;
+  return (size_t)(upflow8_band(W) * W + RG * 8 * W) * sizeof(float);
+}
+
+void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* tmp,
+                        float* out, hipStream_t stream) {
+  const long nrows = (long)NC * 8 * H, t2 = (long)NC * H * W;
+  if (t2 == 0) return;
+  hipLaunchKernelGGL(cvx::upflow8_cols_kernel, dim3((unsigned)((nrows + cvx::UP_ROWS - 1) / cvx::UP_ROWS)), dim3(256),
+                     upflow8_cols_lds(W), stream, g, aw, nrows, W, upflow8_band(W), tmp);
+  hipLaunchKernelGGL(cvx::upflow8_rows_kernel, dim3((unsigned)((t2 + 255) / 256)), dim3(256), 0, stream, tmp, ah, NC,
+                     H, W, out);
 }
 
 }  // namespace rs

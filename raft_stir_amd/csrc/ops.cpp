@@ -37,8 +37,9 @@ void corr_lookup_bwd_launch(float* const* gpyr, const int* Hs, const int* Ws, co
                             bool dout_bf16, hipStream_t stream, int dstride);
 size_t corr_volume_split_ws(int B, int N1, int C, int levels, const int* Hs, const int* Ws);
 int corr_bwd_pitch(int N2);
-void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* out,
-                        hipStream_t stream);
+void upflow8_bwd_launch(const float* g, const float* ah, const float* aw, int NC, int H, int W, float* tmp,
+                        float* out, hipStream_t stream);
+size_t upflow8_cols_lds(int W);
 void corr_bwd_gemm_launch(const void* G, const void* Gl, int Ep, const void* f1, const void* f1l, const void* f2,
                           const void* f2l, int B, int N1, int N2, int C, void* df1, void* df2, hipStream_t stream);
 void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, const int* Ss, int levels, long rows,
@@ -454,10 +455,12 @@ Tensor upflow8_backward(const Tensor& g, const Tensor& ah, const Tensor& aw) {
                   ah.size(1) == H && aw.is_cuda() && aw.is_contiguous() && aw.scalar_type() == at::kFloat &&
                   aw.size(0) == 8 * W && aw.size(1) == W,
               "upflow8_backward: interpolation matrices [8H, H] / [8W, W] fp32");
+  TORCH_CHECK(rs::upflow8_cols_lds(W) <= 65536, "upflow8_backward: width ", W, " exceeds the column pass's LDS");
   const c10::DeviceGuard guard(g.device());
   Tensor out = at::empty({g.size(0), g.size(1), H, W}, g.options());
+  Tensor tmp = at::empty({g.size(0) * g.size(1) * 8 * H * W}, g.options());
   rs::upflow8_bwd_launch(g.data_ptr<float>(), ah.data_ptr<float>(), aw.data_ptr<float>(), g.size(0) * g.size(1), H, W,
-                         out.data_ptr<float>(), cur_stream());
+                         tmp.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
   RS_CHECK_LAUNCH();
   return out;
 }

@@ -429,10 +429,11 @@ def test_split_bf16_matches_aten(cuda, n):
     assert torch.equal(hi, want_hi) and torch.equal(lo, want_lo)
 
 
-@pytest.mark.parametrize("HW", [(46, 62), (11, 37), (1, 5)])
+@pytest.mark.parametrize("HW", [(46, 62), (11, 37), (1, 5), (7, 1)])
 def test_upflow8_backward_matches_autograd(cuda, HW):
-    """csrc/convex_upsample.hip upflow8_bwd_kernel: the adjoint of RAFT-small's
-    x8 bilinear upsampling (align_corners=True), deterministic gather form, vs
+    """csrc/convex_upsample.hip upflow8_{cols,rows}_kernel: the adjoint of
+    RAFT-small's x8 bilinear upsampling (align_corners=True), two deterministic
+    gather passes, vs
     the autograd of F.interpolate (fp32, the training forward's arithmetic)."""
     from raft_stir_amd.models.fused_train import _interp_matrix
     H, W = HW
