@@ -592,6 +592,216 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
   }
 }
 
+// ------------------------------------------------- tiled backward on MFMA
+// bf16 features, C % 64 == 0 (RAFT C = 256, RAFT-small C = 128).  Same 4 x 4
+// query tile, box and per-query fallback as otf_tile_bwd_kernel, but both
+// contractions run on MFMA:
+//   df1[q][c]    += sum_cell G[q][cell] f2[cell][c]   mfma_f32_16x16x32_bf16,
+//                   K = box cells (32 per step), 16 channels per wave and
+//                   64-channel chunk, accumulated in registers over levels;
+//   df2[cell][c]  = sum_q G[q][cell] f1[q][c]         mfma_f32_16x16x16_bf16,
+//                   K = the 16 queries, then ONE atomic per (cell, channel)
+//                   straight from the accumulators.
+// G is split into bf16 hi + lo (two MFMAs per product, fp32 accumulation), so
+// the gradient keeps ~16 mantissa bits -- the fp32 VALU kernel's accuracy at a
+// fraction of its LDS traffic.  Both GEMMs need their K dimension contiguous
+// per lane, so the gather writes G twice: [q][cell] (df1) and [cell][q] (df2);
+// f2's box chunk and f1 are staged channel-major ([c][cell], [c][q]).
+constexpr int GQP = MAXC + 8;  // Gq row pitch (bf16): 16-B reads of 16 rows cover the banks
+constexpr int QP = 20;         // Gc row pitch (bf16)
+constexpr int FP = 16;         // F1T row pitch (bf16; 2-way bank conflicts, and the block fits twice per CU)
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+template <typename GT, int CQ, bool DET>
+__global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __restrict__ f1, Lvl f2, int levels,
+                                                               const float* __restrict__ coords, int B, int H1,
+                                                               int W1, int tiles_x, int tiles_y, int per_xcd, int r,
+                                                               float scale, const GT* __restrict__ dout,
+                                                               float* __restrict__ df1, LvlMut df2) {
+  constexpr int C = CQ * 32, NCH = C / 64;
+  static_assert(C % 64 == 0, "64-channel chunks");
+  __shared__ __attribute__((aligned(16))) bf16_t Gq[2][16][GQP];   // [hi / lo][query][box cell]
+  __shared__ __attribute__((aligned(16))) bf16_t Gc[2][MAXC][QP];  // [hi / lo][box cell][query]
+  __shared__ __attribute__((aligned(16))) bf16_t F2T[64][GQP];     // f2 box, one 64-channel chunk, [c][cell]
+  __shared__ __attribute__((aligned(16))) bf16_t F1T[C][FP];       // the tile's f1, [c][query]
+  __shared__ uint8_t live[MAXC];  // box cell with a nonzero gradient
+  __shared__ int qX0[16], qY0[16], qn[16];
+  __shared__ float qfx[16], qfy[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (tile >= B * tiles_x * tiles_y) return;  // whole block, before any barrier
+  const int b = tile / (tiles_x * tiles_y), t2 = tile % (tiles_x * tiles_y);
+  const int ty = t2 / tiles_x, tx = t2 % tiles_x;
+  const int N1 = H1 * W1;
+  const int D = 2 * r + 1, K2 = D * D, E = D + 1, E2 = E * E, CH = levels * K2;
+
+  if (t < 16) {
+    const int y = ty * TQ + (t >> 2), x = tx * TQ + (t & 3);
+    qn[t] = (y < H1 && x < W1) ? y * W1 + x : -1;
+  }
+  __syncthreads();
+  for (int i = t; i < 16 * (C / 8); i += 256) {  // F1T[c][q] (zero rows for queries outside the image)
+    const int q = i / (C / 8), cg = i % (C / 8);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (qn[q] >= 0) v = *reinterpret_cast<const uint4*>(f1 + ((size_t)b * N1 + qn[q]) * C + 8 * cg);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      F1T[8 * cg + 2 * j][q] = (bf16_t)(w[j] & 0xffffu);
+      F1T[8 * cg + 2 * j + 1][q] = (bf16_t)(w[j] >> 16);
+    }
+  }
+  f32x4_t a1[NCH];  // df1: query 4 q4 + j, channel 64 k + 16 wave + r16
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) a1[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int l = 0; l < levels; ++l) {
+    const int H = f2.H[l], W = f2.W[l];
+    __syncthreads();  // the previous level's readers of q* / G / F2T are done
+    if (t < 16) {
+      const int n = qn[t] >= 0 ? qn[t] : 0;
+      const float inv = 1.f / (float)(1 << l);
+      const float cx = coords[((size_t)b * 2 + 0) * N1 + n] * inv, cy = coords[((size_t)b * 2 + 1) * N1 + n] * inv;
+      const float bx = floorf(cx), by = floorf(cy);
+      qX0[t] = (int)bx - r;
+      qY0[t] = (int)by - r;
+      qfx[t] = cx - bx;
+      qfy[t] = cy - by;
+    }
+    __syncthreads();
+    int xmn = 0x7fffffff, ymn = 0x7fffffff, xmx = -0x7fffffff, ymx = -0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (qn[q] >= 0) {
+        xmn = min(xmn, qX0[q]);
+        xmx = max(xmx, qX0[q]);
+        ymn = min(ymn, qY0[q]);
+        ymx = max(ymx, qY0[q]);
+      }
+    const bool fallback = (xmx - xmn + E) * (ymx - ymn + E) > MAXC;  // identical in every thread
+    const bf16_t* f2b = static_cast<const bf16_t*>(f2.p[l]) + (size_t)b * H * W * C;
+    for (int sub = 0; sub < (fallback ? 16 : 1); ++sub) {
+      if (fallback && qn[sub] < 0) continue;  // uniform
+      const int bx0 = fallback ? qX0[sub] : xmn, by0 = fallback ? qY0[sub] : ymn;
+      const int bw = fallback ? E : xmx - xmn + E, bh = fallback ? E : ymx - ymn + E;
+      const int nc = bw * bh, ncp = round_up(nc, 32);
+      if (sub > 0) __syncthreads();  // the previous window's readers are done
+      for (int i = t; i < 16 * ncp / 2; i += 256) {  // zero G over the padded box
+        const int q = i / (ncp / 2), c2 = i % (ncp / 2);
+        reinterpret_cast<uint32_t*>(&Gq[0][q][0])[c2] = 0u;
+        reinterpret_cast<uint32_t*>(&Gq[1][q][0])[c2] = 0u;
+      }
+      for (int i = t; i < ncp * 8; i += 256) {
+        const int cell = i >> 3, q2 = i & 7;
+        reinterpret_cast<uint32_t*>(&Gc[0][cell][0])[q2] = 0u;
+        reinterpret_cast<uint32_t*>(&Gc[1][cell][0])[q2] = 0u;
+      }
+      for (int i = t; i < ncp; i += 256) live[i] = 0;
+      __syncthreads();
+      // G[q][box cell]: each window cell (ca along x, cc along y) sums its <= 4 taps
+      for (int i = t; i < 16 * E2; i += 256) {
+        const int q = i / E2, cell = i - q * E2;
+        if (qn[q] < 0 || (fallback && q != sub)) continue;
+        const int ca = cell / E, cc = cell - ca * E;
+        const float fx = qfx[q], fy = qfy[q];
+        const GT* g = dout + ((size_t)b * N1 + qn[q]) * CH + l * K2;
+        float acc = 0.f;
+#pragma unroll
+        for (int di = 0; di < 2; ++di) {
+          const int ii = ca - di;
+          if (ii < 0 || ii >= D) continue;
+          const float wx = di == 0 ? (1.f - fx) : fx;
+#pragma unroll
+          for (int dj = 0; dj < 2; ++dj) {
+            const int jj = cc - dj;
+            if (jj < 0 || jj >= D) continue;
+            const float wy = dj == 0 ? (1.f - fy) : fy;
+            acc += wx * wy * io<GT>::ld(g + ii * D + jj);
+          }
+        }
+        acc *= scale;
+        const bf16_t hi = f2bf(acc), lo = f2bf(acc - bf2f(hi));
+        const int bc = (qY0[q] + cc - by0) * bw + (qX0[q] + ca - bx0);
+        Gq[0][q][bc] = hi;
+        Gq[1][q][bc] = lo;
+        Gc[0][bc][q] = hi;
+        Gc[1][bc][q] = lo;
+        if (acc != 0.f) live[bc] = 1;
+      }
+      __syncthreads();
+      // df2[box cell][c] = sum_q G[q][cell] f1[q][c]: wave = channel tiles wave, wave + 4, ..
+      for (int m = 0; m < ncp / 16; ++m) {
+        const int cr = 16 * m + r16;  // A row (cell) of this lane
+        const v4s_t ahi = *reinterpret_cast<const v4s_t*>(&Gc[0][cr][4 * q4]);
+        const v4s_t alo = *reinterpret_cast<const v4s_t*>(&Gc[1][cr][4 * q4]);
+        int cl[4];
+        bool ok[4], any = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // D rows of this lane: cells 16 m + 4 q4 + j
+          const int cell = 16 * m + 4 * q4 + j;
+          const int X = bx0 + cell % bw, Y = by0 + cell / bw;
+          ok[j] = cell < nc && live[cell] && X >= 0 && X < W && Y >= 0 && Y < H;
+          cl[j] = ok[j] ? Y * W + X : 0;
+          any = any || ok[j];
+        }
+        if (!__builtin_amdgcn_ballot_w64(any)) continue;  // wave-uniform: a dead 16-cell group
+        for (int n = wave; n < C / 16; n += 4) {
+          const v4s_t bf = *reinterpret_cast<const v4s_t*>(&F1T[16 * n + r16][4 * q4]);
+          f32x4_t d = {0.f, 0.f, 0.f, 0.f};
+          d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ahi, bf, d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(alo, bf, d, 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (!ok[j]) continue;
+            const size_t off = ((size_t)b * H * W + cl[j]) * C + 16 * n + r16;
+            if constexpr (DET)
+              fx_add(reinterpret_cast<unsigned long long*>(df2.p[l]) + off, d[j]);
+            else
+              atomicAdd(df2.p[l] + off, d[j]);
+          }
+        }
+      }
+      // df1[q][c] += sum_cell G[q][cell] f2[cell][c], per 64-channel chunk of f2's box
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        if (k > 0) __syncthreads();  // the previous chunk's MFMA reads of F2T are done
+        for (int i = t; i < ncp * 8; i += 256) {
+          const int cell = i >> 3, pc = i & 7;
+          const int X = bx0 + cell % bw, Y = by0 + cell / bw;
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (cell < nc && X >= 0 && X < W && Y >= 0 && Y < H)
+            v = *reinterpret_cast<const uint4*>(f2b + ((size_t)Y * W + X) * C + 64 * k + 8 * pc);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            F2T[8 * pc + 2 * j][cell] = (bf16_t)(w[j] & 0xffffu);
+            F2T[8 * pc + 2 * j + 1][cell] = (bf16_t)(w[j] >> 16);
+          }
+        }
+        __syncthreads();
+        for (int kc = 0; kc < ncp / 32; ++kc) {
+          const bf16x8_t ahi = *reinterpret_cast<const bf16x8_t*>(&Gq[0][r16][32 * kc + 8 * q4]);
+          const bf16x8_t alo = *reinterpret_cast<const bf16x8_t*>(&Gq[1][r16][32 * kc + 8 * q4]);
+          const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(&F2T[16 * wave + r16][32 * kc + 8 * q4]);
+          a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, a1[k], 0, 0, 0);
+          a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, a1[k], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // df1 rows: query 4 q4 + j, channel 64 k + 16 wave + r16
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = 4 * q4 + j;
+    if (qn[q] < 0) continue;
+    float* o = df1 + ((size_t)b * N1 + qn[q]) * C + 16 * wave + r16;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) o[64 * k] = a1[k][j];
+  }
+}
+
 // 32.32 fixed point (int64) -> fp32
 __global__ __launch_bounds__(256) void fx_to_f32_kernel(const long long* __restrict__ in, long n,
                                                         float* __restrict__ out) {
@@ -678,7 +888,26 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     const char* e2 = getenv("RS_OTF_TILE_BWD");
     return !(e && e[0] == '0') && !(e2 && e2[0] == '0');
   }();
-  if (tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+  if (tile_env && fm_bf16 && C % 64 == 0 && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+    const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
+    const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
+    const bf16_t* f1b = static_cast<const bf16_t*>(f1);
+#define RS_LM(GT)                                                                                          \
+  if (det)                                                                                                 \
+    hipLaunchKernelGGL((otf::otf_tile_bwd_mma_kernel<GT, CQ, true>), dim3(8 * per_xcd), dim3(256), 0, stream, \
+                       f1b, p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, scale,                \
+                       static_cast<const GT*>(dout), df1, d);                                               \
+  else                                                                                                     \
+    hipLaunchKernelGGL((otf::otf_tile_bwd_mma_kernel<GT, CQ, false>), dim3(8 * per_xcd), dim3(256), 0, stream, \
+                       f1b, p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, scale,                \
+                       static_cast<const GT*>(dout), df1, d)
+    switch (cq) {
+      case 2: { constexpr int CQ = 2; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
+      case 4: { constexpr int CQ = 4; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
+      default: { constexpr int CQ = 8; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
+    }
+#undef RS_LM
+  } else if (tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
     const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
     const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
 #define RS_LT(T, GT)                                                                                      \

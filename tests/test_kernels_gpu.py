@@ -186,9 +186,11 @@ def test_onthefly_tiled_forward(cuda, C, r, out_bf16):
 @pytest.mark.parametrize("C,r", [(256, 4), (128, 3), (96, 4)])
 @pytest.mark.parametrize("det", [False, True])
 def test_onthefly_tiled_backward(cuda, C, r, det):
-    """csrc/corr_onthefly.hip otf_tile_bwd_kernel (4 x 4 query tiles: cell
-    gradients gathered over the tile's bounding box, one df2 atomic per
-    (cell, channel) per tile, per-window fallback for incoherent tiles) vs
+    """csrc/corr_onthefly.hip tiled backward -- otf_tile_bwd_mma_kernel for
+    C % 64 == 0 (both contractions on MFMA, split-bf16 cell gradients),
+    otf_tile_bwd_kernel for C = 96 (4 x 4 query tiles: cell gradients gathered
+    over the tile's bounding box, one df2 atomic per (cell, channel) per tile,
+    per-window fallback for incoherent tiles) -- vs
     fp32 autograd through a per-level bilinear oracle (ops/reference.py
     corr_onthefly with the pooled levels as leaves).  Deterministic mode
     (32.32 fixed-point atomics) is bitwise repeatable."""
