@@ -3,7 +3,10 @@
 per-queue busy time, GPU-idle time, and the main-queue gaps (what the other
 queues run while the main stream waits).
 
-    python scripts/trace_streams.py gpurun_out/trace/train_kernel_trace.csv.gz
+    python scripts/trace_streams.py gpurun_out/trace/train_kernel_trace.csv.gz [A_ms B_ms]
+
+With A_ms B_ms: also list every kernel of the step that starts in [A, B] ms
+(queue, stream, start, duration) -- what each queue runs around a gap.
 """
 import collections
 import csv
@@ -13,7 +16,7 @@ import sys
 TOP = 25
 
 
-def main(path):
+def main(path, window=None):
     op = gzip.open if path.endswith(".gz") else open
     rows = list(csv.DictReader(op(path, "rt")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -87,7 +90,15 @@ def main(path):
         print(f"queue {q} top kernels:")
         for k in sorted(fam, key=fam.get, reverse=True)[:TOP]:
             print(f"  {fam[k]:7.3f} ms {n[k]:4d}x  {k}")
+    if window:
+        a, b = window
+        print(f"kernels starting in [{a}, {b}] ms (queue / stream, start, duration):")
+        for r in step:
+            s, e = T(r)
+            if a <= (s - t0) / 1e6 <= b:
+                print(f"  q{r['Queue_Id']} s{r.get('Stream_Id', '?')} {(s - t0) / 1e6:8.3f} {(e - s) / 1e3:8.1f} us  "
+                      + r["Kernel_Name"].replace("void ", "")[:90])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], (float(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else None)
