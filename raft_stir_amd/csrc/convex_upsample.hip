@@ -123,7 +123,7 @@ __global__ __launch_bounds__(WPB * 64) void convex_up_fwd_kernel(
 template <typename MT, typename GT>
 __global__ __launch_bounds__(WPB * 64) void convex_up_bwd_kernel(
     const float* __restrict__ flow, const MT* __restrict__ mask, const GT* __restrict__ dup,
-    int N, int H, int W, MT* __restrict__ dmask, float* __restrict__ partial) {
+    int N, int H, int W, MT* __restrict__ dmask, int dpitch, float* __restrict__ partial) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int a = lane >> 3, x0 = blockIdx.x * XB + wave * XW + (lane & 7), y = blockIdx.y, n = blockIdx.z;
   const bool in = x0 < W;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(WPB * 64) void convex_up_bwd_kernel(
     for (int k = 0; k < 9; ++k) dm[k][b] = p[k][b] * (dm[k][b] - dot);
   }
   if (in) {
-    MT* d = dmask + cp * 576 + 8 * a;
+    MT* d = dmask + cp * dpitch + 8 * a;
 #pragma unroll
     for (int k = 0; k < 9; ++k) st8(d + 64 * k, dm[k]);
   }
@@ -292,9 +292,9 @@ void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, i
                        static_cast<const float*>(mask), N, H, W, out);
 }
 
-// partial: scratch (N*H*W*18) fp32
+// partial: scratch (N*H*W*18) fp32; dmask: (N,H,W,dpitch), channels 0..575 written
 void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
-                          bool dup_bf16, int N, int H, int W, void* dmask, float* dflow,
+                          bool dup_bf16, int N, int H, int W, void* dmask, int dpitch, float* dflow,
                           float* partial, hipStream_t stream) {
   const long cps = (long)N * H * W;
   if (cps == 0) return;
@@ -302,7 +302,7 @@ void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, c
 #define RS_L(MT, GT)                                                                         \
   hipLaunchKernelGGL((cvx::convex_up_bwd_kernel<MT, GT>), grid, block, 0, stream, flow,     \
                      static_cast<const MT*>(mask), static_cast<const GT*>(dup), N, H, W,     \
-                     static_cast<MT*>(dmask), partial)
+                     static_cast<MT*>(dmask), dpitch, partial)
   if (mask_bf16) {
     if (dup_bf16) RS_L(bf16_t, bf16_t); else RS_L(bf16_t, float);
   } else {

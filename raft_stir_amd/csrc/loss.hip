@@ -10,6 +10,9 @@
 // in registers across the N predictions), per-block partial sums reduced
 // deterministically by a second tiny kernel; the backward is one pass that
 // writes every prediction's gradient w_i * valid * sign(pred_i - gt) / M.
+// The same forward pass also forms the training metrics of the last
+// prediction (reference train.py:62-70: mean EPE and the 1 / 3 / 5 px
+// accuracies over the valid pixels), which took ~40 small ATen launches.
 #include "common.h"
 
 namespace rs {
@@ -17,14 +20,17 @@ namespace loss {
 
 constexpr int THREADS = 256;
 
-// grid-stride over (b, y, x); B planes of HW pixels.  preds: [N][B][2][HW]
+constexpr int NACC = 6;  // loss, EPE, < 1 px, < 3 px, < 5 px, valid count
+
+// grid-stride over (b, y, x); B planes of HW pixels.  preds: [N][B][2][HW];
+// partial: [gridDim.x][NACC]
 __global__ __launch_bounds__(THREADS) void seq_loss_fwd_kernel(const float* __restrict__ preds,
                                                                 const float* __restrict__ gt,
                                                                 const float* __restrict__ valid, int N,
                                                                 int B, long HW, float gamma, float max_flow,
                                                                 float inv_m, float* __restrict__ partial) {
   const long P = (long)B * HW;
-  float acc = 0.f;
+  float acc[NACC] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (long p = (long)blockIdx.x * THREADS + threadIdx.x; p < P; p += (long)gridDim.x * THREADS) {
     const long b = p / HW, q = p - b * HW;
     const long g0 = b * 2 * HW + q;
@@ -34,35 +40,59 @@ __global__ __launch_bounds__(THREADS) void seq_loss_fwd_kernel(const float* __re
     float w = 1.f, s = 0.f;
     for (int i = N - 1; i >= 0; --i) {  // weight gamma^(N-1-i)
       const float* pr = preds + (size_t)i * B * 2 * HW + g0;
-      s += w * (fabsf(pr[0] - gu) + fabsf(pr[HW] - gv));
+      const float du = pr[0] - gu, dv = pr[HW] - gv;
+      s += w * (fabsf(du) + fabsf(dv));
+      if (i == N - 1) {  // metrics of the final prediction
+        const float epe = sqrtf(du * du + dv * dv);
+        acc[1] += epe;
+        acc[2] += epe < 1.f ? 1.f : 0.f;
+        acc[3] += epe < 3.f ? 1.f : 0.f;
+        acc[4] += epe < 5.f ? 1.f : 0.f;
+      }
       w *= gamma;
     }
-    acc += s;
+    acc[0] += s;
+    acc[5] += 1.f;
   }
-  acc = wave_sum(acc);
-  __shared__ float sm[THREADS / 64];
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __shared__ float sm[NACC][THREADS / 64];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) {
+    const float v = wave_sum(acc[k]);
+    if ((threadIdx.x & 63) == 0) sm[k][threadIdx.x >> 6] = v;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < NACC) {
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < THREADS / 64; ++k) t += sm[k];
-    partial[blockIdx.x] = t * inv_m;
+    for (int w = 0; w < THREADS / 64; ++w) t += sm[threadIdx.x][w];
+    partial[blockIdx.x * NACC + threadIdx.x] = threadIdx.x == 0 ? t * inv_m : t;
   }
 }
 
+// out[0] = loss; out[1..4] = EPE, 1 / 3 / 5 px accuracy (means over the valid
+// pixels, 0 when there are none): fixed-order fp64 sums of the block partials
 __global__ __launch_bounds__(THREADS) void sum_kernel(const float* __restrict__ partial, int n,
                                                       float* __restrict__ out) {
-  double t = 0.0;
-  for (int i = threadIdx.x; i < n; i += THREADS) t += partial[i];
-  __shared__ double sm[THREADS];
-  sm[threadIdx.x] = t;
+  __shared__ double sm[NACC][THREADS];
+  double t[NACC] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < n; i += THREADS)
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) t[k] += partial[i * NACC + k];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) sm[k][threadIdx.x] = t[k];
   __syncthreads();
   for (int s = THREADS / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sm[threadIdx.x] += sm[threadIdx.x + s];
+    if (threadIdx.x < s)
+#pragma unroll
+      for (int k = 0; k < NACC; ++k) sm[k][threadIdx.x] += sm[k][threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = (float)sm[0];
+  if (threadIdx.x == 0) {
+    const double cnt = sm[5][0] > 1.0 ? sm[5][0] : 1.0;
+    out[0] = (float)sm[0][0];
+#pragma unroll
+    for (int k = 1; k < 5; ++k) out[k] = (float)(sm[k][0] / cnt);
+  }
 }
 
 __global__ __launch_bounds__(THREADS) void seq_loss_bwd_kernel(const float* __restrict__ preds,
@@ -101,6 +131,7 @@ static int loss_grid(long P) {
   return (int)(g < 2048 ? g : 2048);
 }
 
+// partial: nblocks * loss::NACC floats; out: 5 floats (loss, EPE, 1 / 3 / 5 px)
 void seq_loss_fwd_launch(const float* preds, const float* gt, const float* valid, int N, int B, long HW,
                          float gamma, float max_flow, float* partial, int nblocks, float* out,
                          hipStream_t s) {
@@ -111,6 +142,7 @@ void seq_loss_fwd_launch(const float* preds, const float* gt, const float* valid
 }
 
 int seq_loss_blocks(long P) { return loss_grid(P); }
+int seq_loss_partials(long P) { return loss_grid(P) * loss::NACC; }
 
 void seq_loss_bwd_launch(const float* preds, const float* gt, const float* valid, int N, int B, long HW,
                          float gamma, float max_flow, const float* gout, float* grad, hipStream_t s) {

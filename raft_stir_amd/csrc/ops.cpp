@@ -59,7 +59,7 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, int N, int H, int W,
                           float* out, hipStream_t stream);
 void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
-                          bool dup_bf16, int N, int H, int W, void* dmask, float* dflow,
+                          bool dup_bf16, int N, int H, int W, void* dmask, int dpitch, float* dflow,
                           float* partial, hipStream_t stream);
 void gru_gate_zr_launch(bool bf, const void* zr, const void* h, const void* x, long P, int hd,
                         int cin, void* z, void* r, void* rhx, hipStream_t s);
@@ -465,8 +465,11 @@ Tensor upflow8_backward(const Tensor& g, const Tensor& ah, const Tensor& aw) {
   return out;
 }
 
+// dmask_out: optional (N,H,W,Cp) buffer (Cp >= 576, Cp % 8 == 0, the mask's dtype) the mask
+// gradient is written into (channels 0..575; the rest untouched) -- e.g. the fused engine's
+// padded d_mask, without a copy
 std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& mask,
-                                             const Tensor& dup) {
+                                             const Tensor& dup, const c10::optional<Tensor>& dmask_out) {
   check_gpu(flow, "flow");
   check_gpu(mask, "mask");
   check_gpu(dup, "grad");
@@ -482,10 +485,20 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
               "convex_upsample_backward: contiguous, 16-byte aligned operands required");
   const c10::DeviceGuard guard(flow.device());
   Tensor dflow = at::empty_like(flow);
-  Tensor dmask = at::empty_like(mask);
+  Tensor dmask;
+  if (dmask_out) {
+    dmask = *dmask_out;
+    TORCH_CHECK(dmask.is_cuda() && dmask.is_contiguous() && dmask.scalar_type() == mask.scalar_type() &&
+                    dmask.dim() == 4 && dmask.size(0) == N && dmask.size(1) == H && dmask.size(2) == W &&
+                    dmask.size(3) >= 576 && dmask.size(3) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(dmask.data_ptr()) & 15) == 0,
+                "convex_upsample_backward: dmask_out must be a contiguous, aligned (N,H,W,>=576) buffer of the mask's dtype");
+  } else {
+    dmask = at::empty_like(mask);
+  }
   Tensor partial = at::empty({(int64_t)N * H * W * 18}, flow.options());
   rs::convex_up_bwd_launch(flow.data_ptr<float>(), mask.data_ptr(), is_bf16(mask), dup.data_ptr(),
-                           is_bf16(dup), N, H, W, dmask.data_ptr(), dflow.data_ptr<float>(),
+                           is_bf16(dup), N, H, W, dmask.data_ptr(), (int)dmask.size(3), dflow.data_ptr<float>(),
                            partial.data_ptr<float>(), cur_stream());
   RS_CHECK_LAUNCH();
   return {dflow, dmask};
@@ -658,7 +671,7 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("corr_otf(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, bool out_bf16) -> Tensor");
   m.def("corr_otf_backward(Tensor f1, Tensor[] f2, Tensor coords, int radius, float scale, Tensor dout) -> Tensor[]");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
-  m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> Tensor[]");
+  m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad, Tensor(a!)? dmask_out=None) -> Tensor[]");
   m.def("upflow8_backward(Tensor g, Tensor ah, Tensor aw) -> Tensor");
   m.def("gru_gate_zr(Tensor zr, Tensor h, Tensor x) -> Tensor[]");
   m.def("gru_gate_q(Tensor q, Tensor z, Tensor h) -> Tensor[]");

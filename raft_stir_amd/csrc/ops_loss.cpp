@@ -10,6 +10,7 @@ namespace rs {
 void seq_loss_fwd_launch(const float* preds, const float* gt, const float* valid, int N, int B, long HW,
                          float gamma, float max_flow, float* partial, int nblocks, float* out, hipStream_t s);
 int seq_loss_blocks(long P);
+int seq_loss_partials(long P);
 void seq_loss_bwd_launch(const float* preds, const float* gt, const float* valid, int N, int B, long HW,
                          float gamma, float max_flow, const float* gout, float* grad, hipStream_t s);
 }  // namespace rs
@@ -35,19 +36,21 @@ void check(const Tensor& preds, const Tensor& gt, const Tensor& valid) {
               "seq_loss: valid must be (B,H,W)");
 }
 
-Tensor seq_loss(const Tensor& preds, const Tensor& gt, const Tensor& valid, double gamma, double max_flow) {
+// returns (loss, metrics): metrics = [EPE, 1 px, 3 px, 5 px] of the last prediction over the valid pixels
+std::vector<Tensor> seq_loss(const Tensor& preds, const Tensor& gt, const Tensor& valid, double gamma,
+                             double max_flow) {
   check(preds, gt, valid);
   const c10::DeviceGuard guard(preds.device());
   const int N = preds.size(0), B = gt.size(0);
   const long HW = (long)gt.size(2) * gt.size(3);
   const int nb = rs::seq_loss_blocks((long)B * HW);
-  Tensor partial = at::empty({nb}, gt.options());
-  Tensor out = at::empty({}, gt.options());
+  Tensor partial = at::empty({rs::seq_loss_partials((long)B * HW)}, gt.options());
+  Tensor out = at::empty({5}, gt.options());
   rs::seq_loss_fwd_launch(preds.data_ptr<float>(), gt.data_ptr<float>(), valid.data_ptr<float>(), N, B, HW,
                           (float)gamma, (float)max_flow, partial.data_ptr<float>(), nb, out.data_ptr<float>(),
                           stream());
   RS_CHECK_LAUNCH();
-  return out;
+  return {out.select(0, 0), out.narrow(0, 1, 4)};
 }
 
 Tensor seq_loss_backward(const Tensor& grad_out, const Tensor& preds, const Tensor& gt, const Tensor& valid,
@@ -68,7 +71,7 @@ Tensor seq_loss_backward(const Tensor& grad_out, const Tensor& preds, const Tens
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
-  m.def("seq_loss(Tensor preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
+  m.def("seq_loss(Tensor preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor[]");
   m.def("seq_loss_backward(Tensor grad, Tensor preds, Tensor gt, Tensor valid, float gamma, float max_flow) "
         "-> Tensor");
 }

@@ -648,8 +648,8 @@ class FusedTrainLoop(torch.autograd.Function):
         if g_up is None:
             g_up = torch.zeros(n, 2, 8 * H, 8 * W, device=dev)
         flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
-        dflow, dmask = R.convex_upsample_backward(flows, S["mask"], g_up.contiguous())
-        S["d_mask"][..., :576].copy_(dmask)
+        # the mask gradient straight into the padded d_mask slots (channels 576.. stay zero)
+        dflow, _ = R.convex_upsample_backward(flows, S["mask"], g_up.contiguous(), S["d_mask"])
         S["d_flow"][..., :2].copy_(dflow.permute(0, 2, 3, 1))
         for i in reversed(range(iters)):
             hx, hx1, head = sl(S["hx"], i), sl(S["hx"], i + 1), sl(S["head"], i)

@@ -6,9 +6,10 @@ Unlike the reference, metrics are returned as device tensors (no ``.item()``
 host sync per step); the logger materialises them every SUM_FREQ steps.
 
 When the predictions are consecutive views of one (N, B, 2, H, W) tensor on
-the GPU (the fused training engine returns them that way) the loss is one
-fused HIP pass forward and one backward (csrc/loss.hip) instead of ~6 ATen
-kernels per prediction each way.
+the GPU (the fused training engine returns them that way) the loss and the
+metrics are one fused HIP pass forward and the loss gradient one pass
+backward (csrc/loss.hip), instead of ~6 ATen kernels per prediction each
+way plus ~40 for the metrics.
 """
 from __future__ import annotations
 
@@ -22,10 +23,12 @@ class _SeqLoss(torch.autograd.Function):
     def forward(ctx, preds, gt, valid, gamma, max_flow):
         ctx.save_for_backward(preds, gt, valid)
         ctx.gamma, ctx.max_flow = gamma, max_flow
-        return torch.ops.raft_stir.seq_loss(preds, gt, valid, gamma, max_flow)
+        loss, metrics = torch.ops.raft_stir.seq_loss(preds, gt, valid, gamma, max_flow)
+        ctx.mark_non_differentiable(metrics)
+        return loss, metrics
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _gm):
         preds, gt, valid = ctx.saved_tensors
         gp = torch.ops.raft_stir.seq_loss_backward(g.float().reshape(()), preds, gt, valid, ctx.gamma,
                                                    ctx.max_flow)
@@ -58,11 +61,9 @@ def sequence_loss(flow_preds, flow_gt, valid, gamma=0.8, max_flow=MAX_FLOW, sync
     if stacked is not None:
         gt = flow_gt.float().contiguous()
         vf = valid.float().contiguous()
-        loss = _SeqLoss.apply(stacked, gt, vf, float(gamma), float(max_flow))
-        with torch.no_grad():
-            mag = torch.sum(gt ** 2, dim=1).sqrt()
-            v = (vf >= 0.5) & (mag < max_flow)
-            metrics = flow_metrics(flow_preds[-1].detach(), gt, v)
+        # the kernel also forms the last prediction's metrics (flow_metrics' semantics)
+        loss, m = _SeqLoss.apply(stacked, gt, vf, float(gamma), float(max_flow))
+        metrics = {"epe": m[0], "1px": m[1], "3px": m[2], "5px": m[3]}
         if sync_metrics:
             metrics = {k: float(t) for k, t in metrics.items()}
         return loss, metrics

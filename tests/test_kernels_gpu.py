@@ -269,6 +269,14 @@ def test_convex_upsample(cuda, mask_bf16):
     torch.testing.assert_close(fb.grad.cpu(), fa.grad, rtol=1e-4, atol=1e-3)
     tol = 3e-2 if mask_bf16 else 1e-4
     torch.testing.assert_close(mb.grad.float().cpu(), ma.grad, rtol=tol, atol=tol)
+    # dmask_out: written in place into a padded (N, H, W, 640) buffer, pad channels untouched
+    mn = mb.detach().permute(0, 2, 3, 1).contiguous()
+    pad = torch.full((N, H, W, 640), 7.0, device=cuda, dtype=dt)
+    df, dm = torch.ops.raft_stir.convex_upsample_backward(fb.detach(), mn, gout.to(cuda), pad)
+    assert dm.data_ptr() == pad.data_ptr()
+    assert torch.equal(pad[..., :576], mb.grad.permute(0, 2, 3, 1))
+    assert bool((pad[..., 576:] == 7.0).all())
+    torch.testing.assert_close(df, fb.grad)
 
 
 @pytest.mark.parametrize("sep", [True, False])

@@ -23,6 +23,8 @@ def test_seq_loss_matches_composite(cuda):
     assert _stacked(preds) is not None
     gt = torch.randn(B, 2, H, W, device=cuda) * 20
     gt[0, :, :4] = 500.0                        # |gt| >= max_flow -> masked
+    with torch.no_grad():  # the last prediction within a few px of gt: nontrivial px accuracies
+        base[(N - 1) * B:] = gt + torch.randn_like(gt) * 3
     valid = (torch.rand(B, H, W, device=cuda) > 0.3).float()
     loss, metrics = sequence_loss(preds, gt, valid, 0.8, sync_metrics=False)
     base2 = base.detach().clone().requires_grad_(True)
@@ -32,6 +34,12 @@ def test_seq_loss_matches_composite(cuda):
     (ref * 3).backward()
     torch.testing.assert_close(base.grad, base2.grad, atol=1e-9, rtol=1e-6)
     assert set(metrics) == {"epe", "1px", "3px", "5px"}
+    # the kernel's metrics vs flow_metrics over the same valid mask (last prediction)
+    from raft_stir_amd.train.loss import flow_metrics
+    mag = torch.sum(gt ** 2, dim=1).sqrt()
+    want = flow_metrics(preds[-1].detach(), gt, (valid >= 0.5) & (mag < 400))
+    for k in want:
+        torch.testing.assert_close(metrics[k], want[k], atol=1e-5, rtol=1e-5)
 
 
 def test_separate_preds_use_composite(cuda):
