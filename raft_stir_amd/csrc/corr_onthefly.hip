@@ -604,14 +604,21 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
 //                   straight from the accumulators.
 // G is split into bf16 hi + lo (two MFMAs per product, fp32 accumulation), so
 // the gradient keeps ~16 mantissa bits -- the fp32 VALU kernel's accuracy at a
-// fraction of its LDS traffic.  Both GEMMs need their K dimension contiguous
-// per lane, so the gather writes G twice: [q][cell] (df1) and [cell][q] (df2);
-// f2's box chunk and f1 are staged channel-major ([c][cell], [c][q]).
-constexpr int GQP = MAXC + 8;  // Gq row pitch (bf16): 16-B reads of 16 rows cover the banks
-constexpr int QP = 20;         // Gc row pitch (bf16)
-constexpr int FP = 16;         // F1T row pitch (bf16; 2-way bank conflicts, and the block fits twice per CU)
+// fraction of its LDS traffic.  Every operand stays in its natural row-major
+// layout in LDS -- G [q][cell], f2's box chunk [cell][c], f1 [q][c], all
+// staged with plain 16-byte copies -- and the operands whose K runs down the
+// rows (G^T for df2, f2 for df1, f1 for df2) are gathered by
+// ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns
+// 4p..4p+3; lane i receives column i of the 4 rows).
+constexpr int GQP = MAXC + 8;  // G row pitch (bf16): the 16-B reads of 16 rows cover the banks
+constexpr int F2P = 72;        // f2 chunk row pitch (bf16, 144 B): the tr16 reads of 4 rows hit disjoint banks
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s_t otf_tr16(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s_t*)((__attribute__((address_space(3))) bf16_t*)p));
+}
 
 template <typename GT, int CQ, bool DET>
 __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __restrict__ f1, Lvl f2, int levels,
@@ -620,16 +627,17 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
                                                                float scale, const GT* __restrict__ dout,
                                                                float* __restrict__ df1, LvlMut df2) {
   constexpr int C = CQ * 32, NCH = C / 64;
+  constexpr int F1P = C + 16;  // f1 row pitch (bf16): rows 8 banks apart for the tr16 reads
   static_assert(C % 64 == 0, "64-channel chunks");
-  __shared__ __attribute__((aligned(16))) bf16_t Gq[2][16][GQP];   // [hi / lo][query][box cell]
-  __shared__ __attribute__((aligned(16))) bf16_t Gc[2][MAXC][QP];  // [hi / lo][box cell][query]
-  __shared__ __attribute__((aligned(16))) bf16_t F2T[64][GQP];     // f2 box, one 64-channel chunk, [c][cell]
-  __shared__ __attribute__((aligned(16))) bf16_t F1T[C][FP];       // the tile's f1, [c][query]
+  __shared__ __attribute__((aligned(16))) bf16_t Gq[2][16][GQP];  // [hi / lo][query][box cell]
+  __shared__ __attribute__((aligned(16))) bf16_t F2s[MAXC][F2P];  // f2 box, one 64-channel chunk, [cell][c]
+  __shared__ __attribute__((aligned(16))) bf16_t F1s[16][F1P];    // the tile's f1, [query][c]
   __shared__ uint8_t live[MAXC];  // box cell with a nonzero gradient
   __shared__ int qX0[16], qY0[16], qn[16];
   __shared__ float qfx[16], qfy[16];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int r16 = lane & 15, q4 = lane >> 4;
+  const int tq = r16 >> 2, tp = r16 & 3;  // tr16 address roles: row tq, columns 4 tp .. + 4
   const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (tile >= B * tiles_x * tiles_y) return;  // whole block, before any barrier
   const int b = tile / (tiles_x * tiles_y), t2 = tile % (tiles_x * tiles_y);
@@ -642,16 +650,11 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
     qn[t] = (y < H1 && x < W1) ? y * W1 + x : -1;
   }
   __syncthreads();
-  for (int i = t; i < 16 * (C / 8); i += 256) {  // F1T[c][q] (zero rows for queries outside the image)
+  for (int i = t; i < 16 * (C / 8); i += 256) {  // f1 rows (zero for queries outside the image)
     const int q = i / (C / 8), cg = i % (C / 8);
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (qn[q] >= 0) v = *reinterpret_cast<const uint4*>(f1 + ((size_t)b * N1 + qn[q]) * C + 8 * cg);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      F1T[8 * cg + 2 * j][q] = (bf16_t)(w[j] & 0xffffu);
-      F1T[8 * cg + 2 * j + 1][q] = (bf16_t)(w[j] >> 16);
-    }
+    *reinterpret_cast<uint4*>(&F1s[q][8 * cg]) = v;
   }
   f32x4_t a1[NCH];  // df1: query 4 q4 + j, channel 64 k + 16 wave + r16
 #pragma unroll
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
 
   for (int l = 0; l < levels; ++l) {
     const int H = f2.H[l], W = f2.W[l];
-    __syncthreads();  // the previous level's readers of q* / G / F2T are done
+    __syncthreads();  // the previous level's readers of q* / G / F2s are done
     if (t < 16) {
       const int n = qn[t] >= 0 ? qn[t] : 0;
       const float inv = 1.f / (float)(1 << l);
@@ -693,11 +696,6 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
         reinterpret_cast<uint32_t*>(&Gq[0][q][0])[c2] = 0u;
         reinterpret_cast<uint32_t*>(&Gq[1][q][0])[c2] = 0u;
       }
-      for (int i = t; i < ncp * 8; i += 256) {
-        const int cell = i >> 3, q2 = i & 7;
-        reinterpret_cast<uint32_t*>(&Gc[0][cell][0])[q2] = 0u;
-        reinterpret_cast<uint32_t*>(&Gc[1][cell][0])[q2] = 0u;
-      }
       for (int i = t; i < ncp; i += 256) live[i] = 0;
       __syncthreads();
       // G[q][box cell]: each window cell (ca along x, cc along y) sums its <= 4 taps
@@ -726,16 +724,14 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
         const int bc = (qY0[q] + cc - by0) * bw + (qX0[q] + ca - bx0);
         Gq[0][q][bc] = hi;
         Gq[1][q][bc] = lo;
-        Gc[0][bc][q] = hi;
-        Gc[1][bc][q] = lo;
         if (acc != 0.f) live[bc] = 1;
       }
       __syncthreads();
       // df2[box cell][c] = sum_q G[q][cell] f1[q][c]: wave = channel tiles wave, wave + 4, ..
       for (int m = 0; m < ncp / 16; ++m) {
-        const int cr = 16 * m + r16;  // A row (cell) of this lane
-        const v4s_t ahi = *reinterpret_cast<const v4s_t*>(&Gc[0][cr][4 * q4]);
-        const v4s_t alo = *reinterpret_cast<const v4s_t*>(&Gc[1][cr][4 * q4]);
+        // A = G^T: rows (queries) 4 q4 + tq, columns (cells) 16 m + 4 tp
+        const v4s_t ahi = otf_tr16(&Gq[0][4 * q4 + tq][16 * m + 4 * tp]);
+        const v4s_t alo = otf_tr16(&Gq[1][4 * q4 + tq][16 * m + 4 * tp]);
         int cl[4];
         bool ok[4], any = false;
 #pragma unroll
@@ -748,7 +744,7 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
         }
         if (!__builtin_amdgcn_ballot_w64(any)) continue;  // wave-uniform: a dead 16-cell group
         for (int n = wave; n < C / 16; n += 4) {
-          const v4s_t bf = *reinterpret_cast<const v4s_t*>(&F1T[16 * n + r16][4 * q4]);
+          const v4s_t bf = otf_tr16(&F1s[4 * q4 + tq][16 * n + 4 * tp]);  // B = f1: rows = queries
           f32x4_t d = {0.f, 0.f, 0.f, 0.f};
           d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ahi, bf, d, 0, 0, 0);
           d = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(alo, bf, d, 0, 0, 0);
@@ -766,25 +762,23 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
       // df1[q][c] += sum_cell G[q][cell] f2[cell][c], per 64-channel chunk of f2's box
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
-        if (k > 0) __syncthreads();  // the previous chunk's MFMA reads of F2T are done
+        if (k > 0) __syncthreads();  // the previous chunk's MFMA reads of F2s are done
         for (int i = t; i < ncp * 8; i += 256) {
           const int cell = i >> 3, pc = i & 7;
           const int X = bx0 + cell % bw, Y = by0 + cell / bw;
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
           if (cell < nc && X >= 0 && X < W && Y >= 0 && Y < H)
             v = *reinterpret_cast<const uint4*>(f2b + ((size_t)Y * W + X) * C + 64 * k + 8 * pc);
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            F2T[8 * pc + 2 * j][cell] = (bf16_t)(w[j] & 0xffffu);
-            F2T[8 * pc + 2 * j + 1][cell] = (bf16_t)(w[j] >> 16);
-          }
+          *reinterpret_cast<uint4*>(&F2s[cell][8 * pc]) = v;
         }
         __syncthreads();
         for (int kc = 0; kc < ncp / 32; ++kc) {
           const bf16x8_t ahi = *reinterpret_cast<const bf16x8_t*>(&Gq[0][r16][32 * kc + 8 * q4]);
           const bf16x8_t alo = *reinterpret_cast<const bf16x8_t*>(&Gq[1][r16][32 * kc + 8 * q4]);
-          const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(&F2T[16 * wave + r16][32 * kc + 8 * q4]);
+          // B = f2: rows (cells) 32 kc + 8 q4 + tq (+ 4), columns 16 wave + 4 tp
+          const v4s_t b0 = otf_tr16(&F2s[32 * kc + 8 * q4 + tq][16 * wave + 4 * tp]);
+          const v4s_t b1 = otf_tr16(&F2s[32 * kc + 8 * q4 + 4 + tq][16 * wave + 4 * tp]);
+          const bf16x8_t bv = bf16x8_t{b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, a1[k], 0, 0, 0);
           a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, a1[k], 0, 0, 0);
         }
