@@ -611,7 +611,8 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
 // ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns
 // 4p..4p+3; lane i receives column i of the 4 rows).
 constexpr int GQP = MAXC + 8;  // G row pitch (bf16): the 16-B reads of 16 rows cover the banks
-constexpr int F2P = 72;        // f2 chunk row pitch (bf16, 144 B): the tr16 reads of 4 rows hit disjoint banks
+constexpr int F2C = 32;        // f2 box chunk: 32 channels (the block fits three times per CU)
+constexpr int F2P = 48;        // f2 chunk row pitch (bf16, 96 B): the tr16 reads of 4 rows hit disjoint banks
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 
@@ -626,11 +627,11 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
                                                                int W1, int tiles_x, int tiles_y, int per_xcd, int r,
                                                                float scale, const GT* __restrict__ dout,
                                                                float* __restrict__ df1, LvlMut df2) {
-  constexpr int C = CQ * 32, NCH = C / 64;
+  constexpr int C = CQ * 32, NCH = C / F2C;
   constexpr int F1P = C + 16;  // f1 row pitch (bf16): rows 8 banks apart for the tr16 reads
-  static_assert(C % 64 == 0, "64-channel chunks");
+  static_assert(C % 64 == 0, "C % 64");
   __shared__ __attribute__((aligned(16))) bf16_t Gq[2][16][GQP];  // [hi / lo][query][box cell]
-  __shared__ __attribute__((aligned(16))) bf16_t F2s[MAXC][F2P];  // f2 box, one 64-channel chunk, [cell][c]
+  __shared__ __attribute__((aligned(16))) bf16_t F2s[MAXC][F2P];  // f2 box, one 32-channel chunk, [cell][c]
   __shared__ __attribute__((aligned(16))) bf16_t F1s[16][F1P];    // the tile's f1, [query][c]
   __shared__ uint8_t live[MAXC];  // box cell with a nonzero gradient
   __shared__ int qX0[16], qY0[16], qn[16];
@@ -656,7 +657,10 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
     if (qn[q] >= 0) v = *reinterpret_cast<const uint4*>(f1 + ((size_t)b * N1 + qn[q]) * C + 8 * cg);
     *reinterpret_cast<uint4*>(&F1s[q][8 * cg]) = v;
   }
-  f32x4_t a1[NCH];  // df1: query 4 q4 + j, channel 64 k + 16 wave + r16
+  // df1: query 4 q4 + j, channel 32 k + 16 (wave & 1) + r16; waves 0-1 and 2-3 take
+  // alternate 32-cell K steps of the same tiles (summed in LDS at the end)
+  const int wn = wave & 1, wk = wave >> 1;
+  f32x4_t a1[NCH];
 #pragma unroll
   for (int k = 0; k < NCH; ++k) a1[k] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -759,25 +763,25 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
           }
         }
       }
-      // df1[q][c] += sum_cell G[q][cell] f2[cell][c], per 64-channel chunk of f2's box
+      // df1[q][c] += sum_cell G[q][cell] f2[cell][c], per 32-channel chunk of f2's box
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         if (k > 0) __syncthreads();  // the previous chunk's MFMA reads of F2s are done
-        for (int i = t; i < ncp * 8; i += 256) {
-          const int cell = i >> 3, pc = i & 7;
+        for (int i = t; i < ncp * 4; i += 256) {
+          const int cell = i >> 2, pc = i & 3;
           const int X = bx0 + cell % bw, Y = by0 + cell / bw;
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
           if (cell < nc && X >= 0 && X < W && Y >= 0 && Y < H)
-            v = *reinterpret_cast<const uint4*>(f2b + ((size_t)Y * W + X) * C + 64 * k + 8 * pc);
+            v = *reinterpret_cast<const uint4*>(f2b + ((size_t)Y * W + X) * C + F2C * k + 8 * pc);
           *reinterpret_cast<uint4*>(&F2s[cell][8 * pc]) = v;
         }
         __syncthreads();
-        for (int kc = 0; kc < ncp / 32; ++kc) {
+        for (int kc = wk; kc < ncp / 32; kc += 2) {
           const bf16x8_t ahi = *reinterpret_cast<const bf16x8_t*>(&Gq[0][r16][32 * kc + 8 * q4]);
           const bf16x8_t alo = *reinterpret_cast<const bf16x8_t*>(&Gq[1][r16][32 * kc + 8 * q4]);
-          // B = f2: rows (cells) 32 kc + 8 q4 + tq (+ 4), columns 16 wave + 4 tp
-          const v4s_t b0 = otf_tr16(&F2s[32 * kc + 8 * q4 + tq][16 * wave + 4 * tp]);
-          const v4s_t b1 = otf_tr16(&F2s[32 * kc + 8 * q4 + 4 + tq][16 * wave + 4 * tp]);
+          // B = f2: rows (cells) 32 kc + 8 q4 + tq (+ 4), columns 16 wn + 4 tp
+          const v4s_t b0 = otf_tr16(&F2s[32 * kc + 8 * q4 + tq][16 * wn + 4 * tp]);
+          const v4s_t b1 = otf_tr16(&F2s[32 * kc + 8 * q4 + 4 + tq][16 * wn + 4 * tp]);
           const bf16x8_t bv = bf16x8_t{b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, a1[k], 0, 0, 0);
           a1[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, a1[k], 0, 0, 0);
@@ -785,14 +789,26 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
       }
     }
   }
-  // df1 rows: query 4 q4 + j, channel 64 k + 16 wave + r16
+  // df1: waves 2-3 hand their K-half to waves 0-1 through LDS (the F2s area), fixed order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&F2s[0][0]);  // [2 waves][NCH][4][64 lanes]
+  static_assert(2 * NCH * 4 * 64 * 4 <= (int)sizeof(F2s), "df1 hand-off fits in F2s");
+  if (wk == 1) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = 4 * q4 + j;
-    if (qn[q] < 0) continue;
-    float* o = df1 + ((size_t)b * N1 + qn[q]) * C + 16 * wave + r16;
+    for (int k = 0; k < NCH; ++k)
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) o[64 * k] = a1[k][j];
+      for (int j = 0; j < 4; ++j) red[((wn * NCH + k) * 4 + j) * 64 + lane] = a1[k][j];
+  }
+  __syncthreads();
+  if (wk == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * q4 + j;
+      if (qn[q] < 0) continue;
+      float* o = df1 + ((size_t)b * N1 + qn[q]) * C + 16 * wn + r16;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) o[F2C * k] = a1[k][j] + red[((wn * NCH + k) * 4 + j) * 64 + lane];
+    }
   }
 }
 

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5 session 42: OTF MFMA backward with row-major staging + tr16 reads (tests, microbench, OTF training).
+# Round 5 session 42-43: OTF MFMA backward (row-major staging + tr16 reads; 32-channel f2 chunks) (tests, microbench, OTF training).
 set -o pipefail
-OUT=gpurun_out/r5s42
+OUT=gpurun_out/r5s${SESSION:-42}
 mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
