@@ -118,6 +118,51 @@ __global__ __launch_bounds__(256) void bwd_fin_kernel(const float* __restrict__ 
   }
 }
 
+// Context features of the update block (reference core/raft.py:108-110):
+// net, inp = split(cnet); net = tanh(net); inp = relu(inp), written straight
+// into the fused engine's hidden-state slot and context buffer (row pitches
+// hxp / ip), and the adjoint from the engine's fp32 gradient rows G (pitch gp):
+//   dcnet = [G_h * (1 - tanh^2) | G_inp * (inp > 0)]
+// -- one pass each way instead of split / tanh / relu / copies forward and
+// casts / tanh / relu backward / cat backward.
+template <typename T>
+__global__ __launch_bounds__(256) void ctx_act_kernel(const T* __restrict__ cn, long P, int hd, int cd,
+                                                      T* __restrict__ hx, int hxp, T* __restrict__ inp, int ip) {
+  const int ct = hd + cd;
+  const long total = P * ct;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / ct;
+    const int c = (int)(i - p * ct);
+    const float v = io<T>::ld(cn + i);
+    if (c < hd)
+      io<T>::st(hx + p * hxp + c, tanhf_(v));
+    else
+      io<T>::st(inp + p * ip + (c - hd), fmaxf(v, 0.f));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ctx_act_bwd_kernel(const float* __restrict__ G, int gp,
+                                                          const T* __restrict__ hx, int hxp,
+                                                          const T* __restrict__ inp, int ip, long P, int hd,
+                                                          int cd, T* __restrict__ dcn) {
+  const int ct = hd + cd;
+  const long total = P * ct;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / ct;
+    const int c = (int)(i - p * ct);
+    const float g = G[p * gp + c];
+    float d;
+    if (c < hd) {
+      const float t = io<T>::ld(hx + p * hxp + c);
+      d = g * (1.f - t * t);
+    } else {
+      d = io<T>::ld(inp + p * ip + (c - hd)) > 0.f ? g : 0.f;
+    }
+    io<T>::st(dcn + i, d);
+  }
+}
+
 inline unsigned grid_for(long total) {
   long g = (total + 255) / 256;
   if (g > 65535L * 4) g = 65535L * 4;
@@ -181,6 +226,20 @@ void gru_bwd_fin_launch(bool bf, const float* dhd, const void* drhx, const void*
   RS_GRU_T(bf, hipLaunchKernelGGL(gru::bwd_fin_kernel<T>, dim3(gru::grid_for(total)), dim3(256),
                                   0, s, dhd, (const T*)drhx, (const T*)r, (const T*)dhx, P, hd,
                                   cin, (T*)dh, (T*)dx));
+}
+
+void ctx_act_launch(bool bf, const void* cn, long P, int hd, int cd, void* hx, int hxp, void* inp, int ip,
+                    hipStream_t s) {
+  const long total = P * (hd + cd);
+  RS_GRU_T(bf, hipLaunchKernelGGL(gru::ctx_act_kernel<T>, dim3(gru::grid_for(total)), dim3(256), 0, s,
+                                  (const T*)cn, P, hd, cd, (T*)hx, hxp, (T*)inp, ip));
+}
+
+void ctx_act_bwd_launch(bool bf, const float* G, int gp, const void* hx, int hxp, const void* inp, int ip, long P,
+                        int hd, int cd, void* dcn, hipStream_t s) {
+  const long total = P * (hd + cd);
+  RS_GRU_T(bf, hipLaunchKernelGGL(gru::ctx_act_bwd_kernel<T>, dim3(gru::grid_for(total)), dim3(256), 0, s, G,
+                                  gp, (const T*)hx, hxp, (const T*)inp, ip, P, hd, cd, (T*)dcn));
 }
 
 }  // namespace rs

@@ -61,6 +61,10 @@ void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, i
 void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
                           bool dup_bf16, int N, int H, int W, void* dmask, int dpitch, float* dflow,
                           float* partial, hipStream_t stream);
+void ctx_act_launch(bool bf, const void* cn, long P, int hd, int cd, void* hx, int hxp, void* inp, int ip,
+                    hipStream_t s);
+void ctx_act_bwd_launch(bool bf, const float* G, int gp, const void* hx, int hxp, const void* inp, int ip, long P,
+                        int hd, int cd, void* dcn, hipStream_t s);
 void gru_gate_zr_launch(bool bf, const void* zr, const void* h, const void* x, long P, int hd,
                         int cin, void* z, void* r, void* rhx, hipStream_t s);
 void gru_gate_q_launch(bool bf, const void* q, const void* z, const void* h, long P, int hd,
@@ -319,7 +323,18 @@ std::vector<Tensor> corr_volume_backward(const std::vector<Tensor>& gpyr, const 
   rs::pyr_grad_fold_launch(ptrs, Hs, Ws, Ss, gpyr.size(), (long)B * N1, (float)scale, cur_stream(), G.data_ptr(), Ep,
                            split ? Gl.data_ptr() : nullptr);
   RS_CHECK_LAUNCH();
-  Tensor df1 = at::empty_like(f1), df2 = at::empty_like(f2);
+  // df1 and df2 as the two halves of one buffer when they have the same size
+  // (the feature encoder ran both images as one batch: the caller can then
+  // hand the whole buffer back as that batch's gradient, no concatenation)
+  Tensor df1, df2;
+  if (f1.numel() == f2.numel()) {
+    Tensor both = at::empty({2, f1.numel()}, f1.options());
+    df1 = both[0].view(f1.sizes());
+    df2 = both[1].view(f2.sizes());
+  } else {
+    df1 = at::empty_like(f1);
+    df2 = at::empty_like(f2);
+  }
   if (split) {
     TORCH_CHECK((uintptr_t)f1.data_ptr() % 16 == 0 && (uintptr_t)f2.data_ptr() % 16 == 0,
                 "corr_volume_backward: fp32 features must be 16-B aligned");
@@ -508,6 +523,44 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
 // All inputs are NHWC-contiguous, viewed as (P, channels).
 int64_t pixels(const Tensor& t) { return t.numel() / t.size(-1); }
 
+// cn: (B,H,W,hd+cd) contiguous; hx: (B,H,W,>=hd) and inp: (B,H,W,cd), contiguous rows, cn's dtype
+void context_act(const Tensor& cn, const Tensor& hx, const Tensor& inp, int64_t hd) {
+  check_gpu(cn, "cn");
+  check_dtype(cn, {at::kFloat, at::kBFloat16}, "cn");
+  TORCH_CHECK(cn.dim() == 4 && hx.dim() == 4 && inp.dim() == 4 && cn.is_contiguous() && hx.is_contiguous() &&
+                  inp.is_contiguous() && hx.scalar_type() == cn.scalar_type() && inp.scalar_type() == cn.scalar_type(),
+              "context_act: contiguous NHWC tensors of one dtype");
+  const int64_t cd = cn.size(3) - hd;
+  TORCH_CHECK(hd > 0 && cd > 0 && hx.size(3) >= hd && inp.size(3) == cd && hx.sizes().slice(0, 3) == cn.sizes().slice(0, 3) &&
+                  inp.sizes().slice(0, 3) == cn.sizes().slice(0, 3),
+              "context_act: shapes");
+  const c10::DeviceGuard guard(cn.device());
+  const long P = cn.size(0) * cn.size(1) * cn.size(2);
+  rs::ctx_act_launch(is_bf16(cn), cn.data_ptr(), P, (int)hd, (int)cd, hx.data_ptr(), (int)hx.size(3), inp.data_ptr(),
+                     (int)cd, cur_stream());
+  RS_CHECK_LAUNCH();
+}
+
+// G: (B,H,W,gp) fp32 gradient rows [d h | d inp | ...]; hx / inp as context_act left them
+Tensor context_act_backward(const Tensor& G, const Tensor& hx, const Tensor& inp, int64_t hd) {
+  check_gpu(G, "G");
+  check_dtype(G, {at::kFloat}, "G");
+  TORCH_CHECK(G.dim() == 4 && hx.dim() == 4 && inp.dim() == 4 && G.is_contiguous() && hx.is_contiguous() &&
+                  inp.is_contiguous() && hx.scalar_type() == inp.scalar_type(),
+              "context_act_backward: contiguous NHWC tensors");
+  const int64_t cd = inp.size(3);
+  TORCH_CHECK(hd > 0 && G.size(3) >= hd + cd && hx.size(3) >= hd && hx.sizes().slice(0, 3) == G.sizes().slice(0, 3) &&
+                  inp.sizes().slice(0, 3) == G.sizes().slice(0, 3),
+              "context_act_backward: shapes");
+  const c10::DeviceGuard guard(G.device());
+  Tensor dcn = at::empty({G.size(0), G.size(1), G.size(2), hd + cd}, hx.options());
+  const long P = G.size(0) * G.size(1) * G.size(2);
+  rs::ctx_act_bwd_launch(is_bf16(hx), G.data_ptr<float>(), (int)G.size(3), hx.data_ptr(), (int)hx.size(3),
+                         inp.data_ptr(), (int)cd, P, (int)hd, (int)cd, dcn.data_ptr(), cur_stream());
+  RS_CHECK_LAUNCH();
+  return dcn;
+}
+
 std::vector<Tensor> gru_gate_zr(const Tensor& zr, const Tensor& h, const Tensor& x) {
   check_gpu(zr, "zr");
   check_gpu(h, "h");
@@ -673,6 +726,8 @@ TORCH_LIBRARY(raft_stir, m) {
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad, Tensor(a!)? dmask_out=None) -> Tensor[]");
   m.def("upflow8_backward(Tensor g, Tensor ah, Tensor aw) -> Tensor");
+  m.def("context_act(Tensor cn, Tensor(a!) hx, Tensor(b!) inp, int hd) -> ()");
+  m.def("context_act_backward(Tensor G, Tensor hx, Tensor inp, int hd) -> Tensor");
   m.def("gru_gate_zr(Tensor zr, Tensor h, Tensor x) -> Tensor[]");
   m.def("gru_gate_q(Tensor q, Tensor z, Tensor h) -> Tensor[]");
   m.def("gru_bwd_q(Tensor dhn, Tensor z, Tensor h, Tensor qt) -> Tensor[]");
@@ -695,6 +750,8 @@ TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {
   m.impl("convex_upsample", &convex_upsample);
   m.impl("convex_upsample_backward", &convex_upsample_backward);
   m.impl("upflow8_backward", &upflow8_backward);
+  m.impl("context_act", &context_act);
+  m.impl("context_act_backward", &context_act_backward);
   m.impl("gru_gate_zr", &gru_gate_zr);
   m.impl("gru_gate_q", &gru_gate_q);
   m.impl("gru_bwd_q", &gru_bwd_q);

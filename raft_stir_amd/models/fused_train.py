@@ -560,8 +560,14 @@ class FusedTrainLoop(torch.autograd.Function):
         f1w, f1b = eng.f1w, eng.f1b
         S = eng.buffers(B, H, W, iters, dev)
         sl = lambda t, i: t[i * B:(i + 1) * B]
-        S["hx"][:B, ..., :HD].copy_(net.permute(0, 2, 3, 1))
-        S["inp"].copy_(inp.permute(0, 2, 3, 1))
+        if inp is None:
+            # net: the context encoder's raw output -- split + tanh / relu
+            # (reference core/raft.py:108-110) straight into the slots, one pass
+            cn = net.permute(0, 2, 3, 1).to(S["inp"].dtype).contiguous()
+            R.context_act(cn, S["hx"][:B], S["inp"], HD)
+        else:
+            S["hx"][:B, ..., :HD].copy_(net.permute(0, 2, 3, 1))
+            S["inp"].copy_(inp.permute(0, 2, 3, 1))
         C = S["C"]
         sl(C, 0).copy_(coords1.detach())
         c0 = coords0.detach().float().contiguous()
@@ -616,7 +622,8 @@ class FusedTrainLoop(torch.autograd.Function):
             ctx.save_for_backward(*otf_t)
         ctx.defer = bool(defer) and eng.side_stream(dev) is not None
         ctx.c0 = c0
-        ctx.net_dtype, ctx.inp_dtype = net.dtype, inp.dtype
+        ctx.net_dtype = net.dtype
+        ctx.inp_dtype = inp.dtype if inp is not None else None  # None: net was the raw context output
         return up
 
     @staticmethod
@@ -700,8 +707,12 @@ class FusedTrainLoop(torch.autograd.Function):
             if otf is not None:
                 for g in d_otf:
                     g.record_stream(main)
-        d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
-        d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
+        if ctx.inp_dtype is None:  # adjoint of context_act: the raw context output's gradient, one pass
+            d_net = R.context_act_backward(G, S["hx"][:B], S["inp"], HD).permute(0, 3, 1, 2).to(ctx.net_dtype)
+            d_inp = None
+        else:
+            d_net = G[..., :HD].permute(0, 3, 1, 2).to(ctx.net_dtype)
+            d_inp = G[..., HD:HD + 128].permute(0, 3, 1, 2).to(ctx.inp_dtype)
 
         grads = FusedTrainLoop._param_grads(ctx, FusedTrainLoop._wgrads, S, C, B, H, W, n, main, side)
         if otf is None:

@@ -73,6 +73,33 @@ _FUSED_PREP = True  # one-kernel input normalisation into the fnet batch
 OVERLAP = {"cnet": True, "flow": True, "defer": True, "defer_enc": False}
 
 
+class _SplitPair(torch.autograd.Function):
+    """``torch.split(x, [n, len(x) - n])`` whose backward returns the two
+    gradients' common buffer when they are its adjacent halves with x's
+    strides (the correlation backward writes d fmap1 / d fmap2 that way,
+    csrc/ops.cpp corr_volume_backward) instead of concatenating them."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.n, ctx.shape = n, x.shape
+        return x[:n], x[n:]
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        if g1 is None or g2 is None:
+            z = g2 if g1 is None else g1
+            if z is None:
+                return None, None
+            g1 = torch.zeros_like(g2) if g1 is None else g1
+            g2 = torch.zeros(ctx.shape[0] - ctx.n, *ctx.shape[1:], device=g1.device, dtype=g1.dtype) if g2 is None else g2
+        if (g1.dtype == g2.dtype and g1.stride() == g2.stride() and g1.untyped_storage().data_ptr()
+                == g2.untyped_storage().data_ptr()
+                and g2.storage_offset() == g1.storage_offset() + g1.shape[0] * g1.stride(0)):
+            return g1.as_strided((g1.shape[0] + g2.shape[0],) + tuple(g1.shape[1:]), g1.stride(),
+                                 g1.storage_offset()), None
+        return torch.cat([g1, g2], 0), None
+
+
 class RAFT(nn.Module):
     def __init__(self, args=None, **overrides):
         super().__init__()
@@ -232,7 +259,7 @@ class RAFT(nn.Module):
                             xc = fc[k](xc)
                 cnet = xc
                 image1.record_stream(side)  # main-stream block read on side (kept by cnet's backward)
-                fmap1, fmap2 = torch.split(xf, [image1.shape[0], image2.shape[0]], dim=0)
+                fmap1, fmap2 = _SplitPair.apply(xf, image1.shape[0])
             else:
                 fmap1, fmap2 = self.fnet([image1, image2])
             # The reference casts the features to fp32 (core/raft.py:102-103).
@@ -252,15 +279,21 @@ class RAFT(nn.Module):
             else:
                 main.wait_stream(side)
                 cnet = _StreamHandoff.apply(cnet, side)
-            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
-            net = torch.tanh(net)
-            inp = torch.relu(inp)
+            fused_train = not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn)
+            if fused_train and not self.cfg.small:
+                # the fused engine splits the context features and applies tanh / relu
+                # itself, straight into its buffers (FusedTrainLoop, context_act)
+                net, inp = cnet, None
+            else:
+                net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+                net = torch.tanh(net)
+                inp = torch.relu(inp)
 
             coords0, coords1 = self.initialize_flow(image1)
             if flow_init is not None:
                 coords1 = coords1 + flow_init
 
-            if not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn):
+            if fused_train:
                 eng = self._train_engine()
                 cstate, ctoken, otf_t = FusedTrainEngine.corr_inputs(corr_fn)
                 otf = None if not otf_t else (corr_fn.radius, corr_fn.scale, len(otf_t) - 1)

@@ -22,6 +22,6 @@ for rep in $(seq ${REPS:-2}); do
     if [ $arm = base ]; then D=$BASE; else D=.; fi
     (cd $D && timeout -k 10 400 python bench.py --steps 30 --warmup 5 --infer-reps 50 ${BENCH_ARGS}) > $OUT/$arm.log 2>&1 \
       || { tail -30 $OUT/$arm.log; exit 1; }
-    echo "[$arm] $(tail -1 $OUT/$arm.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("inference", {}).get("fps"))')" | tee -a $OUT/ab.txt
+    echo "[$arm] $(tail -1 $OUT/$arm.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], (d.get("inference") or {}).get("fps"))')" | tee -a $OUT/ab.txt
   done
 done
