@@ -1036,11 +1036,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
   a.w_bytes = L.w_bytes;
   a.chs = L.chs;
   a.f32 = L.f32;
-  static const int xcd_env = [] {
-    const char* e = getenv("RS_CONV_XCD_REMAP");
-    return e ? atoi(e) : 1;
-  }();
-  a.xcd_remap = xcd_env;
+  a.xcd_remap = 1;
   if (L.geo) {
     a.Hi = L.Hi; a.Wi = L.Wi; a.SY = L.SY; a.SX = L.SX;
     a.oH = L.oH; a.oW = L.oW; a.OSY = L.OSY; a.OSX = L.OSX; a.OOY = L.OOY; a.OOX = L.OOX;
@@ -1096,7 +1092,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     conv_1x1_launch(a, L.tile, stream);
     return;
   }
-  if (L.tile >= 60) {  // weight-streaming tiles (conv_v3.hip), fragment-major weights
+  if (L.tile >= 56) {  // weight-streaming tiles (conv_v3.hip), fragment-major weights
     conv_v3_launch(a, L.tile, stream);
     return;
   }

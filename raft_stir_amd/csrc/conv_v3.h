@@ -297,6 +297,8 @@ __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
 inline bool v3_geom(int tile, int* nwm, int* mw, int* thw, int* nwp) {
   *nwp = 1;
   switch (tile) {
+    case 56: *nwm = 4; *mw = 1; *thw = 1; return true;  // one patch row: 4x the blocks of 61 (batch-1 grids)
+    case 57: *nwm = 4; *mw = 1; *thw = 2; return true;
     case 60: *nwm = 4; *mw = 1; *thw = 6; return true;
     case 61: *nwm = 4; *mw = 1; *thw = 3; return true;
     case 62: *nwm = 4; *mw = 2; *thw = 6; return true;
@@ -319,6 +321,8 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* thw, int* nwp) {
     const dim3 block(64 * nwm * nwp);                                                              \
     constexpr int R1 = KH_ * KW_ == 9 ? 12 : 10, R2 = KH_ * KW_ == 9 ? 9 : 5;                       \
     switch (tile) {                                                                                \
+      case 56: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 1, R1>), grid, block, 0, stream, a); break; \
+      case 57: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 2, R1>), grid, block, 0, stream, a); break; \
       case 60: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 6, R1>), grid, block, 0, stream, a); break; \
       case 61: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 3, R1>), grid, block, 0, stream, a); break; \
       case 62: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 2, 6, R2>), grid, block, 0, stream, a); break; \

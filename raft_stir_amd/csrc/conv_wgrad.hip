@@ -660,10 +660,7 @@ WgradPlan wgrad_plan(const WgradLaunch& L, bool det) {
   // and more blocks co-running with the main queue's kernels; in situ 1024
   // target blocks beat 2048 and 4096 (401.3 / 402.3 vs 397.8 / 399.3 vs
   // 390.6 / 392.0 pairs/s, profiles/r4/ab_knobs_s33.txt)
-  static const int target_blocks = [] {
-    const char* e = getenv("RS_WGRAD_BLOCKS");
-    return e ? atoi(e) : 1024;
-  }();
+  constexpr int target_blocks = 1024;
   int ksplit = cdiv(target_blocks, pl.ntiles * pl.mtiles);
   ksplit = max(1, min(ksplit, cdiv(P, wgrad::BK * 8)));
   if (det) ksplit = min(ksplit, 32);

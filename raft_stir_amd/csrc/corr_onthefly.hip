@@ -20,7 +20,7 @@
 // decomposition as corr_lookup's backward), then df1 accumulates in registers
 // (plain store once per pixel: every pixel owns its df1 row) and df2_l
 // receives g * f1 through float atomics (cells are shared between pixels).
-// Default kernels (per-query ones above as fallback / RS_OTF_TILE=0): 4 x 4
+// Default kernels (the per-query ones above serve fp32 features in the forward): 4 x 4
 // query TILES -- the forward gathers the bounding box of the tile's 16
 // windows once per level and computes the cell dots as a small GEMM on MFMA
 // (otf_tile_kernel); the backward gathers the tile's cell gradients over the
@@ -845,11 +845,7 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
   }
   const int N1 = H1 * W1;
   const int cq = C / 32;
-  static const bool tile_env = [] {  // RS_OTF_TILE=0: per-query kernel only (A/B)
-    const char* e = getenv("RS_OTF_TILE");
-    return !(e && e[0] == '0');
-  }();
-  if (fm_bf16 && tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+  if (fm_bf16 && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
     const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
     const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
 #define RS_L(OT)                                                                                        \
@@ -893,12 +889,7 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
     p.W[l] = d.W[l] = l < levels ? Ws[l] : 0;
   }
   const int cq = C / 32;
-  static const bool tile_env = [] {  // RS_OTF_TILE=0 or RS_OTF_TILE_BWD=0: per-query backward (A/B)
-    const char* e = getenv("RS_OTF_TILE");
-    const char* e2 = getenv("RS_OTF_TILE_BWD");
-    return !(e && e[0] == '0') && !(e2 && e2[0] == '0');
-  }();
-  if (tile_env && fm_bf16 && C % 64 == 0 && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+  if (fm_bf16 && C % 64 == 0 && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
     const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
     const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
     const bf16_t* f1b = static_cast<const bf16_t*>(f1);
@@ -917,7 +908,7 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
       default: { constexpr int CQ = 8; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
     }
 #undef RS_LM
-  } else if (tile_env && (2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
+  } else if ((2 * r + 2) * (2 * r + 2) <= otf::MAXC) {
     const int tiles_x = cdiv(W1, otf::TQ), tiles_y = cdiv(H1, otf::TQ);
     const int per_xcd = cdiv(B * tiles_x * tiles_y, 8);
 #define RS_LT(T, GT)                                                                                      \

@@ -309,11 +309,6 @@ bool enc_halo_launch(const bf16_t* x, int xstr, const bf16_t* w, int Ktot, bf16_
   // CU-filling blocks of one stream serialise behind the other's; graphed
   // 1088x436 inference (< 1024) 4 tiles 286-289 FPS, 2: 278-281, 12: 266-268
   a.tpb = a.ntiles * gy >= 1024 ? 12 : 4;
-  static const int tpb_env = [] {  // RS_HALO_TPB: fixed tiles per block (tuning A/B)
-    const char* e = getenv("RS_HALO_TPB");
-    return e ? atoi(e) : 0;
-  }();
-  if (tpb_env > 0) a.tpb = tpb_env;
   const int gx = cdiv(a.ntiles, a.tpb);
   if (cin == 64)
     hipLaunchKernelGGL((ench::enc_halo_kernel<64, 64>), dim3(gx, gy), dim3(256), 0, stream, a);

@@ -275,17 +275,11 @@ struct EncWgradLaunch {
 };
 
 int enc_wgrad_splits(int B, int H, int W, int Cin, int Cout, int* tpb) {
-  // RS_ENC_WGRAD_TPB: minimum tiles per block (fewer blocks, fewer partial
-  // tiles to write and reduce; A/B switch)
-  static const int tmin = [] {
-    const char* e = getenv("RS_ENC_WGRAD_TPB");
-    return e ? atoi(e) : 0;
-  }();
   const int ntiles = B * cdiv(H, encw::TH) * cdiv(W, encw::TW);
   const int chan = cdiv(Cout, 64) * cdiv(Cin, 64);
   int want = 256 / chan;  // ~one block per CU
   if (want < 1) want = 1;
-  *tpb = std::max(cdiv(ntiles, want), tmin);
+  *tpb = cdiv(ntiles, want);
   return cdiv(ntiles, *tpb);
 }
 

@@ -406,10 +406,7 @@ int pick_apply_splits(int B, int P, int C, int vn) {
 }
 
 int pick_splits(int B, int P, int C, int vn) {
-  static const int target = [] {  // RS_NORM_RED_BLOCKS: total reduction blocks (A/B knob)
-    const char* e = getenv("RS_NORM_RED_BLOCKS");
-    return e && atoi(e) > 0 ? atoi(e) : 512;
-  }();
+  constexpr int target = 512;  // total reduction blocks (larger grids measured slower in situ, round 4)
   const int rows = THREADS / (C / vn);
   int S = cdiv(target, B);
   S = max(1, min(S, cdiv(P, rows * 8)));

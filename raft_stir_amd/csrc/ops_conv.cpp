@@ -211,17 +211,17 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 60 && tile <= 68) || tile == 70,
-              "conv_fused: tile must be in [0,54], [60,68] or 70");
+  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 56 && tile <= 68) || tile == 70,
+              "conv_fused: tile must be in [0,54], [56,68] or 70");
   if (tile == 70) {  // conv_gemm1.hip: 1x1 GEMM over 64-channel K chunks
     TORCH_CHECK(KH == 1 && KW == 1 && !f32, "conv_fused: tile 70 is the bf16 1x1 GEMM");
     for (size_t s = 0; s < segs.size(); ++s)
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tile 70 needs segment channels % 64 == 0");
   }
-  const bool v3 = tile >= 60 && tile <= 68;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
+  const bool v3 = tile >= 56 && tile <= 68;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
   if ((tile >= 42 && tile <= 54) || v3)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
-                "conv_fused: tiles 42-54 and 60-68 are instantiated for 3x3, 1x5 and 5x1 kernels only");
+                "conv_fused: tiles 42-68 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
   TORCH_CHECK(!(tile >= 38 && tile <= 40) || f32, "conv_fused: tiles 38-40 are the fp32 split-K tiles");
   TORCH_CHECK(tile != 5 || Cout <= 16, "conv_fused: tile 5 (small-N) needs Cout <= 16");
@@ -250,7 +250,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
               "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
   if (v3) {  // fragment-major rows in 32-row blocks; blocks past the weight read as zeros
     TORCH_CHECK(w.size(0) % 32 == 0 && w.size(0) >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
-                "conv_fused: tiles 60-68 need fragment-major weights with round_up(Cout, 32) rows (< 2 GiB)");
+                "conv_fused: tiles 56-68 need fragment-major weights with round_up(Cout, 32) rows (< 2 GiB)");
   } else {
     TORCH_CHECK(w.size(0) >= (Cout + tileM - 1) / tileM * tileM,
                 "conv_fused: packed weight needs >= round_up(Cout, ", tileM, ") rows");
@@ -318,7 +318,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   TORCH_CHECK(epi >= 0 && epi <= EPI_NORM, "conv_fused: unknown epilogue kind");
   if (nx.chs)
     TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3 && tile != 70,
-                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-54, 60-70)");
+                "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-70)");
   L.chs = nx.chs;
   rs::conv_launch(L, stream());
   RS_CHECK_LAUNCH();

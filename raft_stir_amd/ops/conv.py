@@ -63,13 +63,13 @@ def pack_weight_split(weight: torch.Tensor, segs: Sequence[SegSpec], cout_pad: i
     return split_weight(pack_weight(weight, segs, cout_pad, torch.float32))
 
 
-V3_TILES = (60, 61, 62, 63, 64, 65, 66, 67, 68)
+V3_TILES = (56, 57, 60, 61, 62, 63, 64, 65, 66, 67, 68)
 
 
 @torch.no_grad()
 def frag_weight(w: torch.Tensor) -> torch.Tensor:
     """A packed weight [Cout_pad][taps][Ktot] in the fragment-major layout of
-    the weight-streaming tiles 60-68 (csrc/conv_v3.h): per 32-row block, per
+    the weight-streaming tiles 56-68 (csrc/conv_v3.h): per 32-row block, per
     64-channel K chunk, per tap, per 16-channel slice, the 1 KB A fragment of a
     32x32x16 MFMA (lane h*32 + r holds row r, channels 16 ks + 8 h .. + 8), so
     each wave's weight stream is one contiguous run of 1 KB loads.  Same shape
@@ -197,7 +197,7 @@ def tuned_tiles_f32() -> dict:
 
 
 def frag_eligible(w: torch.Tensor, kh: int, kw: int) -> bool:
-    """Can the weight-streaming tiles 60-68 serve this packed weight?"""
+    """Can the weight-streaming tiles 56-68 serve this packed weight?"""
     return kh * kw in (5, 9) and w.dim() == 3 and w.shape[0] % 32 == 0 and w.shape[2] % 64 == 0
 
 
@@ -207,7 +207,7 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
     """segs: list of (NHWC bf16 buffer, channel offset, channels read).
     ``nscale`` with ``epi=EPI_NORM``: out = [relu if hd](acc * nscale + bias)
     [then relu(. + aux1)].  ``wf``: the same weight in the fragment-major
-    layout (:func:`frag_weight`), which the weight-streaming tiles 60-68 read;
+    layout (:func:`frag_weight`), which the weight-streaming tiles 56-68 read;
     without it those tiles are not chosen."""
     if wf is None:  # the training engine tags its packed weights with their fragment-major copy
         wf = getattr(w, "_rs_frag", None)
@@ -231,7 +231,7 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
                 tile = choose_tile(P, cout, chans, kh * kw)
     if tile in V3_TILES:
         if wf is None:
-            raise ValueError("conv_fused: tiles 60-68 read the fragment-major weight: pass wf=frag_weight(w)")
+            raise ValueError("conv_fused: tiles 56-68 read the fragment-major weight: pass wf=frag_weight(w)")
         w = wf
     if nscale is None:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
