@@ -52,6 +52,11 @@ _F32_ENGINE = True
 from ..ops.upsample import convex_upsample
 
 
+# RAFT-small head conv K in bf16 (96 channels padded to 128 with zero weights:
+# K % 64, so the weight-streaming tiles can serve it; profiles/r5/README.md)
+_SMALL_HEAD_K = 128
+
+
 class _Conv:
     """One packed convolution: weight [Cout_pad][taps][Ktot] bf16 + fp32 bias."""
 
@@ -122,7 +127,10 @@ class FusedUpdate:
                 _C([gru.convz, gru.convr], [(256, [(0, hd, 0), (hd, cd + 82, hd)])]),
                 _C(gru.convq, [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]),
             )]
-            self.head = _C(ub.flow_head.conv1, [(96, [(0, hd, 0)])])
+            # bf16: K padded to 128 (hx[96:128] meets zero weights) so the
+            # weight-streaming tiles (K % 64) can serve it on batch-1 grids
+            self.head_k = 96 if f32 else _SMALL_HEAD_K
+            self.head = _C(ub.flow_head.conv1, [(self.head_k, [(0, hd, 0)])])
             self.head_c = 128
             self.flow = _C(ub.flow_head.conv2, [(128, [(0, 128, 0)])])
             self.mask0 = self.mask2 = None
@@ -270,7 +278,8 @@ class FusedUpdate:
                 cf([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
                            EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0, wf=q.wf)
             if small:
-                cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0, wf=self.head.wf)
+                cf([(hx, 0, self.head_k)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0,
+                   wf=self.head.wf)
                 torch.ops.raft_stir.flow_head(bufs["head"], 0, 128, self.flow_w32, self.flow_b32, coords1, None)
             else:
                 cf([(hx, 0, hd)], self.head.w, self.head.b, 3, 3, 512 if want_up else 256, EPI_RELU,
