@@ -55,6 +55,8 @@ from ..ops.upsample import convex_upsample
 # RAFT-small head conv K in bf16 (96 channels padded to 128 with zero weights:
 # K % 64, so the weight-streaming tiles can serve it; profiles/r5/README.md)
 _SMALL_HEAD_K = 128
+# ... and its GRU-q conv's input segments padded to 64-multiples (bf16)
+_SMALL_Q_PAD = True
 
 
 class _Conv:
@@ -123,9 +125,18 @@ class FusedUpdate:
             self.conv = _C(enc.conv, [(128, [(0, 128, 0)])])
             self.f1_c = 64
             gru = ub.gru
+            if f32 or not _SMALL_Q_PAD:
+                q_segs = [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]
+                self.rh_c, self.q_xoff = pad_to(hd, 32), hd
+            else:
+                # bf16: segments of 64-multiples for the 64-deep-K tiles -- r*h in a
+                # 128-channel buffer (channels 96.. stay zero) and x read as
+                # hx[64:256] (h[64:96] and the pad meet zero weights)
+                q_segs = [(128, [(0, hd, 0)]), (192, [(hd, cd + 82, hd - 64)])]
+                self.rh_c, self.q_xoff = 128, 64
             self.gru = [(
                 _C([gru.convz, gru.convr], [(256, [(0, hd, 0), (hd, cd + 82, hd)])]),
-                _C(gru.convq, [(pad_to(hd, 32), [(0, hd, 0)]), (160, [(hd, cd + 82, 0)])]),
+                _C(gru.convq, q_segs),
             )]
             # bf16: K padded to 128 (hx[96:128] meets zero weights) so the
             # weight-streaming tiles (K % 64) can serve it on batch-1 grids
@@ -158,6 +169,8 @@ class FusedUpdate:
             self.flow = _C(ub.flow_head.conv2, [(256, [(0, 256, 0)])])
             self.mask2 = _C(ub.mask[2], [(256, [(0, 256, 0)])])
         self.hd, self.cd = hd, cd
+        if not small:
+            self.rh_c, self.q_xoff = pad_to(hd, 32), hd
         f1 = ub.encoder.convf1
         self.f1_w = f1.weight.detach().float().permute(2, 3, 1, 0).contiguous()  # [7][7][2][Cout]
         self.f1_b = f1.bias.detach().float().contiguous()
@@ -190,7 +203,7 @@ class FusedUpdate:
             e = lambda c: torch.empty(B, H, W, c, device=dev, dtype=dt)  # noqa: E731
             z = lambda c: torch.zeros(B, H, W, c, device=dev, dtype=dt)  # noqa: E731
             bufs = dict(corr=z(self.corr_pad), f1=e(self.f1_c), mot=e(self.mot_c), hx=z(self.hx_c),
-                        z=e(self.hd), rh=z(pad_to(self.hd, 32)), head=e(self.head_c))
+                        z=e(self.hd), rh=z(self.rh_c), head=e(self.head_c))
             if not self.model.cfg.small:
                 bufs["c1"] = e(256)
                 bufs["mask"] = e(576)
@@ -275,7 +288,7 @@ class FusedUpdate:
                 rhc = bufs["rh"].shape[-1]
                 cf([(hx, 0, self.hx_c)], zr.w, zr.b, zr.kh, zr.kw, 2 * hd, EPI_GRU_ZR,
                            bufs["z"], 0, hd=hd, out2=bufs["rh"], o2off=0, aux1=hx, a1off=0, wf=zr.wf)
-                cf([(bufs["rh"], 0, rhc), (hx, hd, self.hx_c - hd)], q.w, q.b, q.kh, q.kw, hd,
+                cf([(bufs["rh"], 0, rhc), (hx, self.q_xoff, self.hx_c - self.q_xoff)], q.w, q.b, q.kh, q.kw, hd,
                            EPI_GRU_Q, hx, 0, aux1=hx, a1off=0, aux2=bufs["z"], a2off=0, wf=q.wf)
             if small:
                 cf([(hx, 0, self.head_k)], self.head.w, self.head.b, 3, 3, 128, EPI_RELU, bufs["head"], 0,

@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--small", action="store_true", help="tune RAFT-small's calls")
     ap.add_argument("--merge", action="store_true", help="update the existing table instead of replacing it")
+    ap.add_argument("--show", default="", help="print every candidate's time (and error) for keys containing this")
     ap.add_argument("--infer-only", action="store_true", help="record only the inference forward's calls")
     ap.add_argument("--f32", action="store_true",
                     help="fp32 inference calls on the split-bf16 F32 tiles -> the 'tiles_f32' table")
@@ -141,10 +142,14 @@ def main():
         for t in sorted(set(cands + [heur])):
             try:
                 res[t] = gtime(lambda: C.conv_fused(**kw, tile=t), args.reps)
-            except RuntimeError as e:
+            except (RuntimeError, ValueError) as e:
                 if t == heur:
                     print("  heuristic tile failed:", str(e).splitlines()[0], flush=True)
+                if args.show and args.show in key:
+                    print(f"  {key} t{t}: {str(e).splitlines()[0][:120]}", flush=True)
                 continue
+        if args.show and args.show in key:
+            print("  " + key + " " + " ".join(f"t{t}={v:.1f}" for t, v in sorted(res.items())), flush=True)
         if not res:
             print(f"{tag:5s} {key:42s} no applicable tile, skipped", flush=True)
             continue
