@@ -1013,7 +1013,8 @@ struct ConvLaunch {
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
 
-void conv_launch(const ConvLaunch& L, hipStream_t stream) {
+// false: the tile is not instantiated for this kernel size (the host raises)
+bool conv_launch(const ConvLaunch& L, hipStream_t stream) {
   conv::Args a{};
   for (int s = 0; s < 3; ++s) {
     a.seg[s].ptr = static_cast<const bf16_t*>(L.seg_ptr[s]);
@@ -1056,7 +1057,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
       default: RS_GEO(128, 64, 2, 2, 32); break;  // 4
     }
 #undef RS_GEO
-    return;
+    return true;
   }
   if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8, split-K 38-40 (host-checked)
 #define RS_F32(BM_, BN_, KG_)                                                                       \
@@ -1069,12 +1070,12 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     else if (L.tile == 40) RS_F32(64, 64, 2);
     else RS_F32(128, 64, 1);
 #undef RS_F32
-    return;
+    return true;
   }
   if (L.tile == 41) {  // tile 3 (64x64, 32-deep K, register-staged) with 4-way intra-block split-K
     dim3 grid(cdiv(a.P, 64), cdiv(L.Cout, 64));
     hipLaunchKernelGGL((conv::conv_lds_kernel<64, 64, 2, 2, 32, false, false, 4>), grid, dim3(1024), 0, stream, a);
-    return;
+    return true;
   }
   if (L.tile >= 24 && L.tile <= 26) {  // halo (patch) tiles: grid = Cout tiles x (images x patch rows x patch columns)
     const int TH = L.tile == 26 ? 4 : 8, BM = L.tile == 25 ? 64 : 128;
@@ -1082,19 +1083,16 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     if (L.tile == 24) hipLaunchKernelGGL((conv::conv_halo_kernel<128, 8, 192>), grid, dim3(256), 0, stream, a);
     else if (L.tile == 25) hipLaunchKernelGGL((conv::conv_halo_kernel<64, 8, 192>), grid, dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((conv::conv_halo_kernel<128, 4, 128>), grid, dim3(256), 0, stream, a);
-    return;
+    return true;
   }
   if (L.tile >= 42 && L.tile <= 54) {  // lean unrolled-tap tiles (conv_v2.hip)
-    conv_v2_launch(a, L.tile, stream);
-    return;
+    return conv_v2_launch(a, L.tile, stream);
   }
   if (L.tile == 70) {  // 1x1 convs as plain GEMMs (conv_gemm1.hip)
-    conv_1x1_launch(a, L.tile, stream);
-    return;
+    return conv_1x1_launch(a, L.tile, stream);
   }
   if (L.tile >= 56) {  // weight-streaming tiles (conv_v3.hip), fragment-major weights
-    conv_v3_launch(a, L.tile, stream);
-    return;
+    return conv_v3_launch(a, L.tile, stream);
   }
   if (L.tile == 5) {
     hipLaunchKernelGGL(conv::conv_smalln_kernel, dim3(cdiv(a.P, 16)), dim3(256), 0, stream, a);
@@ -1176,6 +1174,7 @@ void conv_launch(const ConvLaunch& L, hipStream_t stream) {
     hipLaunchKernelGGL((conv::conv_kernel<WM, WN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N),
                        0, stream, a);
   }
+  return true;
 }
 
 static int egrid(long total) {

@@ -95,9 +95,7 @@ struct V3 {
   }
 };
 
-// EXP: timing-experiment bits (profiles/r5/conv_v3_experiments_s3.log): 1 no A wait, 2 no halo
-// refill, 4 no chunk barrier, 8 every A load from slice 0, 16 MFMAs only, 32 no main loop
-template <int KH, int KW, int NWM, int MW, int THW, int RA, int NWP = 1, int EXP = 0>
+template <int KH, int KW, int NWM, int MW, int THW, int RA, int NWP = 1>
 __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
   using C = V3<KH, KW, NWM, MW, THW, RA, NWP>;
   constexpr int TH = C::TH, NW = C::NW;
@@ -229,15 +227,14 @@ __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
 #define V3_SLICE(J)                                                                            \
   if constexpr ((J) < NSL) {                                                                   \
     constexpr int sa_ = ((J) + D) % RA, sc_ = (J) % RA, fb_ = (J) & 1;                         \
-    if constexpr (EXP & 16) {                                                                  \
-    } else if constexpr (EXP & 8) { V3_LDA(0, sa_); } else { V3_LDA((J) + D, sa_); }           \
-    if constexpr (C::hcnt(J) > 0 && !(EXP & 18)) V3_ISSUE_H(cc + 1, hnxt, (J) * PPP, C::hcnt(J)); \
-    if constexpr ((J) + 1 < NSL && !(EXP & 16)) V3_RDB(fb_ ^ 1, dcur, (J) + 1);                \
-    if constexpr (!(EXP & 17)) wait_vmcnt<(EXP & 2) ? D * MW : ((J) + 1 == NSL ? C::bwait() : C::nwait(J))>(); \
+    V3_LDA((J) + D, sa_);                                                                      \
+    if constexpr (C::hcnt(J) > 0) V3_ISSUE_H(cc + 1, hnxt, (J) * PPP, C::hcnt(J));             \
+    if constexpr ((J) + 1 < NSL) V3_RDB(fb_ ^ 1, dcur, (J) + 1);                               \
+    wait_vmcnt<(J) + 1 == NSL ? C::bwait() : C::nwait(J)>();                                   \
     V3_FENCE_A(sc_);                                                                           \
     if constexpr ((J) + 1 == NSL) {                                                            \
       if (cc + 1 < nchunks) {                                                                  \
-        if constexpr (!(EXP & 4)) asm volatile("s_barrier" ::: "memory");                      \
+        asm volatile("s_barrier" ::: "memory");                                                \
         V3_RDB(0, dnxt, 0);                                                                    \
       }                                                                                        \
     }                                                                                          \
@@ -253,7 +250,7 @@ __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
   }
 #define V3_TAP(TT) V3_SLICE(4 * (TT)) V3_SLICE(4 * (TT) + 1) V3_SLICE(4 * (TT) + 2) V3_SLICE(4 * (TT) + 3)
 
-  for (int cc = 0; cc < ((EXP & 32) ? 0 : nchunks); ++cc) {
+  for (int cc = 0; cc < nchunks; ++cc) {
     const int hb = cc & 1;
     const uint32_t dcur = hb ? (uint32_t)(HSL * 16) : 0u, dnxt = hb ? 0u : (uint32_t)(HSL * 16);
     const int hnxt = hb ? 0 : HSL;  // slot base of the other halo buffer
@@ -296,19 +293,15 @@ __global__ __launch_bounds__(64 * NWM * NWP) void conv_v3_kernel(Args a) {
 // tile -> (waves along Cout, 32-row fragments per wave, patch rows per wave, waves along the patch rows)
 inline bool v3_geom(int tile, int* nwm, int* mw, int* thw, int* nwp) {
   *nwp = 1;
+  *mw = 1;
   switch (tile) {
-    case 56: *nwm = 4; *mw = 1; *thw = 1; return true;  // one patch row: 4x the blocks of 61 (batch-1 grids)
-    case 57: *nwm = 4; *mw = 1; *thw = 2; return true;
-    case 60: *nwm = 4; *mw = 1; *thw = 6; return true;
-    case 61: *nwm = 4; *mw = 1; *thw = 3; return true;
-    case 62: *nwm = 4; *mw = 2; *thw = 6; return true;
-    case 63: *nwm = 2; *mw = 1; *thw = 6; return true;
-    case 64: *nwm = 3; *mw = 1; *thw = 6; return true;
-    case 65: *nwm = 2; *mw = 1; *thw = 3; return true;
-    case 66: *nwm = 4; *mw = 1; *thw = 3; *nwp = 2; return true;
-    case 67: *nwm = 4; *mw = 1; *thw = 4; *nwp = 2; return true;
-    case 68: *nwm = 2; *mw = 1; *thw = 3; *nwp = 4; return true;
-    default: return false;
+    case 56: *nwm = 4; *thw = 1; return true;  // one patch row: 4x the blocks of 61 (batch-1 grids)
+    case 57: *nwm = 4; *thw = 2; return true;
+    case 61: *nwm = 4; *thw = 3; return true;
+    case 65: *nwm = 2; *thw = 3; return true;
+    case 66: *nwm = 4; *thw = 3; *nwp = 2; return true;
+    case 68: *nwm = 2; *thw = 3; *nwp = 4; return true;
+    default: return false;  // (60, 62-64, 67: measured, never selected, dropped in round 6)
   }
 }
 
@@ -319,19 +312,14 @@ inline bool v3_geom(int tile, int* nwm, int* mw, int* thw, int* nwp) {
     if (!v3_geom(tile, &nwm, &mw, &thw, &nwp)) return false;                                       \
     const dim3 grid(cdiv(a.Cout, 32 * nwm * mw) * a.B * cdiv(a.H, thw * nwp) * cdiv(a.W, 32));     \
     const dim3 block(64 * nwm * nwp);                                                              \
-    constexpr int R1 = KH_ * KW_ == 9 ? 12 : 10, R2 = KH_ * KW_ == 9 ? 9 : 5;                       \
+    constexpr int R1 = KH_ * KW_ == 9 ? 12 : 10;                                                   \
     switch (tile) {                                                                                \
       case 56: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 1, R1>), grid, block, 0, stream, a); break; \
       case 57: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 2, R1>), grid, block, 0, stream, a); break; \
-      case 60: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 6, R1>), grid, block, 0, stream, a); break; \
       case 61: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 3, R1>), grid, block, 0, stream, a); break; \
-      case 62: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 2, 6, R2>), grid, block, 0, stream, a); break; \
-      case 63: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 6, R1>), grid, block, 0, stream, a); break; \
       case 65: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1>), grid, block, 0, stream, a); break; \
       case 66: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 3, R1, 2>), grid, block, 0, stream, a); break; \
-      case 67: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 4, 1, 4, R1, 2>), grid, block, 0, stream, a); break; \
-      case 68: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1, 4>), grid, block, 0, stream, a); break; \
-      default: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 3, 1, 6, R1>), grid, block, 0, stream, a); break; \
+      default: hipLaunchKernelGGL((conv::conv_v3_kernel<KH_, KW_, 2, 1, 3, R1, 4>), grid, block, 0, stream, a); break; \
     }                                                                                              \
     return true;                                                                                   \
   }

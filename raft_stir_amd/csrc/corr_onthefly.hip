@@ -27,10 +27,13 @@
 // same box into LDS, accumulates df1 in registers and sums each box cell's
 // df2 over the 16 queries before ONE atomic per (cell, channel)
 // (otf_tile_bwd_kernel).
-// Deterministic mode (DET): the df2 contributions are rounded to 32.32
-// fixed point and summed with 64-bit integer atomics -- integer addition is
-// associative, so the sums do not depend on the order the waves arrive in
-// (|df2| < 2^31, resolution 2^-32) -- then converted to fp32 by one pass.
+// Deterministic mode (DET): the df2 contributions are rounded to fixed point
+// and summed with 64-bit integer atomics -- integer addition is associative,
+// so the sums do not depend on the order the waves arrive in -- then
+// converted to fp32 by one pass.  The scale is picked per call from max|dout|
+// and max|f1| (fx_scan_kernel / fx_scale: every sum fits int64 with
+// resolution relative to the data), and a non-finite input turns the whole
+// df2 into NaN (integer sums would saturate it into a finite value).
 
 #include <algorithm>
 #include <type_traits>
@@ -302,8 +305,22 @@ __global__ __launch_bounds__(256) void otf_tile_kernel(const bf16_t* __restrict_
   }
 }
 
-__device__ __forceinline__ void fx_add(unsigned long long* p, float v) {
-  atomicAdd(p, (unsigned long long)__double2ll_rn((double)v * 4294967296.0));
+// Deterministic mode's fixed-point scale, picked per call on the device
+// (fx_scan_kernel): fxs = {bits of max|dout|, bits of max|f1|, non-finite
+// flag}.  Every df2 cell sum is bounded by 4 * nq * max|dout| * max|f1| *
+// |scale| (a query adds at most 4 bilinear weights <= 1 to one cell), so
+// S = 2^(61 - ceil(log2 bound)) keeps every sum inside int64 with a
+// resolution relative to the data (training-scale upstream gradients of
+// ~1e-7 keep ~50 significant bits instead of 32.32's ~9).
+__device__ __forceinline__ double fx_scale(const unsigned* fxs, long nq, float scale) {
+  const double m = (double)__uint_as_float(fxs[0]) * (double)__uint_as_float(fxs[1]) * fabs((double)scale) *
+                   4.0 * (double)nq;
+  if (!(m > 0.0) || fxs[2]) return 4294967296.0;  // all-zero or non-finite input: any scale
+  return ldexp(1.0, 61 - (int)ceil(log2(m)));
+}
+
+__device__ __forceinline__ void fx_add(unsigned long long* p, float v, double S) {
+  atomicAdd(p, (unsigned long long)__double2ll_rn((double)v * S));
 }
 
 template <typename T, typename GT, int CQ, bool DET>
@@ -312,7 +329,9 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
                                                              const float* __restrict__ coords,
                                                              int B, int N1, int r, float scale,
                                                              const GT* __restrict__ dout,
-                                                             float* __restrict__ df1, LvlMut df2) {
+                                                             float* __restrict__ df1, LvlMut df2,
+    const unsigned* __restrict__ fxs) {
+  const double fxS = DET ? fx_scale(fxs, (long)B * N1, scale) : 0.0;
   __shared__ float gs[WAVES][MAXE2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long pix = (long)blockIdx.x * WAVES + wave;
@@ -376,10 +395,10 @@ __global__ __launch_bounds__(WAVES * 64) void otf_bwd_kernel(const T* __restrict
             if constexpr (DET) {  // df2.p[l]: int64 32.32 fixed-point accumulators
               unsigned long long* d = reinterpret_cast<unsigned long long*>(df2.p[l]) +
                                       (size_t)b * H * W * C + off + q * 32;
-              fx_add(d + 0, gc * a[q].x);
-              fx_add(d + 1, gc * a[q].y);
-              fx_add(d + 2, gc * a[q].z);
-              fx_add(d + 3, gc * a[q].w);
+              fx_add(d + 0, gc * a[q].x, fxS);
+              fx_add(d + 1, gc * a[q].y, fxS);
+              fx_add(d + 2, gc * a[q].z, fxS);
+              fx_add(d + 3, gc * a[q].w, fxS);
             } else {
               float* d = d2b + off + q * 32;
               atomicAdd(d + 0, gc * a[q].x);
@@ -432,7 +451,9 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
                                                            const float* __restrict__ coords, int B, int H1,
                                                            int W1, int tiles_x, int tiles_y, int per_xcd, int r,
                                                            float scale, const GT* __restrict__ dout,
-                                                           float* __restrict__ df1, LvlMut df2) {
+                                                           float* __restrict__ df1, LvlMut df2,
+    const unsigned* __restrict__ fxs) {
+  const double fxS = DET ? fx_scale(fxs, (long)B * H1 * W1, scale) : 0.0;
   constexpr int C = CQ * 32;
   __shared__ float Gs[16][MAXC];
   __shared__ __attribute__((aligned(16))) float f2s[MAXC][36];  // 16-B rows: one ds_read_b128 per 4 channels
@@ -564,10 +585,10 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_kernel(const T* __restrict__
             const size_t off = ((size_t)b * H * W + (size_t)Y * W + X) * C + 32 * k + 4 * cg;
             if constexpr (DET) {
               unsigned long long* d = reinterpret_cast<unsigned long long*>(df2.p[l]) + off;
-              fx_add(d + 0, s0);
-              fx_add(d + 1, s1);
-              fx_add(d + 2, s2);
-              fx_add(d + 3, s3);
+              fx_add(d + 0, s0, fxS);
+              fx_add(d + 1, s1, fxS);
+              fx_add(d + 2, s2, fxS);
+              fx_add(d + 3, s3, fxS);
             } else {
               float* d = df2.p[l] + off;
               atomicAdd(d + 0, s0);
@@ -626,7 +647,9 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
                                                                const float* __restrict__ coords, int B, int H1,
                                                                int W1, int tiles_x, int tiles_y, int per_xcd, int r,
                                                                float scale, const GT* __restrict__ dout,
-                                                               float* __restrict__ df1, LvlMut df2) {
+                                                               float* __restrict__ df1, LvlMut df2,
+    const unsigned* __restrict__ fxs) {
+  const double fxS = DET ? fx_scale(fxs, (long)B * H1 * W1, scale) : 0.0;
   constexpr int C = CQ * 32, NCH = C / F2C;
   constexpr int F1P = C + 16;  // f1 row pitch (bf16): rows 8 banks apart for the tr16 reads
   static_assert(C % 64 == 0, "C % 64");
@@ -757,7 +780,7 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
             if (!ok[j]) continue;
             const size_t off = ((size_t)b * H * W + cl[j]) * C + 16 * n + r16;
             if constexpr (DET)
-              fx_add(reinterpret_cast<unsigned long long*>(df2.p[l]) + off, d[j]);
+              fx_add(reinterpret_cast<unsigned long long*>(df2.p[l]) + off, d[j], fxS);
             else
               atomicAdd(df2.p[l] + off, d[j]);
           }
@@ -812,11 +835,53 @@ __global__ __launch_bounds__(256) void otf_tile_bwd_mma_kernel(const bf16_t* __r
   }
 }
 
-// 32.32 fixed point (int64) -> fp32
+// max |dout|, max |f1| (as order-independent uint atomicMax of the
+// non-negative float bits) and a non-finite flag: the inputs of fx_scale
+template <typename T>
+__device__ __forceinline__ float absf_(T v);
+template <>
+__device__ __forceinline__ float absf_<float>(float v) { return fabsf(v); }
+template <>
+__device__ __forceinline__ float absf_<bf16_t>(bf16_t v) { return fabsf(bf2f(v)); }
+
+template <typename TD, typename TF>
+__global__ __launch_bounds__(256) void fx_scan_kernel(const TD* __restrict__ dout, long nd, const TF* __restrict__ f1,
+                                                      long nf, unsigned* __restrict__ fxs) {
+  float md = 0.f, mf = 0.f;
+  unsigned bad = 0;
+  const long st = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += st) {
+    const float v = absf_<TD>(dout[i]);
+    bad |= !(v <= 3.0e38f);  // NaN or Inf
+    md = fmaxf(md, v);
+  }
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += st) {
+    const float v = absf_<TF>(f1[i]);
+    bad |= !(v <= 3.0e38f);
+    mf = fmaxf(mf, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    md = fmaxf(md, __shfl_xor(md, o));
+    mf = fmaxf(mf, __shfl_xor(mf, o));
+    bad |= __shfl_xor(bad, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(fxs + 0, __float_as_uint(md));
+    atomicMax(fxs + 1, __float_as_uint(mf));
+    if (bad) atomicOr(fxs + 2, 1u);
+  }
+}
+
+// fixed point (int64, scale fx_scale) -> fp32; NaN everywhere when an input was
+// not finite (the integer sums cannot carry it), so the step's non-finite check sees it
 __global__ __launch_bounds__(256) void fx_to_f32_kernel(const long long* __restrict__ in, long n,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, const unsigned* __restrict__ fxs,
+                                                        long nq, float scale) {
+  const double inv = 1.0 / fx_scale(fxs, nq, scale);
+  const bool bad = fxs[2] != 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    out[i] = (float)((double)in[i] * (1.0 / 4294967296.0));
+    out[i] = bad ? __builtin_nanf("") : (float)((double)in[i] * inv);
 }
 
 }  // namespace otf
@@ -878,8 +943,21 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
-                         float* const* df2, bool det, float* const* df2f, hipStream_t stream) {
+                         float* const* df2, bool det, float* const* df2f, unsigned* fxs, hipStream_t stream) {
   const int N1 = H1 * W1;
+  if (det) {  // fxs (zeroed by the caller): the fixed-point scale's inputs
+    const long nd = (long)B * N1 * levels * (2 * r + 1) * (2 * r + 1), nf = (long)B * N1 * C;
+    const int g = (int)std::min<long>((nd + 255) / 256, 1024);
+#define RS_FS(TD, TF) \
+  hipLaunchKernelGGL((otf::fx_scan_kernel<TD, TF>), dim3(g), dim3(256), 0, stream, static_cast<const TD*>(dout), nd, \
+                     static_cast<const TF*>(f1), nf, fxs)
+    if (dout_bf16) {
+      if (fm_bf16) RS_FS(bf16_t, bf16_t); else RS_FS(bf16_t, float);
+    } else {
+      if (fm_bf16) RS_FS(float, bf16_t); else RS_FS(float, float);
+    }
+#undef RS_FS
+  }
   otf::Lvl p;
   otf::LvlMut d;
   for (int l = 0; l < 4; ++l) {
@@ -897,11 +975,11 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
   if (det)                                                                                                 \
     hipLaunchKernelGGL((otf::otf_tile_bwd_mma_kernel<GT, CQ, true>), dim3(8 * per_xcd), dim3(256), 0, stream, \
                        f1b, p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, scale,                \
-                       static_cast<const GT*>(dout), df1, d);                                               \
+                       static_cast<const GT*>(dout), df1, d, fxs);                                               \
   else                                                                                                     \
     hipLaunchKernelGGL((otf::otf_tile_bwd_mma_kernel<GT, CQ, false>), dim3(8 * per_xcd), dim3(256), 0, stream, \
                        f1b, p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, scale,                \
-                       static_cast<const GT*>(dout), df1, d)
+                       static_cast<const GT*>(dout), df1, d, fxs)
     switch (cq) {
       case 2: { constexpr int CQ = 2; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
       case 4: { constexpr int CQ = 4; if (dout_bf16) { RS_LM(bf16_t); } else { RS_LM(float); } } break;
@@ -915,11 +993,11 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
   if (det)                                                                                                \
     hipLaunchKernelGGL((otf::otf_tile_bwd_kernel<T, GT, CQ, true>), dim3(8 * per_xcd), dim3(256), 0, stream, \
                        static_cast<const T*>(f1), p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, \
-                       scale, static_cast<const GT*>(dout), df1, d);                                       \
+                       scale, static_cast<const GT*>(dout), df1, d, fxs);                                       \
   else                                                                                                    \
     hipLaunchKernelGGL((otf::otf_tile_bwd_kernel<T, GT, CQ, false>), dim3(8 * per_xcd), dim3(256), 0, stream, \
                        static_cast<const T*>(f1), p, levels, coords, B, H1, W1, tiles_x, tiles_y, per_xcd, r, \
-                       scale, static_cast<const GT*>(dout), df1, d)
+                       scale, static_cast<const GT*>(dout), df1, d, fxs)
     if (fm_bf16) {
       if (dout_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_LT(bf16_t, bf16_t)); }
       else { RS_OTF_DISPATCH_CQ(cq, RS_LT(bf16_t, float)); }
@@ -935,11 +1013,11 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
   if (det)                                                                                   \
     hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ, true>), grid, block, 0, stream,       \
                        static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,        \
-                       static_cast<const GT*>(dout), df1, d);                                \
+                       static_cast<const GT*>(dout), df1, d, fxs);                                \
   else                                                                                       \
     hipLaunchKernelGGL((otf::otf_bwd_kernel<T, GT, CQ, false>), grid, block, 0, stream,      \
                        static_cast<const T*>(f1), p, levels, coords, B, N1, r, scale,        \
-                       static_cast<const GT*>(dout), df1, d)
+                       static_cast<const GT*>(dout), df1, d, fxs)
   if (fm_bf16) {
     if (dout_bf16) { RS_OTF_DISPATCH_CQ(cq, RS_L(bf16_t, bf16_t)); }
     else { RS_OTF_DISPATCH_CQ(cq, RS_L(bf16_t, float)); }
@@ -954,7 +1032,7 @@ void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, c
       const long n = (long)B * Hs[l] * Ws[l] * C;
       const int g = (int)std::min<long>((n + 255) / 256, 16384);
       hipLaunchKernelGGL(otf::fx_to_f32_kernel, dim3(g), dim3(256), 0, stream,
-                         reinterpret_cast<const long long*>(df2[l]), n, df2f[l]);
+                         reinterpret_cast<const long long*>(df2[l]), n, df2f[l], fxs, (long)B * N1, scale);
     }
 }
 

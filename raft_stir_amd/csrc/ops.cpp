@@ -55,7 +55,7 @@ void corr_otf_fwd_launch(const void* f1, const void* const* f2, const int* Hs, c
 void corr_otf_bwd_launch(const void* f1, const void* const* f2, const int* Hs, const int* Ws,
                          int levels, bool fm_bf16, const float* coords, int B, int H1, int W1, int C,
                          int r, float scale, const void* dout, bool dout_bf16, float* df1,
-                         float* const* df2, bool det, float* const* df2f, hipStream_t stream);
+                         float* const* df2, bool det, float* const* df2f, unsigned* fxs, hipStream_t stream);
 void convex_up_fwd_launch(const float* flow, const void* mask, bool mask_bf16, int N, int H, int W,
                           float* out, hipStream_t stream);
 void convex_up_bwd_launch(const float* flow, const void* mask, bool mask_bf16, const void* dup,
@@ -429,9 +429,12 @@ std::vector<Tensor> corr_otf_backward(const Tensor& f1, const std::vector<Tensor
       d[l] = df[l] = res.back().data_ptr<float>();
     }
   }
+  Tensor fxs;  // deterministic mode: max|dout|, max|f1|, non-finite flag (the fixed-point scale)
+  if (det) fxs = at::zeros({4}, f1.options().dtype(at::kInt));
   rs::corr_otf_bwd_launch(f1.data_ptr(), p, Hs, Ws, levels, is_bf16(f1), coords.data_ptr<float>(),
                           B, H1, W1, C, radius, (float)scale, dout.data_ptr(), is_bf16(dout),
-                          df1.data_ptr<float>(), d, det, df, cur_stream());
+                          df1.data_ptr<float>(), d, det, df,
+                          det ? reinterpret_cast<unsigned*>(fxs.data_ptr<int>()) : nullptr, cur_stream());
   RS_CHECK_LAUNCH();
   return res;
 }

@@ -37,7 +37,7 @@ struct ConvLaunch {
   const float* chs;
   int f32;  // fp32 activations / outputs (split-bf16 tiles 6-8, conv_lds_kernel<..., F32>)
 };
-void conv_launch(const ConvLaunch& L, hipStream_t stream);
+bool conv_launch(const ConvLaunch& L, hipStream_t stream);
 struct SconvLaunch {
   const void* x;
   int xstr, Cin, B, Hi, Wi;
@@ -211,8 +211,9 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
-  TORCH_CHECK((tile >= 0 && tile <= 54) || (tile >= 56 && tile <= 68) || tile == 70,
-              "conv_fused: tile must be in [0,54], [56,68] or 70");
+  TORCH_CHECK((tile >= 0 && tile <= 54) || tile == 56 || tile == 57 || tile == 61 || tile == 65 || tile == 66 ||
+                  tile == 68 || tile == 70,
+              "conv_fused: tile must be in [0,54], 56, 57, 61, 65, 66, 68 or 70");
   if (tile == 70) {  // conv_gemm1.hip: 1x1 GEMM over 64-channel K chunks
     TORCH_CHECK(KH == 1 && KW == 1 && !f32, "conv_fused: tile 70 is the bf16 1x1 GEMM");
     for (size_t s = 0; s < segs.size(); ++s)
@@ -320,7 +321,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
     TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3 && tile != 70,
                 "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-70)");
   L.chs = nx.chs;
-  rs::conv_launch(L, stream());
+  TORCH_CHECK(rs::conv_launch(L, stream()), "conv_fused: tile ", L.tile, " is not instantiated for a ", KH, "x", KW,
+              " kernel");
   RS_CHECK_LAUNCH();
 }
 
@@ -408,7 +410,8 @@ void conv_geo(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::IntA
   L.geo = 1;
   L.Hi = Hi; L.Wi = Wi; L.SY = SY; L.SX = SX;
   L.oH = oH; L.oW = oW; L.OSY = OSY; L.OSX = OSX; L.OOY = OOY; L.OOX = OOX;
-  rs::conv_launch(L, stream());
+  TORCH_CHECK(rs::conv_launch(L, stream()), "conv_fused: tile ", L.tile, " is not instantiated for a ", KH, "x", KW,
+              " kernel");
   RS_CHECK_LAUNCH();
 }
 

@@ -171,8 +171,11 @@ class FlyingChairs(FlowDataset):
             return
         split_list = load_chairs_split(split_file, root)
         # a split table for a different release would silently mislabel pairs
-        assert len(split_list) == len(flows), (
-            f"FlyingChairs: split table has {len(split_list)} entries for {len(flows)} flow files")
+        if len(split_list) != len(flows):
+            raise ValueError(
+                f"FlyingChairs: split file {split_file!r} has {len(split_list)} entries but {root!r} holds "
+                f"{len(flows)} flow files; pass split_file= a table with one line (1 = train, 2 = val) per "
+                f"flow file of this directory (the packaged table is for the full 22,872-pair release)")
         want = {"training": 1, "validation": 2}.get(split)
         for i in range(len(flows)):
             if split_list[i] == want:

@@ -16,9 +16,9 @@ reference creates by registering the same norm module twice).
 MI355X notes: the encoders run once per image pair; on the GPU bf16 path
 their 3x3 (stride 1 and 2) and 1x1 convolutions run on the hand-written
 implicit-GEMM kernels (ops/enc_conv.py; fp32 -- inference and training -- on
-the split-bf16 F32 tiles; the 7x7 stem runs on csrc/stem.hip for fp32
-inference and on MIOpen in training, measured faster there; RAFT-small's
-narrow bottleneck convs run on csrc/sconv.hip at inference), and every
+the split-bf16 F32 tiles; the 7x7 stem runs on csrc/stem.hip, forward and
+weight gradient; RAFT-small's narrow bottleneck convs run on csrc/sconv.hip
+and csrc/sconv_train.hip), and every
 norm -> ReLU (-> residual add -> ReLU) chain is one fused NHWC pass of
 csrc/norm.hip (ops/norm.py) instead of PyTorch's instance_norm, which would
 copy each channels_last map to NCHW and back.  NHWC also keeps the 1x1

@@ -75,9 +75,10 @@ OVERLAP = {"cnet": True, "flow": True, "defer": True, "defer_enc": False}
 
 class _SplitPair(torch.autograd.Function):
     """``torch.split(x, [n, len(x) - n])`` whose backward returns the two
-    gradients' common buffer when they are its adjacent halves with x's
-    strides (the correlation backward writes d fmap1 / d fmap2 that way,
-    csrc/ops.cpp corr_volume_backward) instead of concatenating them."""
+    gradients' common buffer when they are adjacent halves of one tensor with
+    the same strides (the correlation backward writes d fmap1 / d fmap2 that
+    way, csrc/ops.cpp corr_volume_backward) instead of concatenating them; a
+    missing half's gradient is zeros of that half's shape (from ctx.shape)."""
 
     @staticmethod
     def forward(ctx, x, n):
@@ -86,12 +87,16 @@ class _SplitPair(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g1, g2):
+        n, shape = ctx.n, ctx.shape
+        if g1 is None and g2 is None:
+            return None, None
         if g1 is None or g2 is None:
             z = g2 if g1 is None else g1
-            if z is None:
-                return None, None
-            g1 = torch.zeros_like(g2) if g1 is None else g1
-            g2 = torch.zeros(ctx.shape[0] - ctx.n, *ctx.shape[1:], device=g1.device, dtype=g1.dtype) if g2 is None else g2
+            if g1 is None:
+                g1 = torch.zeros((n,) + tuple(shape[1:]), device=z.device, dtype=z.dtype)
+            else:
+                g2 = torch.zeros((shape[0] - n,) + tuple(shape[1:]), device=z.device, dtype=z.dtype)
+        assert tuple(g1.shape) == (n,) + tuple(shape[1:]) and tuple(g2.shape) == (shape[0] - n,) + tuple(shape[1:])
         if (g1.dtype == g2.dtype and g1.stride() == g2.stride() and g1.untyped_storage().data_ptr()
                 == g2.untyped_storage().data_ptr()
                 and g2.storage_offset() == g1.storage_offset() + g1.shape[0] * g1.stride(0)):

@@ -59,6 +59,21 @@ def from_nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 3, 1, 2)
 
 
+def _fused_bwd_ok(gpyr, B, N1, H2, W2, C, bf16, f32) -> bool:
+    """The preconditions of torch.ops.raft_stir.corr_volume_backward
+    (csrc/ops.cpp), checked here so shapes it refuses (large batches or grids)
+    take the fold + library-GEMM fallback instead of raising."""
+    if C % 128 or not (bf16 or f32):
+        return False
+    Ep = -(-(H2 * W2) // 64) * 64  # csrc/corr_bwd.hip corr_bwd_pitch (BK = 64)
+    coarse = sum(g.shape[2] * g.shape[3] for g in gpyr[1:])
+    row_fold = Ep <= 6144 and coarse <= 4096  # csrc/corr_lookup.hip pyr_fold_rows_kernel
+    g0 = gpyr[0]
+    if not (row_fold or (bf16 and g0.stride(1) % 4 == 0 and g0.data_ptr() % 16 == 0)):
+        return False
+    return B * N1 * Ep * 2 < 2 ** 31 and B * max(N1, H2 * W2) * C * 2 < 2 ** 31
+
+
 class _CorrVolume(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f1, f2, state: CorrState):
@@ -82,9 +97,7 @@ class _CorrVolume(torch.autograd.Function):
         g0 = state.gpyr[0]
         bf16 = f1.dtype == torch.bfloat16 and f2.dtype == torch.bfloat16
         f32 = f1.dtype == torch.float32 and f2.dtype == torch.float32
-        row_fold = -(-(H2 * W2) // 64) * 64 <= 6144  # csrc/corr_lookup.hip pyr_fold_rows_kernel
-        if C % 128 == 0 and ((bf16 and (row_fold or (g0.stride(1) % 4 == 0 and g0.data_ptr() % 16 == 0)))
-                             or (f32 and row_fold)):
+        if _fused_bwd_ok(state.gpyr, B, N1, H2, W2, C, bf16, f32):
             # csrc/corr_bwd.hip: one fold pass into a padded bf16 G, then both
             # feature-gradient GEMMs in one MFMA launch (deterministic); fp32
             # features: split-bf16 operands, three K passes, fp32 gradients

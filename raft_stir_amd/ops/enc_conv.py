@@ -655,13 +655,14 @@ def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residu
 #             3x3's (0, 0) phase as a second K segment (conv_pair)
 #   wgrad   : split-K MFMA over dY pixels with strided X rows
 _GEO = True
-_GEO_SCOPE = [True]  # per-encoder switch (geo_scope): RAFT-small's encoder keeps MIOpen
+_GEO_SCOPE = [True]  # per-encoder switch (geo_scope): off for RAFT-small's encoder (its narrow convs run on sconv)
 
 
 class geo_scope:
     """Enable / disable the strided-geometry path inside a block (set by the
-    encoder: RAFT-small's narrow bottleneck encoder measured faster on
-    MIOpen -- 657 vs 602 pairs/s -- while full RAFT's is neutral-to-faster)."""
+    encoder: RAFT-small's narrow 32-96-channel bottleneck convs run on the
+    csrc/sconv.hip / sconv_train.hip kernels instead -- the geometry tiles
+    measured 602 vs 657 pairs/s there -- while full RAFT uses them)."""
 
     def __init__(self, on: bool):
         self.on = on

@@ -25,6 +25,23 @@ from raft_stir_amd.export.pointtrack import (NUMITERS, POINTCOUNT, RaftPointTrac
 from raft_stir_amd.utils.padder import InputPadder  # noqa: E402
 
 
+def _torchscript_fallback(module, inputs, path, device):
+    """No onnx package: the same graph as TorchScript, reloaded and checked
+    against eager at the reference's ONNX tolerance (atol = rtol = 1e-2,
+    reference rafttoonnx.py:88; measured differences are ~1e-5)."""
+    module.eval()
+    with torch.no_grad(), _reference_mode():
+        traced = torch.jit.trace(module, inputs, check_trace=False)
+        traced.save(path)
+        want, got = module(*inputs), torch.jit.load(path, map_location=device)(*inputs)
+    err = max((w - g).abs().max().item() for w, g in zip(want, got))
+    for w, g in zip(want, got):
+        if not torch.allclose(g, w, atol=1e-2, rtol=1e-2):
+            raise AssertionError(f"{os.path.basename(path)} parity failed: max|diff|={err}")
+    print(f"onnx not installed: wrote {path} (TorchScript, max|diff| vs eager {err:.2e})")
+    return path
+
+
 def testconvertmodel(args, device):
     """Bare model on padded demo frames -> raftsmall.onnx (reference :49-92)."""
     images = sorted(glob.glob(os.path.join(args.path, "*.png")) + glob.glob(os.path.join(args.path, "*.jpg")))
@@ -38,30 +55,22 @@ def testconvertmodel(args, device):
     if onnx_available():
         return export_onnx(module, (image1, image2), os.path.join(args.out, "raftsmall.onnx"),
                            ["image1", "image2"], ["flow_low", "flow_up"])
-    # no onnx package: the same graph as TorchScript (raftsmall.pt), checked against eager
-    path = os.path.join(args.out, "raftsmall.pt")
-    module.eval()
-    with torch.no_grad(), _reference_mode():
-        traced = torch.jit.trace(module, (image1, image2), check_trace=False)
-        traced.save(path)
-        want, got = module(image1, image2), torch.jit.load(path, map_location=device)(image1, image2)
-    err = max((w - g).abs().max().item() for w, g in zip(want, got))
-    if err > 1e-3:
-        raise AssertionError(f"raftsmall.pt parity failed: max|diff|={err}")
-    print(f"onnx not installed: wrote {path} (TorchScript, max|diff| vs eager {err:.2e})")
-    return path
+    return _torchscript_fallback(module, (image1, image2), os.path.join(args.out, "raftsmall.pt"), device)
 
 
-def convertmodeldirect(args, device):
-    """Bare model on 1x3x512x640 -> raftsmall_STIR.onnx (reference :94-118)."""
-    if not onnx_available():
-        return None
+def convertmodeldirect(args, device, size=(512, 640)):
+    """Bare model on 1x3x512x640 (the STIR frame shape) -> raftsmall_STIR.onnx
+    (reference :94-118); without onnx, raftsmall_STIR.pt (TorchScript) with
+    the same parity check."""
     model = load_model(args, device)
     g = torch.Generator().manual_seed(0)
-    image1 = (torch.rand(1, 3, 512, 640, generator=g) * 255).to(device)
-    image2 = (torch.rand(1, 3, 512, 640, generator=g) * 255).to(device)
-    return export_onnx(_FlowOnly(model, NUMITERS), (image1, image2), os.path.join(args.out, "raftsmall_STIR.onnx"),
-                       ["image1", "image2"], ["flow_low", "flow_up"])
+    image1 = (torch.rand(1, 3, *size, generator=g) * 255).to(device)
+    image2 = (torch.rand(1, 3, *size, generator=g) * 255).to(device)
+    module = _FlowOnly(model, NUMITERS)
+    if onnx_available():
+        return export_onnx(module, (image1, image2), os.path.join(args.out, "raftsmall_STIR.onnx"),
+                           ["image1", "image2"], ["flow_low", "flow_up"])
+    return _torchscript_fallback(module, (image1, image2), os.path.join(args.out, "raftsmall_STIR.pt"), device)
 
 
 def convertmodelpointtrack(args, device):

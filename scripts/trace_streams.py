@@ -5,12 +5,17 @@ queues run while the main stream waits).
 
     python scripts/trace_streams.py gpurun_out/trace/train_kernel_trace.csv.gz [A_ms B_ms]
 
+Steps are delimited by the optimizer kernel; TRACE_ANCHOR=<kernel substring>
+(with TRACE_GROUP=<max index distance inside one anchor group>) delimits
+them by another kernel instead (scripts/bench_encoders.py: stem_fwd, 60).
+
 With A_ms B_ms: also list every kernel of the step that starts in [A, B] ms
 (queue, stream, start, duration) -- what each queue runs around a gap.
 """
 import collections
 import csv
 import gzip
+import os
 import sys
 
 TOP = 25
@@ -20,10 +25,16 @@ def main(path, window=None):
     op = gzip.open if path.endswith(".gz") else open
     rows = list(csv.DictReader(op(path, "rt")))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if ("FusedAdam" in r["Kernel_Name"] or "adamw_kernel" in r["Kernel_Name"])]
+    anchor = os.environ.get("TRACE_ANCHOR")  # e.g. "stem_fwd": steps delimited by this kernel's groups
+    if anchor:
+        idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
+        idx = [i - 1 for i in idx]  # the step ends just before the anchor group
+    else:
+        idx = [i for i, r in enumerate(rows) if ("FusedAdam" in r["Kernel_Name"] or "adamw_kernel" in r["Kernel_Name"])]
     groups = []
+    gap = int(os.environ.get("TRACE_GROUP", "2"))
     for i in idx:
-        if groups and i - groups[-1][-1] <= 2:
+        if groups and i - groups[-1][-1] <= gap:
             groups[-1].append(i)
         else:
             groups.append([i])

@@ -24,7 +24,7 @@ import torch  # noqa: E402
 
 F32_CANDIDATES = [6, 7, 8, 38, 39, 40]
 CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 42, 43,
-              44, 45, 46, 48, 49, 50, 51, 52, 53, 54, 56, 57, 60, 61, 62, 63, 64, 65, 66, 67, 68, 70]  # 56-68: calls that carry a wf weight; 70: 1x1
+              44, 45, 46, 48, 49, 50, 51, 52, 53, 54, 56, 57, 61, 65, 66, 68, 70]  # 56-68: calls that carry a wf weight; 70: 1x1
 
 
 def record_calls(args):

@@ -319,7 +319,7 @@ def test_packaged_chairs_split_rejects_other_release(fake_root, tmp_path, monkey
     """A Chairs copy whose pair count differs from the packaged table's 22,872
     fails loudly instead of mislabelling train / validation pairs."""
     monkeypatch.chdir(tmp_path)
-    with pytest.raises(AssertionError, match="split table has 22872 entries for 3 flow files"):
+    with pytest.raises(ValueError, match="has 22872 entries but .* holds 3 flow files"):
         datasets.FlyingChairs(split="training", root=f"{fake_root}/FlyingChairs_release/data",
                               split_file="no_such_split.txt")
 

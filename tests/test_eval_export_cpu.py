@@ -111,6 +111,11 @@ def test_cli_scripts(fake_root, tmp_path):
     assert os.path.exists(tmp_path / "exp" / "raft_pointtrackSTIR.pt")
     # the demo-shape export of the bare model (ONNX, or TorchScript without onnx)
     assert os.path.exists(tmp_path / "exp" / "raftsmall.pt") or os.path.exists(tmp_path / "exp" / "raftsmall.onnx")
+    # ... and the STIR-shape (1x3x512x640) bare-model export, reference rafttoonnx.py:94-118
+    assert (os.path.exists(tmp_path / "exp" / "raftsmall_STIR.pt")
+            or os.path.exists(tmp_path / "exp" / "raftsmall_STIR.onnx"))
+    if not os.path.exists(tmp_path / "exp" / "raftsmall_STIR.onnx"):
+        assert "raftsmall_STIR.pt (TorchScript, max|diff| vs eager" in res.stdout
     # without --random_init a missing checkpoint is an error (reference CLIs load strictly)
     res = subprocess.run([sys.executable, os.path.join(ROOT, "evaluate.py"), "--small", "--dataset", "kitti",
                           "--data_root", r, "--model", str(tmp_path / "typo.pth")], env=env,

@@ -88,7 +88,7 @@ def test_conv_v2_tiles_vs_conv2d(cuda, k, tile, shape):
 def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
     """csrc/conv_v3.h (weight-streaming tiles: per-wave A fragments global ->
     VGPR from the fragment-major layout, halo per 64-channel chunk in LDS, one
-    barrier per chunk): every tile 60-64 on partial patches in both
+    barrier per chunk): every tile on partial patches in both
     directions, three input segments (4 chunks: the halo double buffer flips
     an even and an odd number of times), Cout not a multiple of the block's
     (the row blocks past the packed weight read as zeros)."""
@@ -114,6 +114,31 @@ def test_conv_v3_tiles_vs_conv2d(cuda, k, tile, shape):
     got = out[..., :cout].float().permute(0, 3, 1, 2)
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
     assert (out[..., cout:] == 7).all()
+
+
+@pytest.mark.parametrize("tile", list(V3_TILES))
+def test_conv_v3_tiles_segment_offsets(cuda, tile):
+    """The v3 tiles on segment windows that start inside their tensors, the
+    layout of RAFT-small's padded GRU-q conv (models/fused_update.py: r*h in
+    a 128-channel buffer, x read as hx[64:256] of a 256-channel buffer with
+    zero weights on the pad): nonzero offsets and strides wider than the
+    window, vs F.conv2d on the same windows."""
+    torch.manual_seed(6)
+    B, H, W = 1, 13, 45
+    rh = torch.randn(B, H, W, 128, device=cuda).to(torch.bfloat16)
+    hx = torch.randn(B, H, W, 256, device=cuda).to(torch.bfloat16)
+    segs = [(rh, 0, 128), (hx, 64, 192)]
+    cin, cout = 128 + 192, 96
+    for kh, kw in ((1, 5), (5, 1), (3, 3)):
+        w = torch.randn(cout, cin, kh, kw, device=cuda) * 0.05
+        w[:, 96:128] = 0  # the zero-weight pad channels of the small engine's r*h buffer
+        b = torch.randn(cout, device=cuda)
+        wp = pack_weight(w, [(128, [(0, 128, 0)]), (192, [(128, 192, 0)])], pad_to(cout, 32))
+        out = torch.zeros(B, H, W, cout, device=cuda, dtype=torch.bfloat16)
+        conv_fused(segs, wp, pack_bias(b), kh, kw, cout, EPI_SCALE, out, 0, scale=0.5, tile=tile, wf=frag_weight(wp))
+        x = torch.cat([rh, hx[..., 64:]], -1).float().permute(0, 3, 1, 2)
+        ref = F.conv2d(x, _bf(w), b, padding=(kh // 2, kw // 2)) * 0.5
+        torch.testing.assert_close(out.float().permute(0, 3, 1, 2), ref, atol=3e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("cout", [256, 576, 70])
