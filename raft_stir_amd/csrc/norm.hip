@@ -84,6 +84,20 @@ struct Args {
   int B, P, C, S, G;
   int relu;
   float inv_n;
+  // second upstream gradient (backward), added to dy on the fly: the skip
+  // path's gradient of a residual block's input
+  const void* dy2;
+  // affine residual: res is a RAW tensor normalised on the fly,
+  // r = (res - rmean) * rrstd * rgamma + rbeta (the downsample shortcut's
+  // norm, no ReLU); backward: its (sum g, sum g * xhat) partials go to ws2,
+  // apply_bwd writes its input gradient (rs1 / rs2 = its finalized sums) to dres
+  const float* rmean;
+  const float* rrstd;
+  const float* rgamma;
+  const float* rbeta;
+  const float* rs1;
+  const float* rs2;
+  float* ws2;
 };
 
 // BatchNorm running-statistics update, applied by finalize_kernel<0> for
@@ -112,11 +126,12 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
   const int b = blockIdx.y, s = blockIdx.x;
   const int chunk = cdiv(a.P, a.S);
   const int p0 = s * chunk, p1 = min(a.P, p0 + chunk);
-  float acc0[VN], acc1[VN];
+  float acc0[VN], acc1[VN], racc0[VN], racc1[VN];
 #pragma unroll
-  for (int i = 0; i < VN; ++i) acc0[i] = acc1[i] = 0.f;
+  for (int i = 0; i < VN; ++i) acc0[i] = acc1[i] = racc0[i] = racc1[i] = 0.f;
   const int g = a.G == 1 ? 0 : b;
-  float mu[VN], rs_[VN], ga[VN], be[VN];
+  const bool aff = MODE == 1 && a.rmean != nullptr;  // affine residual (+ its own partials)
+  float mu[VN], rs_[VN], ga[VN], be[VN], rmu[VN], rrs[VN], rsc[VN], rsh[VN];
   if (MODE == 1 && row < rows) {
 #pragma unroll
     for (int i = 0; i < VN; ++i) {
@@ -125,14 +140,21 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
       rs_[i] = a.rstd[g * a.C + c];
       ga[i] = a.gamma ? a.gamma[c] : 1.f;
       be[i] = a.beta ? a.beta[c] : 0.f;
+      if (aff) {
+        rmu[i] = a.rmean[g * a.C + c];
+        rrs[i] = a.rrstd[g * a.C + c];
+        rsc[i] = (a.rgamma ? a.rgamma[c] : 1.f) * rrs[i];
+        rsh[i] = (a.rbeta ? a.rbeta[c] : 0.f) - rmu[i] * rsc[i];
+      }
     }
   }
   if (row < rows) {
     const T* x = static_cast<const T*>(a.x) + (size_t)b * a.P * a.C;
     const T* dy = static_cast<const T*>(a.dy) + (size_t)b * a.P * a.C;
+    const T* dy2 = a.dy2 ? static_cast<const T*>(a.dy2) + (size_t)b * a.P * a.C : nullptr;
     const T* res = a.res ? static_cast<const T*>(a.res) + (size_t)b * a.P * a.C : nullptr;
     for (int p = p0 + row; p < p1; p += rows * 4) {
-      typename V::raw xq[4], dq[4], rq[4];
+      typename V::raw xq[4], dq[4], rq[4], eq[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int pp = p + u * rows;
@@ -141,6 +163,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
           xq[u] = V::ldraw(x + off);
           if (MODE == 1) {
             dq[u] = V::ldraw(dy + off);
+            if (dy2) eq[u] = V::ldraw(dy2 + off);
             if (res) rq[u] = V::ldraw(res + off);
           }
         }
@@ -157,8 +180,13 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
             acc1[i] += xv[i] * xv[i];
           }
         } else {
-          float dv[VN], rv[VN];
+          float dv[VN], rv[VN], ev[VN];
           V::cvt(dq[u], dv);
+          if (dy2) {
+            V::cvt(eq[u], ev);
+#pragma unroll
+            for (int i = 0; i < VN; ++i) dv[i] += ev[i];
+          }
           if (res) V::cvt(rq[u], rv);
 #pragma unroll
           for (int i = 0; i < VN; ++i) {
@@ -166,7 +194,11 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
             const float pre = ga[i] * xh + be[i];
             const float y1 = a.relu ? fmaxf(pre, 0.f) : pre;
             float gg = dv[i];
-            if (res && rv[i] + y1 <= 0.f) gg = 0.f;
+            if (res && (aff ? rv[i] * rsc[i] + rsh[i] : rv[i]) + y1 <= 0.f) gg = 0.f;
+            if (aff) {  // the residual branch's gradient, before the main branch's ReLU mask
+              racc0[i] += gg;
+              racc1[i] += gg * ((rv[i] - rmu[i]) * rrs[i]);
+            }
             if (a.relu && pre <= 0.f) gg = 0.f;
             acc0[i] += gg;
             acc1[i] += gg * xh;
@@ -177,23 +209,26 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
   }
   __shared__ float sm[THREADS * 8 * 2];
   const int rr = row < rows ? row : rows;  // idle threads park outside
+  for (int set = 0; set < (aff ? 2 : 1); ++set) {
+    if (set) __syncthreads();  // the first set's combine is done with sm
 #pragma unroll
-  for (int i = 0; i < VN; ++i) {
-    if (row < rows) {
-      sm[(rr * a.C + col * VN + i) * 2] = acc0[i];
-      sm[(rr * a.C + col * VN + i) * 2 + 1] = acc1[i];
+    for (int i = 0; i < VN; ++i) {
+      if (row < rows) {
+        sm[(rr * a.C + col * VN + i) * 2] = set ? racc0[i] : acc0[i];
+        sm[(rr * a.C + col * VN + i) * 2 + 1] = set ? racc1[i] : acc1[i];
+      }
     }
-  }
-  __syncthreads();
-  for (int c = tid; c < a.C; c += THREADS) {
-    float t0 = 0.f, t1 = 0.f;
-    for (int r = 0; r < rows; ++r) {
-      t0 += sm[(r * a.C + c) * 2];
-      t1 += sm[(r * a.C + c) * 2 + 1];
+    __syncthreads();
+    for (int c = tid; c < a.C; c += THREADS) {
+      float t0 = 0.f, t1 = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        t0 += sm[(r * a.C + c) * 2];
+        t1 += sm[(r * a.C + c) * 2 + 1];
+      }
+      float* w = (set ? a.ws2 : a.ws) + (((size_t)b * a.S + s) * a.C + c) * 2;
+      w[0] = t0;
+      w[1] = t1;
     }
-    float* w = a.ws + (((size_t)b * a.S + s) * a.C + c) * 2;
-    w[0] = t0;
-    w[1] = t1;
   }
 }
 
@@ -203,7 +238,14 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
 // (short serial chains: batch-norm groups have B * S partials per channel).
 template <int MODE>
 __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, int S, int C, int G,
-                                                       float eps, float inv_n, float* o0, float* o1, Running run) {
+                                                       float eps, float inv_n, float* o0, float* o1, Running run,
+                                                       const float* ws2 = nullptr, float* o2 = nullptr,
+                                                       float* o3 = nullptr) {
+  if (blockIdx.z) {  // the second partial set (MODE 1 with an affine residual)
+    ws = ws2;
+    o0 = o2;
+    o1 = o3;
+  }
   const int g = blockIdx.x;
   const int c = blockIdx.y * 8 + (threadIdx.x & 7);
   const int part = threadIdx.x >> 3;
@@ -288,13 +330,20 @@ __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
   const int b = blockIdx.y, g = a.G == 1 ? 0 : b;
   const int chunk = cdiv(a.P, a.S);
   const int p0 = blockIdx.x * chunk, p1 = min(a.P, p0 + chunk);
-  float sc[VN], sh[VN];
+  float sc[VN], sh[VN], rsc[VN], rsh[VN];
+  const bool aff = a.rmean != nullptr;
 #pragma unroll
   for (int i = 0; i < VN; ++i) {
     const int c = col * VN + i;
     const float r = a.rstd[g * a.C + c];
     sc[i] = (a.gamma ? a.gamma[c] : 1.f) * r;
     sh[i] = (a.beta ? a.beta[c] : 0.f) - a.mean[g * a.C + c] * sc[i];
+    rsc[i] = 1.f;
+    rsh[i] = 0.f;
+    if (aff) {
+      rsc[i] = (a.rgamma ? a.rgamma[c] : 1.f) * a.rrstd[g * a.C + c];
+      rsh[i] = (a.rbeta ? a.rbeta[c] : 0.f) - a.rmean[g * a.C + c] * rsc[i];
+    }
   }
   const size_t base = (size_t)b * a.P * a.C + col * VN;
   const T* x = static_cast<const T*>(a.x) + base;
@@ -322,7 +371,7 @@ __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
       for (int i = 0; i < VN; ++i) {
         float v = xv[0][i] * sc[i] + sh[i];
         if (relu) v = fmaxf(v, 0.f);
-        if (res) v = fmaxf(v + rv[0][i], 0.f);
+        if (res) v = fmaxf(v + rv[0][i] * rsc[i] + rsh[i], 0.f);
         out[i] = v;
       }
       V::store(y + (size_t)pp * a.C, out);
@@ -344,6 +393,8 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   // pre = x*sc + sh ; dx = k1*gg - k1*m1 - (x - mean)*k2  with
   // k1 = gamma*rstd, m1 = s1/N, k2 = gamma*rstd^2*s2/N
   float sc[VN], sh[VN], k0[VN], k2[VN], mu[VN];
+  float rsc[VN], rsh[VN], rk0[VN], rk2[VN], rmu[VN];
+  const bool aff = a.rmean != nullptr;
 #pragma unroll
   for (int i = 0; i < VN; ++i) {
     const int c = col * VN + i;
@@ -354,22 +405,34 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
     sh[i] = (a.beta ? a.beta[c] : 0.f) - mu[i] * sc[i];
     k0[i] = sc[i] * a.s1[g * a.C + c] * a.inv_n;
     k2[i] = sc[i] * r * a.s2[g * a.C + c] * a.inv_n;
+    rsc[i] = 1.f;
+    rsh[i] = rk0[i] = rk2[i] = rmu[i] = 0.f;
+    if (aff) {  // the residual's own normalisation (forward constants, backward sums)
+      const float rr = a.rrstd[g * a.C + c];
+      rmu[i] = a.rmean[g * a.C + c];
+      rsc[i] = (a.rgamma ? a.rgamma[c] : 1.f) * rr;
+      rsh[i] = (a.rbeta ? a.rbeta[c] : 0.f) - rmu[i] * rsc[i];
+      rk0[i] = rsc[i] * a.rs1[g * a.C + c] * a.inv_n;
+      rk2[i] = rsc[i] * rr * a.rs2[g * a.C + c] * a.inv_n;
+    }
   }
   const size_t base = (size_t)b * a.P * a.C + col * VN;
   const T* x = static_cast<const T*>(a.x) + base;
   const T* dy = static_cast<const T*>(a.dy) + base;
+  const T* dy2 = a.dy2 ? static_cast<const T*>(a.dy2) + base : nullptr;
   const T* res = a.res ? static_cast<const T*>(a.res) + base : nullptr;
   T* dx = static_cast<T*>(a.dx) + base;
   T* dres = a.dres ? static_cast<T*>(a.dres) + base : nullptr;
   const bool relu = a.relu;
   for (int p = p0 + row; p < p1; p += rows * UNR) {
-    typename V::raw xq[UNR], dq[UNR], rq[UNR];
+    typename V::raw xq[UNR], dq[UNR], rq[UNR], eq[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int pp = p + u * rows;
       if (pp < p1) {
         xq[u] = V::ldraw(x + (size_t)pp * a.C);
         dq[u] = V::ldraw(dy + (size_t)pp * a.C);
+        if (dy2) eq[u] = V::ldraw(dy2 + (size_t)pp * a.C);
         if (res) rq[u] = V::ldraw(res + (size_t)pp * a.C);
       }
     }
@@ -377,17 +440,24 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
     for (int u = 0; u < UNR; ++u) {
       const int pp = p + u * rows;
       if (pp >= p1) break;
-      float dxo[VN], dro[VN], xv[VN], dv[VN], rv[VN];
+      float dxo[VN], dro[VN], xv[VN], dv[VN], rv[VN], ev[VN];
       V::cvt(xq[u], xv);
       V::cvt(dq[u], dv);
+      if (dy2) {
+        V::cvt(eq[u], ev);
+#pragma unroll
+        for (int i = 0; i < VN; ++i) dv[i] += ev[i];
+      }
       if (res) V::cvt(rq[u], rv);
 #pragma unroll
       for (int i = 0; i < VN; ++i) {
         const float pre = xv[i] * sc[i] + sh[i];
         const float y1 = relu ? fmaxf(pre, 0.f) : pre;
         float gout = dv[i];
-        if (res && rv[i] + y1 <= 0.f) gout = 0.f;
-        dro[i] = gout;
+        if (res && rv[i] * rsc[i] + rsh[i] + y1 <= 0.f) gout = 0.f;
+        // residual input gradient: the skip gradient itself, or through the
+        // residual's normalisation (affine residual)
+        dro[i] = aff ? rsc[i] * gout - rk0[i] - (rv[i] - rmu[i]) * rk2[i] : gout;
         const float gg = (relu && pre <= 0.f) ? 0.f : gout;
         dxo[i] = sc[i] * gg - k0[i] - (xv[i] - mu[i]) * k2[i];
       }
@@ -446,11 +516,14 @@ void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, flo
                      C, G, eps, inv_n, mean, rstd, run);
 }
 
+// rnorm (4 pointers or null): the residual is raw and normalised with
+// (mean, rstd, gamma, beta) = rnorm[0..3] (affine residual, no ReLU)
 void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
-                     int G, bool relu, void* y, hipStream_t s) {
+                     int G, bool relu, void* y, const float* const* rnorm, hipStream_t s) {
   norm::Args a{};
   a.x = x; a.res = res; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.y = y;
+  if (rnorm) { a.rmean = rnorm[0]; a.rrstd = rnorm[1]; a.rgamma = rnorm[2]; a.rbeta = rnorm[3]; }
   a.B = B; a.P = P; a.C = C; a.G = G; a.relu = relu;
   a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
   if (bf16)
@@ -459,22 +532,30 @@ void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mea
     hipLaunchKernelGGL(norm::apply_fwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
 }
 
+// dy2: second upstream gradient (added on the fly) or null.  rnorm: as in
+// norm_fwd_launch; then ws2 (same size as ws) and rs1 / rs2 receive the
+// residual normalisation's sums and dres its input gradient.
 void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
-                     void* dres, hipStream_t s) {
+                     void* dres, const void* dy2, const float* const* rnorm, float* ws2, float* rs1,
+                     float* rs2, hipStream_t s) {
   norm::Args a{};
   a.x = x; a.dy = dy; a.res = res; a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta;
-  a.B = B; a.P = P; a.C = C; a.G = G; a.relu = relu; a.ws = ws;
+  a.B = B; a.P = P; a.C = C; a.G = G; a.relu = relu; a.ws = ws; a.dy2 = dy2;
+  if (rnorm) {
+    a.rmean = rnorm[0]; a.rrstd = rnorm[1]; a.rgamma = rnorm[2]; a.rbeta = rnorm[3];
+    a.ws2 = ws2;
+  }
   a.S = norm::pick_splits(B, P, C, bf16 ? 8 : 4);
   dim3 grid(a.S, B);
   if (bf16)
     hipLaunchKernelGGL((norm::reduce_kernel<bf16_t, 1>), grid, dim3(norm::THREADS), 0, s, a);
   else
     hipLaunchKernelGGL((norm::reduce_kernel<float, 1>), grid, dim3(norm::THREADS), 0, s, a);
-  hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 8)), dim3(256), 0, s, ws, B, a.S,
-                     C, G, 0.f, 0.f, s1, s2, norm::Running{});
-  a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres;
+  hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 8), rnorm ? 2 : 1), dim3(256), 0, s, ws, B, a.S,
+                     C, G, 0.f, 0.f, s1, s2, norm::Running{}, ws2, rs1, rs2);
+  a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres; a.rs1 = rs1; a.rs2 = rs2;
   a.inv_n = batch_stats ? 1.f / (float)((G == 1 ? (double)B : 1.0) * P) : 0.f;
   a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
   if (bf16)

@@ -13,11 +13,12 @@ void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, flo
                        float mom, float unb, hipStream_t s);
 void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
-                     int G, bool relu, void* y, hipStream_t s);
+                     int G, bool relu, void* y, const float* const* rnorm, hipStream_t s);
 void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int B, int P, int C,
                      int G, bool relu, bool batch_stats, float* ws, float* s1, float* s2, void* dx,
-                     void* dres, hipStream_t s);
+                     void* dres, const void* dy2, const float* const* rnorm, float* ws2, float* rs1,
+                     float* rs2, hipStream_t s);
 }  // namespace rs
 
 namespace {
@@ -77,9 +78,39 @@ std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps, con
   return {mean, rstd};
 }
 
+// rmean / rrstd (+ rgamma / rbeta): the residual is a RAW tensor normalised
+// on the fly (no ReLU on it) -- the downsample shortcut's norm inside the
+// block's output pass (models/fused_encoder.py)
+struct RNorm {
+  const float* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool on = false;
+};
+
+RNorm rnorm_args(const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rrstd,
+                 const c10::optional<Tensor>& rgamma, const c10::optional<Tensor>& rbeta, const Tensor& mean,
+                 const c10::optional<Tensor>& res, int64_t C) {
+  RNorm r;
+  TORCH_CHECK(bool(rmean) == bool(rrstd), "norm: rmean / rrstd come together");
+  if (!rmean) return r;
+  TORCH_CHECK(bool(res), "norm: an affine residual needs res");
+  TORCH_CHECK(rmean->sizes() == mean.sizes() && rrstd->sizes() == mean.sizes() && rmean->is_contiguous() &&
+                  rrstd->is_contiguous() && rmean->scalar_type() == at::kFloat && rrstd->scalar_type() == at::kFloat,
+              "norm: residual statistics must match the main statistics' shape");
+  check_param(rgamma, C, "rgamma");
+  check_param(rbeta, C, "rbeta");
+  r.p[0] = rmean->data_ptr<float>();
+  r.p[1] = rrstd->data_ptr<float>();
+  r.p[2] = fptr(rgamma);
+  r.p[3] = fptr(rbeta);
+  r.on = true;
+  return r;
+}
+
 Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
                 const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
-                const c10::optional<Tensor>& res, bool relu) {
+                const c10::optional<Tensor>& res, bool relu, const c10::optional<Tensor>& rmean,
+                const c10::optional<Tensor>& rrstd, const c10::optional<Tensor>& rgamma,
+                const c10::optional<Tensor>& rbeta) {
   check_x(x);
   const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
   const int G = mean.size(0);
@@ -89,11 +120,12 @@ Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
   check_param(gamma, C, "gamma");
   check_param(beta, C, "beta");
   check_like(res, x, "residual");
+  const RNorm rn = rnorm_args(rmean, rrstd, rgamma, rbeta, mean, res, C);
   const c10::DeviceGuard g(x.device());
   Tensor y = at::empty_like(x);
   rs::norm_fwd_launch(x.scalar_type() == at::kBFloat16, x.data_ptr(), res ? res->data_ptr() : nullptr,
                       mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
-                      G, relu, y.data_ptr(), stream());
+                      G, relu, y.data_ptr(), rn.on ? rn.p : nullptr, stream());
   RS_CHECK_LAUNCH();
   return y;
 }
@@ -102,14 +134,21 @@ Tensor norm_act(const Tensor& x, const Tensor& mean, const Tensor& rstd,
 // and the (2, G, C) buffer s1 / s2 are views of.
 // batch_stats=false: the statistics were constants (BatchNorm in eval mode), so
 // dx = gamma * rstd * g without the mean/variance terms.
+// dy2: a second upstream gradient added on the fly (the skip path's).  With
+// an affine residual (rmean ...) dres is the gradient of the RAW residual
+// through its normalisation, and a sixth output holds its (2, G, C) sums.
 std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const Tensor& mean,
                                       const Tensor& rstd, const c10::optional<Tensor>& gamma,
                                       const c10::optional<Tensor>& beta,
                                       const c10::optional<Tensor>& res, bool relu,
-                                      bool batch_stats) {
+                                      bool batch_stats, const c10::optional<Tensor>& dy2,
+                                      const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rrstd,
+                                      const c10::optional<Tensor>& rgamma, const c10::optional<Tensor>& rbeta) {
   check_x(x);
   check_like(dy, x, "grad");
+  check_like(dy2, x, "second grad");
   check_like(res, x, "residual");
+  TORCH_CHECK(!rmean || batch_stats, "norm_act_backward: an affine residual needs batch statistics");
   const int B = x.size(0), P = x.size(1) * x.size(2), C = x.size(3);
   const int G = mean.size(0);
   TORCH_CHECK(mean.numel() == (int64_t)G * C && rstd.numel() == (int64_t)G * C && (G == 1 || G == B),
@@ -126,11 +165,21 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
   Tensor s1 = s12.select(0, 0), s2 = s12.select(0, 1);
   Tensor dx = at::empty_like(x);
   Tensor dres = res ? at::empty_like(x) : at::empty({0}, x.options());
+  const RNorm rn = rnorm_args(rmean, rrstd, rgamma, rbeta, mean, res, C);
+  Tensor ws2, r12;
+  if (rn.on) {
+    ws2 = at::empty_like(ws);
+    r12 = at::empty({2, G, C}, fo);
+  }
   rs::norm_bwd_launch(bf, x.data_ptr(), dy.data_ptr(), res ? res->data_ptr() : nullptr,
                       mean.data_ptr<float>(), rstd.data_ptr<float>(), fptr(gamma), fptr(beta), B, P, C,
                       G, relu, batch_stats, ws.data_ptr<float>(), s1.data_ptr<float>(),
-                      s2.data_ptr<float>(), dx.data_ptr(), res ? dres.data_ptr() : nullptr, stream());
+                      s2.data_ptr<float>(), dx.data_ptr(), res ? dres.data_ptr() : nullptr,
+                      dy2 ? dy2->data_ptr() : nullptr, rn.on ? rn.p : nullptr,
+                      rn.on ? ws2.data_ptr<float>() : nullptr, rn.on ? r12.data_ptr<float>() : nullptr,
+                      rn.on ? r12.data_ptr<float>() + (int64_t)G * C : nullptr, stream());
   RS_CHECK_LAUNCH();
+  if (rn.on) return {dx, dres, s1, s2, s12, r12};
   return {dx, dres, s1, s2, s12};
 }
 
@@ -139,8 +188,11 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
   m.def("norm_stats(Tensor x, bool per_sample, float eps, Tensor(a!)? running_mean=None, "
         "Tensor(b!)? running_var=None, Tensor(c!)? nbt=None, Tensor? bias=None, float momentum=0.1, int n=0) -> Tensor[]");
-  m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu) -> Tensor");
-  m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, bool batch_stats) -> Tensor[]");
+  m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, "
+        "Tensor? rmean=None, Tensor? rrstd=None, Tensor? rgamma=None, Tensor? rbeta=None) -> Tensor");
+  m.def("norm_act_backward(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, "
+        "bool relu, bool batch_stats, Tensor? dy2=None, Tensor? rmean=None, Tensor? rrstd=None, "
+        "Tensor? rgamma=None, Tensor? rbeta=None) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_stir, CUDA, m) {

@@ -39,6 +39,7 @@ from ..ops import reference as ref
 from ..ops.upsample import convex_upsample, upflow8
 from .corr import CorrBlock, AlternateCorrBlock
 from .extractor import BasicEncoder, SmallEncoder
+from .fused_encoder import FusedEncoders
 from .fused_update import FusedUpdate
 from .fused_train import DeferGrads, FusedTrainEngine, FusedTrainLoop
 from .update import BasicUpdateBlock, SmallUpdateBlock
@@ -153,6 +154,13 @@ class RAFT(nn.Module):
             self.__dict__["_fused_train"] = eng
         return eng
 
+    def _encoder_engine(self):
+        eng = self.__dict__.get("_fused_enc")
+        if eng is None or eng.model is not self:
+            eng = FusedEncoders(self)
+            self.__dict__["_fused_enc"] = eng
+        return eng
+
     def _fused_engine(self):
         eng = self.__dict__.get("_fused")
         if eng is None or eng.model is not self:
@@ -251,7 +259,14 @@ class RAFT(nn.Module):
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
         with self._autocast(dev), enc_defer:
-            if side is not None:
+            fused_enc = (side is not None and xin is not None and self.training and not test_mode
+                         and FusedEncoders.eligible(self, xin))
+            if fused_enc:
+                # both encoders, forward and backward, as one scheduled node
+                # (models/fused_encoder.py): fnet on main, cnet on the side stream
+                xf, cnet = self._encoder_engine().run(xin, image1, side)
+                fmap1, fmap2 = _SplitPair.apply(xf, image1.shape[0])
+            elif side is not None:
                 # fnet (main) and cnet (side) stage by stage, interleaved on the host
                 xf = xin if xin is not None else torch.cat([image1, image2], dim=0)
                 xc = image1

@@ -42,11 +42,23 @@ def main():
     gf = torch.randn(of.shape, device=dev).to(of.dtype).contiguous(memory_format=torch.channels_last)
     gc = torch.randn(oc.shape, device=dev).to(oc.dtype).contiguous(memory_format=torch.channels_last)
 
+    from raft_stir_amd.models.fused_encoder import FusedEncoders
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        fused = FusedEncoders.eligible(m, xf)
+    print(f"encoder path: {'fused engine (models/fused_encoder.py)' if fused else 'per-module autograd'}")
+
     def step():
         wpack.refresh()
         main = torch.cuda.current_stream(dev)
         side.wait_stream(main)
         with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                f, c = m._encoder_engine().run(xf, xc, side)
+                main.wait_stream(side)
+                c = _StreamHandoff.apply(c, side)
+                loss = (f.float() * gf.float()).sum() + (c.float() * gc.float()).sum()
+                loss.backward()
+                return
             f, c = xf, xc
             ff, fc = m.fnet.stage_fns(), m.cnet.stage_fns()
             for k in range(max(len(ff), len(fc))):

@@ -144,3 +144,50 @@ def test_bn_recalibration_then_eval(cuda):
         y = conv_norm_act(conv, norm, x)
         yr = F.relu(rnorm(rconv(x)))
     torch.testing.assert_close(y, yr, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("kind", ["instance", "batch"])
+def test_norm_affine_residual_and_second_grad(cuda, kind):
+    """csrc/norm.hip extensions used by models/fused_encoder.py: the output
+    pass relu(relu(n2(a)) + n3(d)) with the shortcut's norm n3 applied on the
+    fly to the RAW d, its backward (gradient of a AND of raw d, both norms'
+    parameter sums) and a second upstream gradient added inside the kernels,
+    against fp32 autograd on the module composite."""
+    torch.manual_seed(0)
+    B, C, H, W = 3, 96, 12, 20
+    mk = (lambda: nn.InstanceNorm2d(C)) if kind == "instance" else (lambda: nn.BatchNorm2d(C))
+    n2, n3 = mk().to(cuda), mk().to(cuda)
+    if kind == "batch":
+        with torch.no_grad():
+            for n in (n2, n3):
+                n.weight.uniform_(0.5, 1.5)
+                n.bias.uniform_(-0.3, 0.3)
+    a = (torch.randn(B, C, H, W, device=cuda) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    d = (torch.randn(B, C, H, W, device=cuda) - 0.3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g1 = torch.randn(B, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g2 = torch.randn(B, C, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    # reference (fp32 autograd)
+    af, df = a.float().requires_grad_(), d.float().requires_grad_()
+    ref = torch.relu(torch.relu(n2(af)) + n3(df))
+    (ref * (g1.float() + g2.float())).sum().backward()
+    nh = lambda t: t.permute(0, 2, 3, 1).contiguous()
+    R = torch.ops.raft_stir
+    inst = kind == "instance"
+    st2 = R.norm_stats(nh(a), inst, n2.eps)
+    st3 = R.norm_stats(nh(d), inst, n3.eps)
+    gm = lambda n: None if inst else n.weight.detach()
+    bt = lambda n: None if inst else n.bias.detach()
+    y = R.norm_act(nh(a), st2[0], st2[1], gm(n2), bt(n2), nh(d), True, st3[0], st3[1], gm(n3), bt(n3))
+    torch.testing.assert_close(y.float(), nh(ref.detach()), atol=3e-2, rtol=2e-2)
+    out = R.norm_act_backward(nh(g1), nh(a), st2[0], st2[1], gm(n2), bt(n2), nh(d), True, True, nh(g2),
+                              st3[0], st3[1], gm(n3), bt(n3))
+    da, dd, r12 = out[0], out[1], out[5]
+    scale = lambda t: t.abs().max().item()
+    assert (da.float() - nh(af.grad)).abs().max().item() < 3e-2 * scale(af.grad)
+    assert (dd.float() - nh(df.grad)).abs().max().item() < 3e-2 * scale(df.grad)
+    if not inst:
+        dgamma3, dbeta3 = r12[1].sum(0), r12[0].sum(0)
+        torch.testing.assert_close(dbeta3, n3.bias.grad, atol=2e-2 * scale(n3.bias.grad), rtol=2e-2)
+        torch.testing.assert_close(dgamma3, n3.weight.grad, atol=2e-2 * scale(n3.weight.grad), rtol=2e-2)
+        s12 = out[4]
+        torch.testing.assert_close(s12[0].sum(0), n2.bias.grad, atol=2e-2 * scale(n2.bias.grad), rtol=2e-2)
