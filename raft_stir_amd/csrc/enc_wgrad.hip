@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __re
                                                                int Cin, float* __restrict__ dw) {
   __shared__ float red[4][64];
   const int o = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + o;
+  const int i = blockIdx.x * 64 + o;  // dw element in channels_last order (co, tap, ci)
   const bool live = i < Cout * 9 * Cin;
   float s = 0.f;
   int co = 0, ci = 0, k = 0;
@@ -257,7 +257,9 @@ __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __re
   }
   red[sl][o] = s;
   __syncthreads();
-  if (sl == 0 && live) dw[((size_t)co * Cin + ci) * 9 + k] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+  // channels_last (the layout of the model's conv weights: the gradient is
+  // stored as .grad without a layout copy), coalesced along ci
+  if (sl == 0 && live) dw[i] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
 }
 
 }  // namespace encw

@@ -702,7 +702,8 @@ Tensor enc_wgrad(const Tensor& dy, const Tensor& x) {
   L.nsplit = rs::enc_wgrad_splits(B, H, W, Cin, Cout, &L.tpb);
   const int64_t nblk = int64_t(L.nsplit) * ((Cout + 63) / 64) * ((Cin + 63) / 64);
   Tensor part = at::empty({nblk * 64 * 9 * 64}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(at::kFloat));
+  // channels_last: the element order the reduce kernel writes (co, tap, ci)
+  Tensor dw = at::empty({Cout, Cin, 3, 3}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
   L.part = part.data_ptr<float>();
   L.dw = dw.data_ptr<float>();
   rs::enc_wgrad_launch(L, stream());

@@ -11,14 +11,18 @@ Per-module autograd (ops/enc_conv.py + ops/norm.py) runs every conv and
 every normalisation as its own Function: ~6.9 ms of host enqueue per step
 for ~6.4 ms of GPU work (profiles/r6/README.md, scripts/bench_encoders.py),
 and the normalisation chains cannot be restructured across Function
-boundaries.  Here a plan of the two encoders is built once and
-``FusedEncoders.run`` / ``EncoderFn`` run
+boundaries.  Here a plan of the two encoders is built once and each
+encoder STAGE (stem, six residual blocks, head) is one autograd node
+(``_StageFn``):
 
   forward  : fnet stage k on the main HIP stream, cnet stage k on the side
-             stream, k = stem, six residual blocks, head -- every conv and
-             norm kernel called directly on NHWC buffers;
-  backward : the hand-written reverse of the same plan on the same streams
-             (fnet on main, cnet on side), weight gradients with their dgrads.
+             stream -- every conv and norm kernel called directly on NHWC
+             buffers;
+  backward : the hand-written reverse of each stage on the same stream,
+             weight gradients with their dgrads; autograd interleaves the
+             two encoders' stages as their gradients become ready (a single
+             node per encoder serialised them: cnet's whole backward was
+             issued before fnet's could start).
 
 Normalisation layout per residual block (bias folded away: a per-channel
 constant before instance / train-mode batch norm has no effect and a zero
@@ -39,6 +43,7 @@ gradient statistics come out of the output pass's backward.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -153,6 +158,11 @@ class _Plan:
 
 
 # ------------------------------------------------------------------ conv steps
+# (Statistics written by the conv epilogues instead of a separate pass were
+# measured slower: the v3 / halo convs run 1-2 waves per SIMD, where the
+# epilogue's extra VALU work and LDS transposition are not hidden -- +12-15 %
+# per conv against a 9-24 us statistics pass; branch exp/epilogue-stats,
+# profiles/r6/README.md.)
 def _conv3x3(xn, weight, cout):
     N, H, W, cin = xn.shape
     out = torch.empty(N, H, W, cout, device=xn.device, dtype=_BF)
@@ -186,11 +196,6 @@ def _wgrad3x3(dyn, xn, weight):
     cout, cin = weight.shape[:2]
     N, H, W, _ = xn.shape
     return E._wgrad3x3(dyn, _nchw(xn), xn, weight, cin, cout, N * H * W)
-
-
-class _EncState:
-    """Saved activations of one encoder's forward."""
-    __slots__ = ("x", "a0", "st0", "y0", "blocks", "ylast", "out")
 
 
 def _stem_fwd(plan, x):
@@ -232,29 +237,6 @@ def _head_fwd(plan, y):
     return E._conv_geo_fwd(_nchw(y), h.weight, h.bias, (1, 1), (0, 0))
 
 
-def _enc_stages(plan):
-    """The forward as a list of stage callables over a shared state (so two
-    encoders can be issued stage-interleaved on two streams)."""
-    def stem(s, x):
-        s.x = x
-        s.a0, s.st0, s.y0 = _stem_fwd(plan, x)
-        s.blocks = []
-        return s.y0
-
-    def block(i):
-        def run(s, y):
-            blk, n1, n2, d = plan.blocks[i]
-            out, saved = _block_fwd(blk, n1, n2, d, y)
-            s.blocks.append(saved)
-            return out
-        return run
-
-    def head(s, y):
-        s.ylast = y
-        return _head_fwd(plan, y)
-    return [stem] + [block(i) for i in range(len(plan.blocks))] + [head]
-
-
 # ------------------------------------------------------------------ backward
 def _norm_bwd(n, dy, xn, st, relu, res=None, dy2=None, rn=None, rst=None):
     """(dx, dres, [param grads], [residual-norm param grads]) of
@@ -269,94 +251,127 @@ def _norm_bwd(n, dy, xn, st, relu, res=None, dy2=None, rn=None, rst=None):
     return out[0], out[1], n.param_grads(out[4]), rn.param_grads(out[5])
 
 
-def _enc_bwd_stages(plan, s, grads):
-    """Backward stages in reverse order; each returns the gradient of its input.
-    ``grads``: dict param -> gradient (filled in)."""
-    zero_bias = lambda conv: torch.zeros_like(conv.bias)
+class _Stage:
+    """One stage of one encoder (stem, a residual block or the head): its
+    forward, its backward and its parameters.  ``sink`` is shared by the
+    stages of one encoder: a residual block's backward leaves the skip-path
+    gradient of its input there for the previous stage's backward, which
+    takes it as the second upstream gradient of its output normalisation
+    (no separate add pass, and the autograd edge carries only the conv
+    input gradient)."""
 
-    def head(gpair):
-        h = plan.head
-        gn = E._nhwc(gpair[0].to(_BF))
-        y = s.ylast
-        dy = E._conv_geo_dgrad([gn], [h.weight], _nchw(y).shape, (1, 1), (0, 0))
-        dw, db = E._conv_geo_wgrad(gn, _nchw(y), h.weight, (1, 1), True)
-        grads[h.weight], grads[h.bias] = dw, db
-        return dy, None
+    def __init__(self, plan, kind, index, sink):
+        self.plan, self.kind, self.i, self.sink = plan, kind, index, sink
+        if kind == "stem":
+            conv, n0 = plan.stem
+            self.params = [conv.weight, conv.bias, *n0.params()]
+        elif kind == "head":
+            self.params = [plan.head.weight, plan.head.bias]
+        else:
+            blk, n1, n2, d = plan.blocks[index]
+            self.params = [blk.conv1.weight, blk.conv1.bias, *n1.params(), blk.conv2.weight, blk.conv2.bias,
+                           *n2.params()]
+            if d is not None:
+                self.params += [d[0].weight, d[0].bias, *d[1].params()]
+        self.saved = None
 
-    def block(i):
-        def run(gpair):
-            g, g2 = gpair  # g2: the skip gradient of the next block, added inside the norm kernels
-            blk, n1, n2, d = plan.blocks[i]
-            y, a1, st1, y1, a2, st2, dd_raw, st3 = s.blocks[i]
-            if d is None:
-                da2, dres, pg2, _ = _norm_bwd(n2, g, a2, st2, True, y, g2)
-            else:  # dres: the gradient of the raw shortcut conv output, through its norm
-                da2, dres, pg2, pg3 = _norm_bwd(n2, g, a2, st2, True, dd_raw, g2, d[1], st3)
-            dy1, _ = _dgrad3x3(da2, blk.conv2.weight, blk.conv2.in_channels)
-            grads[blk.conv2.weight] = _wgrad3x3(da2, y1, blk.conv2.weight)
-            grads[blk.conv2.bias] = zero_bias(blk.conv2)
-            for p, gp in zip(n2.params(), pg2):
-                grads[p] = gp
-            da1, _, pg1, _ = _norm_bwd(n1, dy1, a1, st1, True)
-            grads[blk.conv1.bias] = zero_bias(blk.conv1)
-            for p, gp in zip(n1.params(), pg1):
-                grads[p] = gp
-            if d is None:
-                dy, fused = _dgrad3x3(da1, blk.conv1.weight, blk.conv1.in_channels, acc=dres)
-                grads[blk.conv1.weight] = _wgrad3x3(da1, y, blk.conv1.weight)
-                return dy, (None if fused else dres)
-            ddn = dres
-            for p, gp in zip(d[1].params(), pg3):
-                grads[p] = gp
-            grads[d[0].bias] = zero_bias(d[0])
-            stride = tuple(blk.conv1.stride)
-            dy = E._pair_dgrad(da1, ddn, blk.conv1.weight, d[0].weight, _nchw(y).shape, stride)
-            grads[blk.conv1.weight] = E._conv_geo_wgrad(da1, _nchw(y), blk.conv1.weight, stride, False)[0]
-            grads[d[0].weight] = E._conv_geo_wgrad(ddn, _nchw(y), d[0].weight, stride, False)[0]
-            return dy, None
-        return run
+    # ------------------------------------------------------------- forward
+    def forward(self, x):
+        if self.kind == "stem":
+            a0, st0, y0 = _stem_fwd(self.plan, x)
+            self.saved = (x, a0, st0)
+            return y0
+        if self.kind == "head":
+            self.saved = (x,)
+            return _head_fwd(self.plan, x)
+        blk, n1, n2, d = self.plan.blocks[self.i]
+        out, self.saved = _block_fwd(blk, n1, n2, d, x)
+        return out
 
-    def stem(gpair):
-        g, g2 = gpair
-        conv, n0 = plan.stem
-        da0, _, pg0, _ = _norm_bwd(n0, g, s.a0, s.st0, True, None, g2)
-        for p, gp in zip(n0.params(), pg0):
-            grads[p] = gp
-        gw = torch.empty(conv.weight.shape, device=g.device, dtype=torch.float32)
-        R.stem_wgrad(E._nhwc(s.x), da0, conv.weight.shape[0], gw)
-        grads[conv.weight] = gw.to(conv.weight.dtype)
-        grads[conv.bias] = zero_bias(conv)
-        return None, None
-    return [head] + [block(i) for i in reversed(range(len(plan.blocks)))] + [stem]
+    # ------------------------------------------------------------ backward
+    def _zero_bias(self, bias):
+        """The exactly-zero gradient of a conv bias folded into a batch /
+        instance norm: disjoint slices of ONE zeroed buffer per encoder and
+        step (one fill instead of one per bias; distinct memory per
+        parameter, so AccumulateGrad may keep them as .grad)."""
+        buf = self.sink.get("zb")
+        if buf is None or buf[1] + bias.numel() > buf[0].numel():
+            n = sum(c.bias.numel() for c in self.plan.enc.modules() if isinstance(c, nn.Conv2d))
+            buf = [torch.zeros(n, device=bias.device, dtype=bias.dtype), 0]
+            self.sink["zb"] = buf
+        t = buf[0][buf[1]:buf[1] + bias.numel()].view_as(bias)
+        buf[1] += bias.numel()
+        return t
+
+    def backward(self, g):
+        """(input gradient, {param: gradient}); g: this stage's output gradient."""
+        grads = {}
+        g = g.contiguous()
+        g2 = self.sink.pop(self.i, None)  # the next block's skip gradient of this output
+        zb = self._zero_bias
+        if self.kind == "head":
+            h, (y,) = self.plan.head, self.saved
+            gn = g.to(_BF)
+            dy = E._conv_geo_dgrad([gn], [h.weight], _nchw(y).shape, (1, 1), (0, 0))
+            grads[h.weight], grads[h.bias] = E._conv_geo_wgrad(gn, _nchw(y), h.weight, (1, 1), True)
+            return dy, grads
+        if self.kind == "stem":
+            conv, n0 = self.plan.stem
+            x, a0, st0 = self.saved
+            da0, _, pg0, _ = _norm_bwd(n0, g, a0, st0, True, None, g2)
+            grads.update(zip(n0.params(), pg0))
+            gw = torch.empty(conv.weight.shape, device=g.device, dtype=torch.float32)
+            R.stem_wgrad(E._nhwc(x), da0, conv.weight.shape[0], gw)
+            grads[conv.weight] = gw.to(conv.weight.dtype)
+            grads[conv.bias] = zb(conv.bias)
+            return None, grads
+        blk, n1, n2, d = self.plan.blocks[self.i]
+        y, a1, st1, y1, a2, st2, dd_raw, st3 = self.saved
+        if d is None:
+            da2, dres, pg2, _ = _norm_bwd(n2, g, a2, st2, True, y, g2)
+        else:  # dres: the gradient of the raw shortcut conv output, through its norm
+            da2, dres, pg2, pg3 = _norm_bwd(n2, g, a2, st2, True, dd_raw, g2, d[1], st3)
+            grads.update(zip(d[1].params(), pg3))
+        grads.update(zip(n2.params(), pg2))
+        dy1, _ = _dgrad3x3(da2, blk.conv2.weight, blk.conv2.in_channels)
+        grads[blk.conv2.weight] = _wgrad3x3(da2, y1, blk.conv2.weight)
+        grads[blk.conv2.bias] = zb(blk.conv2.bias)
+        da1, _, pg1, _ = _norm_bwd(n1, dy1, a1, st1, True)
+        grads.update(zip(n1.params(), pg1))
+        grads[blk.conv1.bias] = zb(blk.conv1.bias)
+        if d is None:
+            dy, fused = _dgrad3x3(da1, blk.conv1.weight, blk.conv1.in_channels, acc=dres)
+            grads[blk.conv1.weight] = _wgrad3x3(da1, y, blk.conv1.weight)
+            if not fused:
+                self.sink[self.i - 1] = dres
+            return dy, grads
+        grads[d[0].bias] = zb(d[0].bias)
+        stride = tuple(blk.conv1.stride)
+        dy = E._pair_dgrad(da1, dres, blk.conv1.weight, d[0].weight, _nchw(y).shape, stride)
+        grads[blk.conv1.weight] = E._conv_geo_wgrad(da1, _nchw(y), blk.conv1.weight, stride, False)[0]
+        grads[d[0].weight] = E._conv_geo_wgrad(dres, _nchw(y), d[0].weight, stride, False)[0]
+        return dy, grads
 
 
-class EncoderFn(torch.autograd.Function):
-    """One encoder as one autograd node.  Its forward was already run
-    (FusedEncoders.run issues both encoders' forwards stage-interleaved on
-    two streams); this node hands out the output and owns the backward,
-    which autograd runs on the stream of the forward (main for fnet, side for
-    cnet) as soon as THIS encoder's gradient is ready: cnet's backward
-    starts right after the update loop's and overlaps the correlation
-    backward that fnet's waits for."""
+class _StageFn(torch.autograd.Function):
+    """One encoder stage as one autograd node; autograd runs its backward on
+    the stream of its forward (fnet: main, cnet: side) and interleaves the two
+    encoders' stage nodes by creation order, as soon as each gradient is
+    ready (cnet's backward starts right after the update loop's and overlaps
+    the correlation backward that fnet's waits for)."""
 
     @staticmethod
-    def forward(ctx, plan, state, x, *params):
-        ctx.plan, ctx.state = plan, state
-        out = state.out
-        state.out = None
-        return _nchw(out)
+    def forward(ctx, stage, x, *params):
+        ctx.stage = stage
+        return stage.forward(x)
 
     @staticmethod
     def backward(ctx, g):
-        plan, s = ctx.plan, ctx.state
-        if g is None:
-            g = _nchw(torch.zeros(s.ylast.shape[:3] + (plan.head.out_channels,), device=s.ylast.device))
-        grads = {}
-        cur = (g, None)
-        for stage in _enc_bwd_stages(plan, s, grads):
-            cur = stage(cur)
-        ctx.state = None
-        return (None, None, None, *[grads[p] for p in plan.params])
+        stage = ctx.stage
+        dx, grads = stage.backward(g)
+        stage.saved = None
+        ctx.stage = None
+        return (None, dx, *[grads[p] for p in stage.params])
 
 
 class FusedEncoders:
@@ -369,31 +384,31 @@ class FusedEncoders:
 
     @staticmethod
     def eligible(model, x) -> bool:
-        return (ENABLED and x.is_cuda and _ext.use_hip(x) and torch.is_grad_enabled() and torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dtype == torch.float32
-                and x.is_contiguous(memory_format=_CL) and _Plan.ok(model.fnet) and _Plan.ok(model.cnet)
-                and not torch.jit.is_tracing())
+        return (ENABLED and x.is_cuda and _ext.use_hip(x) and torch.is_grad_enabled()
+                and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                and x.dtype == torch.float32 and x.is_contiguous(memory_format=_CL)
+                and _Plan.ok(model.fnet) and _Plan.ok(model.cnet) and not torch.jit.is_tracing())
+
+    @staticmethod
+    def _stages(plan):
+        sink = {}
+        n = len(plan.blocks)
+        return ([_Stage(plan, "stem", -1, sink)] + [_Stage(plan, "block", i, sink) for i in range(n)]
+                + [_Stage(plan, "head", n, sink)])
 
     def run(self, xf, xc, side):
-        """(fnet(xf), cnet(xc)): both forwards issued stage by stage on the
-        main and ``side`` streams, then one :class:`EncoderFn` node per
-        encoder (cnet's created under ``side``).  The caller joins ``side``
-        before the main stream reads cnet's output."""
-        main = torch.cuda.current_stream(xf.device)
-        sf, sc = _EncState(), _EncState()
-        ff, fc = _enc_stages(self.fplan), _enc_stages(self.cplan)
-        side.wait_stream(main)
-        xc.record_stream(side)
-        with torch.no_grad():
-            of, oc = xf, xc
-            for k in range(max(len(ff), len(fc))):
-                if k < len(ff):
-                    of = ff[k](sf, of)
-                if k < len(fc):
-                    with torch.cuda.stream(side):
-                        oc = fc[k](sc, oc)
-        sf.out, sc.out = of, oc
-        f = EncoderFn.apply(self.fplan, sf, xf, *self.fplan.params)
-        with torch.cuda.stream(side):
-            c = EncoderFn.apply(self.cplan, sc, xc, *self.cplan.params)
-        return f, c
+        """(fnet(xf), cnet(xc)) as NCHW views of channels-last bf16: stage k of
+        fnet on the current stream, then stage k of cnet on ``side`` (None:
+        the single-stream schedule, same kernels in the same order).  The
+        caller joins ``side`` before the main stream reads cnet's output."""
+        ff, fc = self._stages(self.fplan), self._stages(self.cplan)
+        on_side = torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(xf.device))
+            xc.record_stream(side)
+        of, oc = xf, xc
+        for sf, sc in zip(ff, fc):
+            of = _StageFn.apply(sf, of, *sf.params)
+            with on_side:
+                oc = _StageFn.apply(sc, oc, *sc.params)
+        return _nchw(of), _nchw(oc)

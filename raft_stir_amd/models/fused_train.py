@@ -344,7 +344,7 @@ class FusedTrainEngine:
             pc.wd = bf[k * ob:k * (ob + n)].view(wds[0], wds[1], k * wds[2])
             ob += n
             # fragment-major copies (bf16 engine): conv_fused finds them through
-            # the packed weight's _rs_frag attribute when a tile 60-64 is chosen
+            # the packed weight's _rs_frag attribute when a weight-streaming tile (56-68) is chosen
             pc.wf = pc.wdf = None
             if hf:
                 pc.wf = bf[ob:ob + ws.numel()].view(ws)

@@ -259,8 +259,7 @@ class RAFT(nn.Module):
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
         with self._autocast(dev), enc_defer:
-            fused_enc = (side is not None and xin is not None and self.training and not test_mode
-                         and FusedEncoders.eligible(self, xin))
+            fused_enc = (xin is not None and self.training and not test_mode and FusedEncoders.eligible(self, xin))
             if fused_enc:
                 # both encoders, forward and backward, as one scheduled node
                 # (models/fused_encoder.py): fnet on main, cnet on the side stream
@@ -294,11 +293,11 @@ class RAFT(nn.Module):
             corr_fn = block(fmap1, fmap2, num_levels=self.cfg.corr_levels,
                             radius=self.cfg.corr_radius, out_dtype=corr_dtype, **kw)
 
-            if side is None:
-                cnet = self.cnet(image1)
-            else:
+            if side is not None:
                 main.wait_stream(side)
                 cnet = _StreamHandoff.apply(cnet, side)
+            elif not fused_enc:
+                cnet = self.cnet(image1)
             fused_train = not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn)
             if fused_train and not self.cfg.small:
                 # the fused engine splits the context features and applies tanh / relu
