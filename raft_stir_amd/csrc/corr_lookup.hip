@@ -450,6 +450,84 @@ __global__ __launch_bounds__(256) void pyr_fold_rows_kernel(PyrMut g, int levels
   }
 }
 
+// Wave-per-row form of the padded bf16 fold (the training shape's operand of
+// corr_bwd.hip: 22,816 rows of 2,852 level-0 cells): each wave owns one row,
+// issues ALL its level-0 loads (QW float4 per lane, 16-B coalesced) and the
+// row's coarse cells (staged in the wave's own LDS slice, no block barrier)
+// before it computes; four rows per 256-thread block.  The block-per-row
+// kernel above issued <= 3 loads per thread behind a block-wide barrier and
+// ran at ~1.7 TB/s (profiles/r2/README.md); this one is bound by the HBM
+// stream (profiles/r6/README.md).
+constexpr int FW_LDS = 1024;  // coarse cells per row (wave): training shape 953
+template <int QW>
+__global__ __launch_bounds__(256) void pyr_fold_wave_kernel(PyrMut g, int levels, float scale,
+                                                            bf16_t* __restrict__ out, int OP, int rows) {
+  __shared__ float cl[4][FW_LDS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;  // whole wave (no block-level barrier below)
+  const int H0 = g.H[0], W0 = g.W[0], E = H0 * W0;
+  const float* r0 = g.p[0] + (size_t)row * g.S[0];
+  float4 v[QW];
+#pragma unroll
+  for (int j = 0; j < QW; ++j) {
+    const int e = (lane + 64 * j) * 4;
+    v[j] = e + 4 <= E ? *reinterpret_cast<const float4*>(r0 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < E && e + 4 > E) {  // the row's ragged tail
+      v[j].x = r0[e];
+      if (e + 1 < E) v[j].y = r0[e + 1];
+      if (e + 2 < E) v[j].z = r0[e + 2];
+    }
+  }
+  int off[4] = {0, 0, 0, 0};
+  {
+    int o = 0;
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      off[l] = o;
+      if (l < levels) {
+        const int n = g.H[l] * g.W[l];
+        const float* rl = g.p[l] + (size_t)row * g.S[l];
+        for (int i = lane; i < n; i += 64) cl[wave][o + i] = rl[i];
+        o += n;
+      }
+    }
+  }
+  // the wave's own LDS slice: order its stores before the other lanes' reads
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const float inv_w = 1.f / (float)W0;
+#pragma unroll
+  for (int j = 0; j < QW; ++j) {
+    const int e = (lane + 64 * j) * 4;
+    if (e >= OP) break;
+    float f[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    if (e < E) {
+      int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (e + k < E) {
+          float w = 1.f;
+#pragma unroll
+          for (int l = 1; l < 4; ++l) {
+            if (l >= levels) break;
+            w *= 0.25f;
+            const int yl = y >> l, xl = x >> l;  // (floor pooling: the last odd row / column has no parent)
+            if (yl < g.H[l] && xl < g.W[l]) f[k] += w * cl[wave][off[l] + yl * g.W[l] + xl];
+          }
+        }
+        if (++x == W0) {
+          x = 0;
+          ++y;
+        }
+      }
+    }
+    const uint2 pk = make_uint2(uint32_t(f2bf(f[0] * scale)) | (uint32_t(f2bf(f[1] * scale)) << 16),
+                                uint32_t(f2bf(f[2] * scale)) | (uint32_t(f2bf(f[3] * scale)) << 16));
+    *reinterpret_cast<uint2*>(out + (size_t)row * OP + e) = pk;
+  }
+}
+
 inline int grid_for(long total) {
   long blocks = (total + 255) / 256;
   if (blocks > 65535L * 8) blocks = 65535L * 8;
@@ -547,6 +625,21 @@ void pyr_grad_fold_launch(float* const* gpyr, const int* Hs, const int* Ws, cons
   if (opitch <= 0) opitch = (int)E;
   long coarse = 0;
   for (int l = 1; l < levels; ++l) coarse += (long)Hs[l] * Ws[l];
+  const bool aligned0 = Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0;
+  bool alignedc = true;
+  for (int l = 1; l < levels; ++l) alignedc = alignedc && gpyr[l] != nullptr;
+  if (out_bf16 && !out_lo && aligned0 && alignedc && opitch % 4 == 0 && opitch <= 64 * 4 * 12 &&
+      coarse <= lookup::FW_LDS && rows < (1L << 31)) {
+    const unsigned grid = (unsigned)((rows + 3) / 4);
+    const int qw = (opitch + 255) / 256;  // float4 per lane
+#define RS_FW(Q) hipLaunchKernelGGL((lookup::pyr_fold_wave_kernel<Q>), dim3(grid), dim3(256), 0, stream, p, levels, \
+                                    scale, static_cast<bf16_t*>(out_bf16), opitch, (int)rows)
+    if (qw <= 4) RS_FW(4);
+    else if (qw <= 8) RS_FW(8);
+    else RS_FW(12);
+#undef RS_FW
+    return;
+  }
   if (out_bf16 && opitch % 4 == 0 && opitch <= 6144 && coarse <= lookup::FOLD_LDS && rows < (1L << 31)) {
     const int vec0 = Ss[0] % 4 == 0 && reinterpret_cast<uintptr_t>(gpyr[0]) % 16 == 0;
     hipLaunchKernelGGL(lookup::pyr_fold_rows_kernel, dim3((unsigned)rows), dim3(256), 0, stream, p, levels, scale,

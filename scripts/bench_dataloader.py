@@ -11,6 +11,7 @@ reference's augmentation parameters, /root/reference/core/datasets.py:199-234,
 the DataLoader with N worker processes.
 
     python scripts/bench_dataloader.py --workers 4 --batch 8 --batches 60
+    python scripts/bench_dataloader.py --ranks 8 --workers 1   # 8 concurrent ranks (slowest rank reported)
 
 Prints one JSON line: pairs/s per rank (one rank = one DataLoader), the
 per-worker rate, and the engine's consumption rate it is compared against.
@@ -61,20 +62,51 @@ def main() -> None:
     ap.add_argument("--files", type=int, default=256, help="synthetic pairs written")
     ap.add_argument("--engine-rate", type=float, default=386.0,
                     help="pairs/s per GPU the training engine consumes (round-3 headline)")
+    ap.add_argument("--ranks", type=int, default=1,
+                    help="concurrent ranks on this host (one DataLoader each, the data-parallel node's feed)")
     a = ap.parse_args()
 
-    import torch
-
-    from raft_stir_amd.data.datasets import fetch_dataloader
-    torch.set_num_threads(1)
     with tempfile.TemporaryDirectory() as root:
         t0 = time.perf_counter()
         write_chairs(root, a.files)
         t_write = time.perf_counter() - t0
-        args = argparse.Namespace(stage="chairs", image_size=[368, 496], batch_size=a.batch, num_workers=a.workers,
-                                  data_root=root, seed=1234,
+        if a.ranks <= 1:
+            rate = _measure(a, root, 0, None)
+        else:
+            import multiprocessing as mp
+            ctx = mp.get_context("spawn")
+            bar, q = ctx.Barrier(a.ranks), ctx.Queue()
+            procs = [ctx.Process(target=_rank_main, args=(a, root, r, bar, q)) for r in range(a.ranks)]
+            for p in procs:
+                p.start()
+            rates = [q.get(timeout=900) for _ in procs]
+            for p in procs:
+                p.join()
+            rate = min(rates)
+    print(json.dumps({
+        "metric": "chairs training feed (FlowDataset + FlowAugmentor + DataLoader), pairs/s per rank",
+        "pairs_per_s": round(rate, 1), "per_worker": round(rate / max(1, a.workers), 1),
+        "workers": a.workers, "ranks": a.ranks, "batch": a.batch, "batches": a.batches, "crop": [368, 496],
+        "engine_pairs_per_s": a.engine_rate, "feed_over_engine": round(rate / a.engine_rate, 2),
+        "cpus_visible": os.cpu_count(), "cpus_usable": len(os.sched_getaffinity(0)), "write_s": round(t_write, 1),
+    }))
+
+
+def _rank_main(a, root, rank, bar, q):
+    q.put(_measure(a, root, rank, bar))
+
+
+def _measure(a, root, rank, bar):
+    """pairs/s of one rank's DataLoader (the slowest rank bounds the step)."""
+    import torch
+
+    from raft_stir_amd.data.datasets import fetch_dataloader
+    torch.set_num_threads(1)
+    if True:
+        args = argparse.Namespace(stage="chairs", image_size=[368, 496], batch_size=a.batch * a.ranks,
+                                  num_workers=a.workers, data_root=root, seed=1234,
                                   chairs_split=os.path.join(root, "FlyingChairs_release", "chairs_split.txt"))
-        loader = fetch_dataloader(args, rank=0, world_size=1, pin_memory=False)
+        loader = fetch_dataloader(args, rank=rank, world_size=a.ranks, pin_memory=False)
         it = iter(loader)
         n_done = 0
 
@@ -87,19 +119,14 @@ def main() -> None:
                 return next(it)
         for _ in range(a.warmup):
             nxt()
+        if bar is not None:
+            bar.wait()  # every rank's workers are up: time them concurrently
         t0 = time.perf_counter()
         for _ in range(a.batches):
             b = nxt()
             n_done += b[0].shape[0]
         dt = time.perf_counter() - t0
-    rate = n_done / dt
-    print(json.dumps({
-        "metric": "chairs training feed (FlowDataset + FlowAugmentor + DataLoader), pairs/s per rank",
-        "pairs_per_s": round(rate, 1), "per_worker": round(rate / max(1, a.workers), 1),
-        "workers": a.workers, "batch": a.batch, "batches": a.batches, "crop": [368, 496],
-        "engine_pairs_per_s": a.engine_rate, "feed_over_engine": round(rate / a.engine_rate, 2),
-        "cpus_visible": os.cpu_count(), "write_s": round(t_write, 1),
-    }))
+    return n_done / dt
 
 
 if __name__ == "__main__":
