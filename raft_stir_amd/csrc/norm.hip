@@ -475,8 +475,12 @@ int pick_apply_splits(int B, int P, int C, int vn) {
   return max(1, min(S, cdiv(P, rows * UNR * 2)));
 }
 
+// total reduction blocks (larger grids measured slower in situ, round 4);
+// norm_set_reduce_blocks: in-situ A/B of the target (RS_NORM_REDUCE_BLOCKS)
+int g_reduce_target = 512;
+
 int pick_splits(int B, int P, int C, int vn) {
-  constexpr int target = 512;  // total reduction blocks (larger grids measured slower in situ, round 4)
+  const int target = g_reduce_target;
   const int rows = THREADS / (C / vn);
   int S = cdiv(target, B);
   S = max(1, min(S, cdiv(P, rows * 8)));
@@ -489,6 +493,8 @@ int grid_elem(size_t nvec) {
 }
 
 }  // namespace norm
+
+void norm_set_reduce_blocks(int n) { norm::g_reduce_target = n > 0 ? n : 512; }
 
 // ------------------------------------------------------------------ launchers
 int norm_ws_floats(int B, int P, int C, bool bf16) {

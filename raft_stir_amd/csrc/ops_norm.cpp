@@ -8,6 +8,7 @@
 
 namespace rs {
 int norm_ws_floats(int B, int P, int C, bool bf16);
+void norm_set_reduce_blocks(int n);
 void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, float eps, float* ws,
                        float* mean, float* rstd, float* rm, float* rv, long long* nbt, const float* rbias,
                        float mom, float unb, hipStream_t s);
@@ -183,9 +184,12 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
   return {dx, dres, s1, s2, s12};
 }
 
+void norm_set_reduce_blocks_op(int64_t n) { rs::norm_set_reduce_blocks((int)n); }
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(raft_stir, m) {
+  m.def("norm_set_reduce_blocks(int n) -> ()", &norm_set_reduce_blocks_op);
   m.def("norm_stats(Tensor x, bool per_sample, float eps, Tensor(a!)? running_mean=None, "
         "Tensor(b!)? running_var=None, Tensor(c!)? nbt=None, Tensor? bias=None, float momentum=0.1, int n=0) -> Tensor[]");
   m.def("norm_act(Tensor x, Tensor mean, Tensor rstd, Tensor? gamma, Tensor? beta, Tensor? res, bool relu, "

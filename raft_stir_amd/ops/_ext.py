@@ -45,6 +45,8 @@ def load(raise_on_error: bool = False) -> bool:
                 try:
                     torch.ops.load_library(path)
                     _LOADED = True
+                    if os.environ.get("RS_NORM_REDUCE_BLOCKS"):  # in-situ A/B knob (csrc/norm.hip)
+                        torch.ops.raft_stir.norm_set_reduce_blocks(int(os.environ["RS_NORM_REDUCE_BLOCKS"]))
                 except Exception as e:  # pragma: no cover - depends on box
                     _LOADED, _ERROR = False, repr(e)
     if raise_on_error and not _LOADED:

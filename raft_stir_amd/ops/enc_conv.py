@@ -69,12 +69,18 @@ def _halo_ok(cin: int, cout: int) -> bool:
 # 96 channels are read as two overlapping 64-channel windows, [0, 64) and
 # [32, 96), with zero weights on the duplicated half.
 _V3 = True
+# 64 -> 64 convs with at least this many pixels stay on the halo kernel: both
+# encoders' 1/2-res convs at the training shape (fnet 730k, cnet 365k pixels;
+# cnet on the halo kernel: 431.5 / 431.0 vs 429.7 / 429.2 pairs/s with v3 tile
+# 65, profiles/r6/ab_halo_cnet_s10.txt -- and its backward gets the halo
+# kernel's skip-gradient accumulation).  RS_HALO_MIN_P: A/B of the crossover
+_HALO_MIN_P = int(os.environ.get("RS_HALO_MIN_P", "300000"))
 
 
 def _v3_tile(P: int, cin: int, cout: int):
     if not _V3 or cin % 32 or cin < 64 or cout % 32:
         return None
-    if cin == 64 and cout == 64 and P >= 600000:
+    if cin == 64 and cout == 64 and P >= _HALO_MIN_P:
         return None
     # (tile 68, the 8-wave 64 x 384-px tile, wins the isolated cnet 1/2-res
     # conv but costs 131 vs 91 us per call inside the training step, where it
