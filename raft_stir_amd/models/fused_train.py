@@ -57,6 +57,7 @@ instantiations.
 from __future__ import annotations
 
 import contextlib
+import os
 
 
 import torch
@@ -73,14 +74,23 @@ CORR_PAD = 384
 SHD = 96          # RAFT-small: hidden dim, 4 levels x 7 x 7 correlation taps (radius 3)
 SCORR_C = 196
 SCORR_PAD = 256
+# RAFT-small bf16: the GRU-q and head forward and the q / conv / convc1 dgrads
+# read 64-multiple K windows (zero weights on the padding) so that the
+# weight-streaming tiles (3x3) and the 1x1 GEMM serve them instead of the
+# 32-deep-K register tiles (inference does the same, models/fused_update.py)
+_SMALL_KPAD = os.environ.get("RS_SMALL_KPAD", "1") != "0"
 
 
 class _PConv:
     """A conv of the update block: forward packing, dgrad packing, grad unpacking."""
 
-    def __init__(self, convs, segs, scale=1.0, wsegs=None):
+    def __init__(self, convs, segs, scale=1.0, wsegs=None, fsegs=None, dk=None):
         self.convs = convs if isinstance(convs, (list, tuple)) else [convs]
         self.segs = segs          # [(C, [(w0, n, s0), ...]), ...] as in pack_weight
+        # the forward's own input windows (default: segs, which also define the
+        # dgrad's output channels) and the dgrad's K (default: Cout to 32)
+        self.fsegs = fsegs if fsegs is not None else segs
+        self.dk = dk
         # segment layout of the weight-gradient GEMM (its K segments must be
         # multiples of 64: RAFT-small reads wider, zero-weighted windows there)
         self.wsegs = wsegs if wsegs is not None else segs
@@ -103,15 +113,21 @@ class _PConv:
         cout, cin, kh, kw = weight.shape
         taps = kh * kw
         wt = weight.permute(0, 2, 3, 1).reshape(cout, taps, cin)
-        w = torch.full((pad_to(cout, 128), taps, self.ktot), fill, dtype=torch.long)
-        kb = 0
-        for c, pieces in self.segs:
-            for w0, n, s0 in pieces:
-                w[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
-            kb += c
-        cy = pad_to(cout, 32)  # the dgrad's K = the gradient slot width (32-channel granules)
+
+        def packed(segs):
+            w = torch.full((pad_to(cout, 128), taps, sum(c for c, _ in segs)), fill, dtype=torch.long)
+            kb = 0
+            for c, pieces in segs:
+                for w0, n, s0 in pieces:
+                    w[:cout, :, kb + s0:kb + s0 + n] = wt[:, :, w0:w0 + n]
+                kb += c
+            return w
+        ws = packed(self.segs)
+        w = ws if self.fsegs is self.segs else packed(self.fsegs)
+        # the dgrad's K = the gradient slot width (32-channel granules, or dk)
+        cy = self.dk or pad_to(cout, 32)
         wd = torch.full((pad_to(self.ktot, 128), taps, cy), fill, dtype=torch.long)
-        wd[:self.ktot] = w[:cy].flip(1).permute(2, 1, 0)
+        wd[:self.ktot] = ws[:cy].flip(1).permute(2, 1, 0)
         self.cy = cy
         wf = frag_weight(w) if frag and frag_eligible(w, kh, kw) else None
         wdf = frag_weight(wd) if frag and frag_eligible(wd, kh, kw) else None
@@ -144,20 +160,27 @@ class FusedTrainEngine:
         enc, g = ub.encoder, ub.gru
         full = lambda c: [(c, [(0, c, 0)])]
         self.small = bool(model.cfg.small)
+        # fp32 training (the reference's default precision): fp32 slots, split-bf16 kernels
+        self.f32 = not bool(model.cfg.mixed_precision)
+        self.spad = self.small and not self.f32 and _SMALL_KPAD
         if self.small:
             # RAFT-small (reference core/update.py SmallMotionEncoder / ConvGRU /
             # FlowHead(96, 128)): hx slot = [h 96 | inp 64 | motion 80 | flow 2 | 0 14]
             # = cat[h, x] of the ConvGRU in ONE 256-channel window
             self.hd, self.hx_c, self.corr_c, self.corr_pad = SHD, 256, SCORR_C, SCORR_PAD
-            self.c1 = _PConv(enc.convc1, [(SCORR_PAD, [(0, SCORR_C, 0)])])
+            dk = 128 if self.spad else None
+            self.c1 = _PConv(enc.convc1, [(SCORR_PAD, [(0, SCORR_C, 0)])], dk=dk)
             self.f2 = _PConv(enc.convf2, full(64))
-            self.cv = _PConv(enc.conv, full(128))
+            self.cv = _PConv(enc.conv, full(128), dk=dk)
             self.zr = [_PConv([g.convz, g.convr], [(256, [(0, SHD + 146, 0)])])]
-            # q reads [r*h | x]; its weight gradient reads 64-aligned windows
-            # (r*h slot zero-padded to 128, x from hx[64:256] with zero weights on h[64:96])
-            self.q = [_PConv(g.convq, [(SHD, [(0, SHD, 0)]), (160, [(SHD, 146, 0)])],
-                             wsegs=[(128, [(0, SHD, 0)]), (192, [(SHD, 146, 32)])])]
-            self.head = _PConv(ub.flow_head.conv1, full(SHD), wsegs=[(128, [(0, SHD, 0)])])
+            # q reads [r*h | x]; its weight gradient (and the padded bf16
+            # forward) reads 64-aligned windows (r*h slot zero-padded to 128,
+            # x from hx[64:256] with zero weights on h[64:96])
+            qw = [(128, [(0, SHD, 0)]), (192, [(SHD, 146, 32)])]
+            self.q = [_PConv(g.convq, [(SHD, [(0, SHD, 0)]), (160, [(SHD, 146, 0)])], wsegs=qw,
+                             fsegs=qw if self.spad else None, dk=dk)]
+            hw = [(128, [(0, SHD, 0)])]  # h' with inp[0:32] behind it (zero weights)
+            self.head = _PConv(ub.flow_head.conv1, full(SHD), wsegs=hw, fsegs=hw if self.spad else None)
             self.flow = _PConv(ub.flow_head.conv2, full(128))
             self.mask2 = None
             self.c2 = None
@@ -177,8 +200,6 @@ class FusedTrainEngine:
             self.convs = [self.c1, self.c2, self.f2, self.cv, *self.zr, *self.q, self.head, self.flow, self.mask2]
         self.f1 = enc.convf1
         self.f1c = self.f1.weight.shape[0]
-        # fp32 training (the reference's default precision): fp32 slots, split-bf16 kernels
-        self.f32 = not bool(model.cfg.mixed_precision)
         self.adt = torch.float32 if self.f32 else torch.bfloat16
         # parameter order handed to autograd (grads are returned in this order)
         self.params = []
@@ -433,7 +454,9 @@ class FusedTrainEngine:
                 head=e(n, 128), inp=e(B, 64),
                 C=torch.empty(n + B, 2, H, W, device=dev),
                 d_flow=torch.zeros(n, H, W, 64, device=dev, dtype=adt),  # 2 real
-                d_head=e(n, 128), d_zr=[e(n, 2 * SHD)], d_q=[e(n, SHD)], d_conv=e(n, 96), d_mot=e(n, 128),
+                # (padded K: d_q's channels 96:128 stay zero, relu_take zero-fills d_conv's 80:)
+                d_head=e(n, 128), d_zr=[e(n, 2 * SHD)], d_q=[z(n, 128) if self.spad else e(n, SHD)],
+                d_conv=e(n, 128 if self.spad else 96), d_mot=e(n, 128),
                 d_f1=e(n, 64), d_corr=e(n, SCORR_PAD),
                 G=torch.empty(B, H, W, 256, device=dev),
             )
@@ -850,10 +873,10 @@ def _small_forward(ctx, eng, corr_state, net, inp, coords0, coords1, iters, defe
         z, r, qq, rh = (sl(S[k][0], i) for k in ("z", "r", "q", "rh"))
         conv_fused([(hx, 0, 256)], zr.w, zr.b, 3, 3, 2 * hd, EPI_GRU_ZR, z, 0, hd=hd, out2=rh, out3=r,
                    aux1=hx, a1off=0)
-        conv_fused([(rh, 0, hd), (hx, hd, 160)], q.w, q.b, 3, 3, hd, EPI_GRU_Q, hx1, 0, out2=qq, aux1=hx,
-                   a1off=0, aux2=z)
+        qseg = [(rh, 0, 128), (hx, 64, 192)] if eng.spad else [(rh, 0, hd), (hx, hd, 160)]
+        conv_fused(qseg, q.w, q.b, 3, 3, hd, EPI_GRU_Q, hx1, 0, out2=qq, aux1=hx, a1off=0, aux2=z)
         head = sl(S["head"], i)
-        conv_fused([(hx1, 0, hd)], eng.head.w, eng.head.b, 3, 3, 128, EPI_RELU, head, 0)
+        conv_fused([(hx1, 0, 128 if eng.spad else hd)], eng.head.w, eng.head.b, 3, 3, 128, EPI_RELU, head, 0)
         R.flow_head(head, 0, 128, eng.flow_w32, eng.flow.b, sl(C, i + 1), coords)
     n = iters * B
     flows = (C[B:].view(iters, B, 2, H, W) - c0).view(n, 2, H, W)
@@ -904,19 +927,19 @@ def _small_backward(ctx, g_up):
         z, r, qq = sl(S["z"][0], i), sl(S["r"][0], i), sl(S["q"][0], i)
         dq, dzr = sl(S["d_q"][0], i), sl(S["d_zr"][0], i)
         R.gru_gate_bwd(G, z, qq, hx, 0, dq, dzr)
-        conv_fused([(dq, 0, hd)], q.wd, None, 3, 3, 256, EPI_GRU_QBWD, G, 0, hd=hd, out2=dzr, o2off=hd,
+        conv_fused([(dq, 0, q.cy)], q.wd, None, 3, 3, 256, EPI_GRU_QBWD, G, 0, hd=hd, out2=dzr, o2off=hd,
                    aux1=hx, a1off=0, aux2=r)
         conv_fused([(dzr, 0, 2 * hd)], zr.wd, None, 3, 3, 256, EPI_ACC_F32, G, 0)
         dcv, dmot = sl(S["d_conv"], i), sl(S["d_mot"], i)
         R.relu_take(G, 160, 80, 96, hx, 160, dcv)  # consumes d motion, drops d flow (coords detached)
-        conv_fused([(dcv, 0, 96)], eng.cv.wd, None, 3, 3, 128, EPI_RELU_BWD, dmot, 0, aux1=sl(S["mot"], i))
+        conv_fused([(dcv, 0, eng.cv.cy)], eng.cv.wd, None, 3, 3, 128, EPI_RELU_BWD, dmot, 0, aux1=sl(S["mot"], i))
         if side is not None:
             side.wait_stream(main)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             conv_fused([(dmot, 96, 32)], eng.f2.wd, None, 3, 3, 64, EPI_RELU_BWD, sl(S["d_f1"], i), 0,
                        aux1=sl(S["f1"], i))
         dcorr = sl(S["d_corr"], i)
-        conv_fused([(dmot, 0, hd)], eng.c1.wd, None, 1, 1, SCORR_PAD, EPI_BIAS, dcorr, 0)
+        conv_fused([(dmot, 0, eng.c1.cy)], eng.c1.wd, None, 1, 1, SCORR_PAD, EPI_BIAS, dcorr, 0)
         if lside is not None:
             lside.wait_stream(main)
         with torch.cuda.stream(lside) if lside is not None else contextlib.nullcontext():

@@ -142,14 +142,16 @@ def test_conv_v3_tiles_segment_offsets(cuda, tile):
 
 
 @pytest.mark.parametrize("cout", [256, 576, 70])
-@pytest.mark.parametrize("epi", [EPI_RELU, EPI_SCALE, EPI_RELU_BWD, EPI_ACC_F32])
+@pytest.mark.parametrize("epi", [EPI_BIAS, EPI_RELU, EPI_SCALE, EPI_RELU_BWD, EPI_ACC_F32])
 @pytest.mark.parametrize("shape", [(2, 11, 19), (1, 9, 70), (8, 46, 62)])
-def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape):
+@pytest.mark.parametrize("ooff", [0, 8])
+def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape, ooff):
     """csrc/conv_gemm1.hip (tile 70): two input segments read from windows of
     wider buffers, pixel counts that are not a multiple of the 128-pixel tile,
     Cout a multiple of 32 (batched epilogue) or not (element-wise epilogue),
-    the epilogue kinds the update block's 1x1 convs use; channels past the
-    output window untouched."""
+    the epilogue kinds the update block's 1x1 convs use (bias / ReLU / scale /
+    ReLU backward through the LDS-staged row stores when the output rows are
+    16-B aligned); channels outside the output window untouched."""
     torch.manual_seed(9)
     B, H, W = shape
     a_buf = torch.randn(B, H, W, 192, device=cuda).to(torch.bfloat16)
@@ -159,7 +161,7 @@ def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape):
     b = torch.randn(cout, device=cuda)
     wp = pack_weight(w, [(128, [(0, 128, 0)]), (256, [(128, 256, 0)])], pad_to(cout, 128))
     f32out = epi == EPI_ACC_F32
-    out0 = torch.randn(B, H, W, cout + 8, device=cuda)
+    out0 = torch.randn(B, H, W, cout + 16, device=cuda)
     out0 = out0 if f32out else out0.to(torch.bfloat16)
     out = out0.clone()
     aux = torch.randn(B, H, W, cout, device=cuda).to(torch.bfloat16)
@@ -167,7 +169,7 @@ def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape):
     if epi == EPI_RELU_BWD:
         kw_.update(aux1=aux, a1off=0)
     bias = None if epi in (EPI_RELU_BWD, EPI_ACC_F32) else pack_bias(b)
-    conv_fused([(a_buf, 64, 128), (b_buf, 0, 256)], wp, bias, 1, 1, cout, epi, out, 0, **kw_)
+    conv_fused([(a_buf, 64, 128), (b_buf, 0, 256)], wp, bias, 1, 1, cout, epi, out, ooff, **kw_)
     ref = F.conv2d(x, _bf(w), None if bias is None else b)
     if epi == EPI_RELU:
         ref = ref.relu()
@@ -176,10 +178,11 @@ def test_conv1x1_gemm_vs_conv2d(cuda, cout, epi, shape):
     elif epi == EPI_RELU_BWD:
         ref = ref * (aux.float().permute(0, 3, 1, 2) > 0)
     elif epi == EPI_ACC_F32:
-        ref = ref + out0[..., :cout].permute(0, 3, 1, 2)
-    got = out[..., :cout].float().permute(0, 3, 1, 2)
+        ref = ref + out0[..., ooff:ooff + cout].permute(0, 3, 1, 2)
+    got = out[..., ooff:ooff + cout].float().permute(0, 3, 1, 2)
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=2e-2)
-    assert torch.equal(out[..., cout:], out0[..., cout:])
+    assert torch.equal(out[..., :ooff], out0[..., :ooff])
+    assert torch.equal(out[..., ooff + cout:], out0[..., ooff + cout:])
 
 
 @pytest.mark.parametrize("epi", [EPI_GRU_ZR, EPI_GRU_Q, EPI_RELU_BWD, EPI_ACC_F32, EPI_GRU_QBWD, EPI_SCALE])
