@@ -662,6 +662,15 @@ def conv_norm(conv: nn.Conv2d, x: torch.Tensor, scale, shift, relu: bool, residu
 #   wgrad   : split-K MFMA over dY pixels with strided X rows
 _GEO = True
 _GEO_SCOPE = [True]  # per-encoder switch (geo_scope): off for RAFT-small's encoder (its narrow convs run on sconv)
+# ... except its convs with >= _WIDE_GEO input AND output channels (the 1x1
+# projection 96 -> 128 / 160 and layer 3's 64 -> 96 stride-2 shortcut): the
+# VALU weight gradient of the projection took 249 / 387 us per call
+# (profiles/r6/README.md); RS_WIDE_GEO=0 keeps every RAFT-small conv on sconv
+_WIDE_GEO = int(os.environ.get("RS_WIDE_GEO", "64"))
+
+
+def _wide(conv: nn.Conv2d) -> bool:
+    return _WIDE_GEO > 0 and conv.in_channels >= _WIDE_GEO and conv.out_channels >= _WIDE_GEO
 
 
 class geo_scope:
@@ -682,7 +691,8 @@ class geo_scope:
 
 
 def _geo_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    if not (_ENABLED and _GEO and _GEO_SCOPE[0]) or x.dtype != torch.bfloat16 or x.dim() != 4 or not _ext.use_hip(x):
+    if not (_ENABLED and _GEO and (_GEO_SCOPE[0] or _wide(conv))) or x.dtype != torch.bfloat16 or x.dim() != 4 \
+            or not _ext.use_hip(x):
         return False
     k, s, p = conv.kernel_size, conv.stride, conv.padding
     if conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros" or isinstance(p, str):
@@ -930,8 +940,8 @@ _SCONV = True
 def sconv_eligible(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:
     """Inside RAFT-small's encoder only (the scope where geo_scope(False) keeps
     the MFMA strided paths off): full RAFT's 64-128-channel convs stay on the
-    MFMA kernels."""
-    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x):
+    MFMA kernels (and so do RAFT-small's wide convs, :func:`_wide`)."""
+    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x) or _geo_ok(conv, x):
         return False
     if x.dtype not in (torch.bfloat16, torch.float32) or not x.is_contiguous(memory_format=_CL):
         return False
@@ -998,8 +1008,9 @@ _register_sconv_refresher()
 def sconv_train_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     """Training form of the narrow-channel path, inside RAFT-small's encoder
     (geo_scope(False)): forward and input gradient on csrc/sconv.hip, weight
-    gradient on csrc/sconv_train.hip.  bf16 under autocast or fp32 without it."""
-    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x):
+    gradient on csrc/sconv_train.hip.  bf16 under autocast or fp32 without it
+    (the wide convs go to the MFMA geometry path, :func:`_wide`)."""
+    if not (_ENABLED and _SCONV) or _GEO_SCOPE[0] or x.dim() != 4 or not _ext.use_hip(x) or _geo_ok(conv, x):
         return False
     if not torch.is_grad_enabled() or not (x.requires_grad or conv.weight.requires_grad):
         return False

@@ -278,6 +278,8 @@ def conv_norm_act(conv: nn.Conv2d, norm: nn.Module, x: torch.Tensor, relu: bool 
             # norm_fn 'none' context encoder): the bias as a separate add
             y = enc_conv.stem(conv, x)
             return norm_act(norm, y + conv.bias.to(y.dtype).view(1, -1, 1, 1), relu, residual)
+        if _ext.use_hip(x) and enc_conv.eligible_geo(conv, x):  # e.g. RAFT-small's wide shortcut ahead of norm_fn 'none'
+            return norm_act(norm, enc_conv.conv_geo(conv, x), relu, residual)
         return norm_act(norm, conv(x), relu, residual)
     if residual is None and enc_conv.stem_eligible(conv, x):  # the 7x7 / stride-2 stem (csrc/stem.hip)
         if isinstance(norm, nn.BatchNorm2d) and not norm.training and not (

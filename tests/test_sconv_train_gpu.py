@@ -16,7 +16,8 @@ CL = torch.channels_last
 @pytest.mark.parametrize("cin,cout,k,s", [(8, 8, 3, 1), (16, 16, 3, 2), (24, 24, 3, 2), (32, 16, 1, 1),
                                           (32, 64, 1, 2), (96, 160, 1, 1), (64, 24, 1, 1)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_sconv_train_fwd_bwd(cuda, cin, cout, k, s, dtype):
+def test_sconv_train_fwd_bwd(cuda, cin, cout, k, s, dtype, monkeypatch):
+    monkeypatch.setattr(enc_conv, "_WIDE_GEO", 0)  # the wide shapes too (RS_WIDE_GEO=0)
     torch.manual_seed(cin + cout + k + s)
     N, H, W = 3, 23, 37
     conv = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2).to(cuda)
@@ -47,3 +48,18 @@ def test_sconv_train_fwd_bwd(cuda, cin, cout, k, s, dtype):
     with enc_conv.geo_scope(False), torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
         enc_conv.sconv_train(conv, x).backward(g)
     assert torch.equal(conv.weight.grad, w1)
+
+
+@pytest.mark.parametrize("cin,cout,k,s", [(96, 160, 1, 1), (96, 128, 1, 1), (64, 96, 1, 2)])
+def test_wide_convs_leave_the_narrow_kernels(cuda, cin, cout, k, s):
+    """RAFT-small's projection and layer-3 shortcut (>= 64 channels in and out)
+    take the MFMA geometry path inside the narrow-kernel scope in bf16 (fp32
+    keeps sconv)."""
+    conv = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2).to(cuda)
+    x = torch.randn(2, cin, 16, 24, device=cuda).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    with enc_conv.geo_scope(False), torch.autocast("cuda", dtype=torch.bfloat16):
+        assert enc_conv.eligible_geo(conv, x)
+        assert not enc_conv.sconv_train_eligible(conv, x) and not enc_conv.sconv_eligible(conv, x)
+    xf = x.detach().float().contiguous(memory_format=CL).requires_grad_(True)
+    with enc_conv.geo_scope(False):
+        assert enc_conv.sconv_train_eligible(conv, xf) and not enc_conv.eligible_geo(conv, xf)
