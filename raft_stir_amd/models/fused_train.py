@@ -79,6 +79,10 @@ SCORR_PAD = 256
 # weight-streaming tiles (3x3) and the 1x1 GEMM serve them instead of the
 # 32-deep-K register tiles (inference does the same, models/fused_update.py)
 _SMALL_KPAD = os.environ.get("RS_SMALL_KPAD", "1") != "0"
+# the all-pairs volume backward issued by the engine right after the last
+# lookup backward, ahead of the weight-gradient issue (ops/corr.py
+# CorrState.early_backward); RS_EARLY_CORR_BWD=0 leaves it to autograd
+_EARLY_CORR_BWD = os.environ.get("RS_EARLY_CORR_BWD", "1") != "0"
 
 
 class _PConv:
@@ -730,6 +734,8 @@ class FusedTrainLoop(torch.autograd.Function):
             if otf is not None:
                 for g in d_otf:
                     g.record_stream(main)
+        if otf is None and _EARLY_CORR_BWD:
+            st.early_backward()
         if ctx.inp_dtype is None:  # adjoint of context_act: the raw context output's gradient, one pass
             d_net = R.context_act_backward(G, S["hx"][:B], S["inp"], HD).permute(0, 3, 1, 2).to(ctx.net_dtype)
             d_inp = None
@@ -958,6 +964,8 @@ def _small_backward(ctx, g_up):
         if otf is not None:
             for g in d_otf:
                 g.record_stream(main)
+    if otf is None and _EARLY_CORR_BWD:
+        st.early_backward()
     d_net = G[..., :hd].permute(0, 3, 1, 2).to(ctx.net_dtype)
     d_inp = G[..., hd:hd + 64].permute(0, 3, 1, 2).to(ctx.inp_dtype)
     grads = FusedTrainLoop._param_grads(ctx, _small_wgrads, S, C, B, H, W, n, main, side)
