@@ -1059,6 +1059,9 @@ bool conv_launch(const ConvLaunch& L, hipStream_t stream) {
 #undef RS_GEO
     return true;
   }
+  if (L.f32 && L.tile >= 81 && L.tile <= 83) {  // fp32 weight-streaming tiles (conv_v3f.hip)
+    return conv_v3f_launch(a, L.tile, stream);
+  }
   if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8, split-K 38-40 (host-checked)
 #define RS_F32(BM_, BN_, KG_)                                                                       \
   hipLaunchKernelGGL((conv::conv_lds_kernel<BM_, BN_, 2, 2, 64, false, true, KG_>),                \

@@ -69,16 +69,21 @@ struct Args {
 };
 
 // fp32 -> (hi, lo) bf16 pairs for 8 consecutive channels: hi = rne(x),
-// lo = rne(x - hi) (F32 tiles: x.w ~= xh.wh + xl.wh + xh.wl)
+// lo = rne(x - hi) (F32 tiles: x.w ~= xh.wh + xl.wh + xh.wl).  The packed
+// gfx950 conversion (v_cvt_pk_bf16_f32, RNE) and one v_pk_add_f32 per pair:
+// 5 VALU ops per 2 values instead of the integer rounding of f2bf
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
   const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t h[4], l[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const bf16_t h0 = f2bf(x[2 * i]), h1 = f2bf(x[2 * i + 1]);
-    const bf16_t l0 = f2bf(x[2 * i] - bf2f(h0)), l1 = f2bf(x[2 * i + 1] - bf2f(h1));
-    h[i] = uint32_t(h0) | (uint32_t(h1) << 16);
-    l[i] = uint32_t(l0) | (uint32_t(l1) << 16);
+    const f32x2v_t v = {x[2 * i], x[2 * i + 1]};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v_t));
+    const f32x2v_t hf = {__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+    h[i] = hu;
+    l[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v - hf, bf16x2v_t));
   }
   hi = make_uint4(h[0], h[1], h[2], h[3]);
   lo = make_uint4(l[0], l[1], l[2], l[3]);
@@ -869,4 +874,6 @@ __device__ __forceinline__ void epilogue32(const Args& a, const f32x16_t (&acc)[
 bool conv_v2_launch(const conv::Args& a, int tile, hipStream_t stream);
 // conv_v3.hip: tiles 60-68 (3x3 / 1x5 / 5x1; weights in the fragment-major layout, ops/conv.py frag_weight)
 bool conv_v3_launch(const conv::Args& a, int tile, hipStream_t stream);
+// conv_v3f.hip: tiles 81-83 (fp32 activations; split fragment-major weights, ops/conv.py frag_weight_split)
+bool conv_v3f_launch(const conv::Args& a, int tile, hipStream_t stream);
 }  // namespace rs

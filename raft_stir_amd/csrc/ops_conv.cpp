@@ -181,9 +181,11 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   // fp32 activations: the split-bf16 register-staged tiles (conv.hip conv_lds_kernel<..., F32>)
   const bool f32 = segs[0].scalar_type() == at::kFloat;
   const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
+  // tiles 81-83 (conv_v3f.hip): fp32 weight streaming, split fragment-major weights
+  const bool v3f = f32 && tile >= 81 && tile <= 83;
   if (f32) {
-    TORCH_CHECK(tile == 6 || tile == 7 || tile == 8 || (tile >= 38 && tile <= 40),
-                "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40 only");
+    TORCH_CHECK(tile == 6 || tile == 7 || tile == 8 || (tile >= 38 && tile <= 40) || v3f,
+                "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40, 81-83 only");
     TORCH_CHECK(epi != EPI_FLOW, "conv_fused: fp32 activations: no flow epilogue (csrc/flowhead.hip serves it)");
   }
   L.f32 = f32 ? 1 : 0;
@@ -212,7 +214,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   L.nseg = segs.size();
   TORCH_CHECK(KH >= 1 && KW >= 1 && KH % 2 == 1 && KW % 2 == 1, "conv_fused: odd kernel sizes only");
   TORCH_CHECK((tile >= 0 && tile <= 54) || tile == 56 || tile == 57 || tile == 61 || tile == 65 || tile == 66 ||
-                  tile == 68 || tile == 70,
+                  tile == 68 || tile == 70 || v3f,
               "conv_fused: tile must be in [0,54], 56, 57, 61, 65, 66, 68 or 70");
   if (tile == 70) {  // conv_gemm1.hip: 1x1 GEMM over 64-channel K chunks
     TORCH_CHECK(KH == 1 && KW == 1 && !f32, "conv_fused: tile 70 is the bf16 1x1 GEMM");
@@ -220,7 +222,12 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tile 70 needs segment channels % 64 == 0");
   }
   const bool v3 = tile >= 56 && tile <= 68;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
-  if ((tile >= 42 && tile <= 54) || v3)
+  if (v3f) {
+    for (size_t s = 0; s < segs.size(); ++s)
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 81-83 need segment channels % 64 == 0");
+    TORCH_CHECK(epi != EPI_NORM, "conv_fused: tiles 81-83 have no EPI_NORM epilogue");
+  }
+  if ((tile >= 42 && tile <= 54) || v3 || v3f)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
                 "conv_fused: tiles 42-68 are instantiated for 3x3, 1x5 and 5x1 kernels only");
   TORCH_CHECK(tile < 16 || KH * KW <= 32, "conv_fused: buffer-DMA tiles (16-37) support at most 32 taps");
@@ -247,9 +254,13 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
       TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: 64-deep-K tiles need segment channels % 64 == 0");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.dim() == 3,
               "conv_fused: packed weight must be contiguous bf16 (Cout_pad, taps, Ktot)");
-  TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == (f32 ? 2 : 1) * Ktot,
-              "conv_fused: packed weight K mismatch", f32 ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
-  if (v3) {  // fragment-major rows in 32-row blocks; blocks past the weight read as zeros
+  TORCH_CHECK(w.size(1) == KH * KW && w.size(2) == (f32 && !v3f ? 2 : 1) * Ktot,
+              "conv_fused: packed weight K mismatch", f32 && !v3f ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
+  if (v3f) {  // [frag(wh) ; frag(wl)]: two halves of round_up(Cout, 32)+ rows each
+    TORCH_CHECK(w.size(0) % 64 == 0 && w.size(0) / 2 >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
+                "conv_fused: tiles 81-83 need split fragment-major weights [frag(wh); frag(wl)] (ops/conv.py "
+                "frag_weight_split)");
+  } else if (v3) {  // fragment-major rows in 32-row blocks; blocks past the weight read as zeros
     TORCH_CHECK(w.size(0) % 32 == 0 && w.size(0) >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
                 "conv_fused: tiles 56-68 need fragment-major weights with round_up(Cout, 32) rows (< 2 GiB)");
   } else {

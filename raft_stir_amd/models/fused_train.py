@@ -64,8 +64,8 @@ import torch
 
 from ..ops import _ext
 from ..ops.conv import (EPI_ACC_F32, EPI_BIAS, EPI_FLOW, EPI_GRU_Q, EPI_GRU_QBWD, EPI_GRU_ZR, EPI_RELU,
-                        EPI_RELU_BWD, EPI_SCALE, conv_fused, frag_eligible, frag_weight, pack_bias, pack_weight,
-                        pad_to)
+                        EPI_RELU_BWD, EPI_SCALE, conv_fused, frag32_eligible, frag_eligible, frag_weight,
+                        frag_weight_split, pack_bias, pack_weight, pad_to)
 
 R = torch.ops.raft_stir
 HD = 128          # hidden dim (full RAFT)
@@ -83,6 +83,9 @@ _SMALL_KPAD = os.environ.get("RS_SMALL_KPAD", "1") != "0"
 # lookup backward, ahead of the weight-gradient issue (ops/corr.py
 # CorrState.early_backward); RS_EARLY_CORR_BWD=0 leaves it to autograd
 _EARLY_CORR_BWD = os.environ.get("RS_EARLY_CORR_BWD", "1") != "0"
+# fp32 engine: split fragment-major copies of the packed weights for the fp32
+# weight-streaming tiles (csrc/conv_v3f.hip), made per step after the gather
+_V3F_TRAIN = True
 
 
 class _PConv:
@@ -368,6 +371,10 @@ class FusedTrainEngine:
             n = wds.numel()
             pc.wd = bf[k * ob:k * (ob + n)].view(wds[0], wds[1], k * wds[2])
             ob += n
+            if self.f32 and _V3F_TRAIN:  # the fp32 weight-streaming tiles 81-83 read [frag(wh); frag(wl)]
+                for t in (pc.w, pc.wd):
+                    if frag32_eligible(t, pc.kh, pc.kw):
+                        t._rs_frag32 = frag_weight_split(t)
             # fragment-major copies (bf16 engine): conv_fused finds them through
             # the packed weight's _rs_frag attribute when a weight-streaming tile (56-68) is chosen
             pc.wf = pc.wdf = None

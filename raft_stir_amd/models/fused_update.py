@@ -46,7 +46,8 @@ import torch.nn.functional as F
 
 from ..ops import _ext
 from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, choose_tile_f32, conv_fused,
-                        frag_eligible, frag_weight, pack_bias, pack_weight, pack_weight_split, pad_to)
+                        frag32_eligible, frag_eligible, frag_weight, frag_weight_split, pack_bias, pack_weight,
+                        pack_weight_split, pad_to)
 
 _F32_ENGINE = True
 from ..ops.upsample import convex_upsample
@@ -71,12 +72,18 @@ class _Conv:
         pack = pack_weight_split if f32 else pack_weight
         self.w = pack(weight, segs, pad_to(self.cout, 128))
         self.b = pack_bias(bias)
-        # fragment-major copy for the weight-streaming tiles (bf16 3x3 / 1x5 / 5x1 only)
+        # fragment-major copy for the weight-streaming tiles (bf16 3x3 / 1x5 / 5x1 only;
+        # fp32: the split [frag(wh); frag(wl)] of tiles 81-83, on the split weight's _rs_frag32)
         self.wf = frag_weight(self.w) if not f32 and frag_eligible(self.w, self.kh, self.kw) else None
+        if f32 and frag32_eligible(self.w, self.kh, self.kw):
+            self.w._rs_frag32 = frag_weight_split(self.w)
 
 
 def _copy_conv(prev: "_Conv", new: "_Conv"):
     prev.w.copy_(new.w)
+    f_prev, f_new = getattr(prev.w, "_rs_frag32", None), getattr(new.w, "_rs_frag32", None)
+    if f_prev is not None and f_new is not None:
+        f_prev.copy_(f_new)
     prev.b.copy_(new.b)
     if prev.wf is not None and new.wf is not None:
         prev.wf.copy_(new.wf)

@@ -83,14 +83,40 @@ def frag_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 F32_TILES = (6, 7, 8)
+# csrc/conv_v3f.hip: the fp32 weight-streaming tiles (81 = 3 patch rows,
+# 82 = 1 row for batch-1 grids, 83 = 2 rows), fed by frag_weight_split
+V3F_TILES = (81, 82, 83)
 
 
-def choose_tile_f32(P: int, cout: int, geo: bool = False) -> int:
+@torch.no_grad()
+def frag_weight_split(w_split: torch.Tensor) -> torch.Tensor:
+    """The F32 tiles' split weight [Cout_pad][taps][2 Ktot] (per 32-channel
+    chunk [wh 32 | wl 32], :func:`split_weight`) -> [frag(wh) ; frag(wl)]
+    [2 Cout_pad][taps][Ktot]: the hi and lo fragment streams of the fp32
+    weight-streaming tiles 81-83, lo blocks after all hi blocks."""
+    cp, taps, k2 = w_split.shape
+    v = w_split.view(cp, taps, k2 // 64, 2, 32)
+    hi = v[:, :, :, 0].reshape(cp, taps, k2 // 2)
+    lo = v[:, :, :, 1].reshape(cp, taps, k2 // 2)
+    return torch.cat([frag_weight(hi), frag_weight(lo)], 0)
+
+
+def frag32_eligible(w_split: torch.Tensor, kh: int, kw: int) -> bool:
+    """Can the fp32 weight-streaming tiles 81-83 serve this split weight?"""
+    return kh * kw in (5, 9) and w_split.dim() == 3 and w_split.shape[0] % 32 == 0 and w_split.shape[2] % 128 == 0
+
+
+_V3F = os.environ.get("RS_V3F", "1") != "0"  # RS_V3F=0: the fp32 engines stay on the register tiles
+
+
+def choose_tile_f32(P: int, cout: int, geo: bool = False, v3f: bool = False) -> int:
     """Split-bf16 fp32 tile: 64x64 for narrow outputs / small grids, else
     128x64 (128x128 at large pixel counts).  Batch-1 grids (<= 768 64x64
     tiles: STIR 1x64x80, Sintel 1x55x136) take the intra-block split-K
     variants, 4 K groups (38) when the grid has at most one tile per CU, else
     2 (40): their register-staged K loop is load-latency bound there."""
+    if v3f and _V3F and not geo:  # split fragment-major weight available: the weight-streaming tiles
+        return 81 if P >= 16384 else 82
     nb64 = -(-P // 64) * -(-cout // 64)
     if nb64 <= 256 and not geo:  # (conv_geo's strided tiles have no split-K variant)
         return 38
@@ -225,7 +251,10 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
         key = tune_key(t0.shape[0], t0.shape[1], t0.shape[2], cout, chans, kh, kw, epi)
         P = t0.shape[0] * t0.shape[1] * t0.shape[2]
         if t0.dtype == torch.float32:  # split-bf16 F32 tiles: measured table, else the heuristic
-            tile = tuned_tiles_f32().get(key) or choose_tile_f32(P, cout)
+            tile = tuned_tiles_f32().get(key)
+            has32 = getattr(w, "_rs_frag32", None) is not None and all(c % 64 == 0 for c in chans)
+            if tile is None or (tile in V3F_TILES and not (has32 and _V3F)):
+                tile = choose_tile_f32(P, cout, v3f=has32)
         else:
             tile = tuned_tiles().get(key)
             if tile is None or (tile in V3_TILES and wf is None) or (tile == GEMM1_TILE and not gemm1_ok(
@@ -235,6 +264,12 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
         if wf is None:
             raise ValueError("conv_fused: tiles 56-68 read the fragment-major weight: pass wf=frag_weight(w)")
         w = wf
+    elif tile in V3F_TILES:
+        wf32 = getattr(w, "_rs_frag32", None)
+        if wf32 is None:
+            raise ValueError("conv_fused: tiles 81-83 read the split fragment-major weight: tag the split "
+                             "weight with _rs_frag32 = frag_weight_split(w)")
+        w = wf32
     if nscale is None:
         torch.ops.raft_stir.conv_fused(tensors, offs, chans, w, bias, kh, kw, cout, epi, float(scale), hd,
                                        out, ooff, out2, o2off, out3, o3off, aux1, a1off, aux2, a2off, tile)

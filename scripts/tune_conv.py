@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-F32_CANDIDATES = [6, 7, 8, 38, 39, 40]
+F32_CANDIDATES = [6, 7, 8, 38, 39, 40, 81, 82, 83]
 CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 42, 43,
               44, 45, 46, 48, 49, 50, 51, 52, 53, 54, 56, 57, 61, 65, 66, 68, 70]  # 56-68: calls that carry a wf weight; 70: 1x1
 
@@ -130,7 +130,8 @@ def main():
                 kw[k] = kw[k].clone()
         t_in = kw["segs"][0][0]
         if args.f32:
-            heur = C.choose_tile_f32(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"])
+            heur = C.choose_tile_f32(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"],
+                                     v3f=getattr(kw["w"], "_rs_frag32", None) is not None)
             cands = F32_CANDIDATES
         else:
             heur = C.choose_tile(t_in.shape[0] * t_in.shape[1] * t_in.shape[2], kw["cout"],
