@@ -107,9 +107,11 @@ __device__ __forceinline__ void ld4(const bf16_t* p, float (&f)[4]) {
   f[3] = bf2f((bf16_t)(u.y >> 16));
 }
 __device__ __forceinline__ void st4(bf16_t* p, const float (&f)[4]) {
-  uint2 pk;
-  pk.x = uint32_t(f2bf(f[0])) | (uint32_t(f2bf(f[1])) << 16);
-  pk.y = uint32_t(f2bf(f[2])) | (uint32_t(f2bf(f[3])) << 16);
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+  uint2 pk;  // two packed conversions (v_cvt_pk_bf16_f32)
+  pk.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t{f[0], f[1]}), b2_t));
+  pk.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2_t{f[2], f[3]}), b2_t));
   *reinterpret_cast<uint2*>(p) = pk;
 }
 __device__ __forceinline__ void acc4(float* p, const float (&f)[4]) {
