@@ -1059,7 +1059,7 @@ bool conv_launch(const ConvLaunch& L, hipStream_t stream) {
 #undef RS_GEO
     return true;
   }
-  if (L.f32 && L.tile >= 81 && L.tile <= 83) {  // fp32 weight-streaming tiles (conv_v3f.hip)
+  if (L.f32 && L.tile >= 81 && L.tile <= 85) {  // fp32 weight-streaming tiles (conv_v3f.hip)
     return conv_v3f_launch(a, L.tile, stream);
   }
   if (L.f32) {  // fp32 activations: split-bf16 register-staged tiles 6 / 7 / 8, split-K 38-40 (host-checked)

@@ -22,9 +22,12 @@
 //    split pass over the activations in memory and no second halo;
 //  * the fp32 epilogues of the F32 tiles (epi_frag_f32: bias / ReLU / scale,
 //    ConvGRU gates and update, ReLU backward, fp32 accumulation, the q-conv
-//    r-gate backward) on fp32 outputs.
+//    r-gate backward, eval-BN scale + shift (+ ReLU, + residual)) on fp32
+//    outputs.
 // Tiles: 81 = 4 waves x 3 patch rows (128 Cout x 96 px), 82 = 4 waves x 1 row
-// (batch-1 grids), 83 = 4 waves x 2 rows.
+// (batch-1 grids), 83 = 4 waves x 2 rows, 84 = 2 x 2 waves (64 Cout x 4 rows:
+// the 64-output encoder convs without a wasted half block), 85 = 84 with one
+// halo buffer (Ktot = 64 only).
 #include "conv_v3.h"
 
 namespace rs {
@@ -33,10 +36,11 @@ namespace conv {
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
-template <int KH, int KW, int NW, int THW, int RA>
+template <int KH, int KW, int NWM, int THW, int RA, int NWP, int SB>
 struct V3F {
   static constexpr int T = KH * KW, NSL = 4 * T, D = RA - 1;
-  static constexpr int TH = THW, TW = 32, BM = 32 * NW;
+  static constexpr int NW = NWM * NWP;  // waves: NWM along Cout x NWP along the patch rows
+  static constexpr int TH = THW * NWP, TW = 32, BM = 32 * NWM;
   static constexpr int HH = TH + KH - 1, HWD = TW + KW - 1;
   static constexpr int PS = 17;                      // 16-B slots per halo pixel (64 fp32 + 1 pad)
   static constexpr int PPR = (HWD * PS + 63) / 64;   // DMA pieces (1 KB) per halo row
@@ -46,8 +50,12 @@ struct V3F {
   static constexpr int HSL = NHPW * NW * 64;         // slots per halo buffer
   static constexpr int LASTP = NSL > RA ? NSL - RA : 1;
   static constexpr int PPP = (NHPW + LASTP - 1) / LASTP;
-  static constexpr int LDS_SLOTS = 2 * HSL;
+  // SB: ONE halo buffer (single-chunk convs, Ktot = 64: no next chunk to
+  // prefetch) -- half the LDS, so two blocks share a CU and one block's halo
+  // load overlaps the other's MFMAs
+  static constexpr int LDS_SLOTS = SB ? HSL : 2 * HSL;
   static constexpr int hcnt(int j) {
+    if (SB) return 0;  // no next-chunk halo pieces inside the slice loop
     j = ((j % NSL) + NSL) % NSL;
     if (j >= LASTP) return 0;
     const int n = NHPW - j * PPP;
@@ -87,7 +95,11 @@ __device__ __forceinline__ void epi32_f32(const Args& a, const f32x16_t (&acc)[N
       if (cb >= a.Cout) continue;
       float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[nb][4 * g + j] + (cb + j < a.Cout && a.bias ? a.bias[cb + j] : 0.f);
+      for (int j = 0; j < 4; ++j) {
+        const bool in = cb + j < a.Cout;
+        const float sc = (E == EPI_NORM && in) ? a.chs[cb + j] : 1.f;  // eval-BN scale (EPI_NORM)
+        v[j] = acc[nb][4 * g + j] * sc + (in && a.bias ? a.bias[cb + j] : 0.f);
+      }
       epi_frag_f32<E>(a, v, cb, pp[nb], vec);
     }
   }
@@ -109,15 +121,16 @@ __device__ __forceinline__ void epilogue32_f32(const Args& a, const f32x16_t (&a
     RS_E3(EPI_GRU_QBWD);
     RS_E3(EPI_RELU);
     RS_E3(EPI_SCALE);
+    RS_E3(EPI_NORM);
 #undef RS_E3
     default: epi32_f32<NB, EPI_BIAS>(a, acc, m0, lane, pp, pb, vec); break;
   }
 }
 
-template <int KH, int KW, int NW, int THW, int RA>
-__global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
-  using C = V3F<KH, KW, NW, THW, RA>;
-  constexpr int TH = C::TH, T = C::T, NSL = C::NSL, D = C::D, BM = C::BM;
+template <int KH, int KW, int NWM, int THW, int RA, int NWP = 1, int SB = 0>
+__global__ __launch_bounds__(64 * NWM * NWP) void conv_v3f_kernel(Args a) {
+  using C = V3F<KH, KW, NWM, THW, RA, NWP, SB>;
+  constexpr int NW = C::NW, TH = C::TH, T = C::T, NSL = C::NSL, D = C::D, BM = C::BM;
   constexpr int HWD = C::HWD, PS = C::PS, PPR = C::PPR, NHP = C::NHP, NHPW = C::NHPW, HSL = C::HSL;
   constexpr int ROWSL = C::ROWSL, PPP = C::PPP;
   constexpr int PH = KH / 2, PW = KW / 2;
@@ -130,6 +143,7 @@ __global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
 
   const int t_ = threadIdx.x, lane = t_ & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t_ >> 6);
+  const int cw = NWP == 1 ? wave : wave % NWM, pw = NWP == 1 ? 0 : wave / NWM;  // Cout slice, patch-row group
   const int H = a.H, W = a.W;
   const int ntx = cdiv(W, 32), npb = cdiv(H, TH) * ntx;
   const int nct = cdiv(a.Cout, BM);
@@ -152,7 +166,7 @@ __global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
 
   // ---- A: this wave's hi and lo fragment streams, 1 KB per slice each
   const i32x4_t rsA = raw_rsrc(a.w, a.w_bytes);
-  const int vA = ((bm0 >> 5) + wave) * NS * 1024 + lane * 16;
+  const int vA = ((bm0 >> 5) + cw) * NS * 1024 + lane * 16;
   const int loff = (int)(a.w_bytes >> 1);  // the lo blocks follow the hi blocks
 
   // ---- halo: piece q of this wave = slots g*64 .. +63 of a halo buffer, g = wave + NW q
@@ -191,7 +205,7 @@ __global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
   const int h = lane >> 5, l32 = lane & 31;
   uint32_t bro[THW];
 #pragma unroll
-  for (int nb = 0; nb < THW; ++nb) bro[nb] = lds0 + (uint32_t)((nb * ROWSL + l32 * PS + 2 * h) * 16);
+  for (int nb = 0; nb < THW; ++nb) bro[nb] = lds0 + (uint32_t)(((pw * THW + nb) * ROWSL + l32 * PS + 2 * h) * 16);
 
   f32x16_t acc[THW];
 #pragma unroll
@@ -311,7 +325,7 @@ __global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
   int pp[THW], pb[THW];
 #pragma unroll
   for (int nb = 0; nb < THW; ++nb) {
-    const int y = y0 + nb, x = x0 + l32;
+    const int y = y0 + pw * THW + nb, x = x0 + l32;
     if (y < H && x < W) {
       pb[nb] = img;
       pp[nb] = (img * H + y) * W + x;
@@ -320,19 +334,23 @@ __global__ __launch_bounds__(64 * NW) void conv_v3f_kernel(Args a) {
       pp[nb] = 0;
     }
   }
-  epilogue32_f32<THW>(a, acc, bm0 + wave * 32, lane, pp, pb);
+  epilogue32_f32<THW>(a, acc, bm0 + cw * 32, lane, pp, pb);
 }
 
 template <int KH, int KW>
 bool v3f_launch(const Args& a, int tile, hipStream_t stream) {
-  constexpr int NW = 4;
   constexpr int RA = KH * KW == 9 ? 9 : 10;  // ring slots: divide the 36 / 20 slices of a chunk
-  const int thw = tile == 81 ? 3 : (tile == 82 ? 1 : 2);
-  const dim3 grid(cdiv(a.Cout, 32 * NW) * a.B * cdiv(a.H, thw) * cdiv(a.W, 32));
+  // (waves along Cout, patch rows per wave, waves along the patch rows)
+  const bool t64 = tile == 84 || tile == 85;
+  const int nwm = t64 ? 2 : 4, thw = tile == 81 ? 3 : (tile == 82 ? 1 : 2), nwp = t64 ? 2 : 1;
+  const dim3 grid(cdiv(a.Cout, 32 * nwm) * a.B * cdiv(a.H, thw * nwp) * cdiv(a.W, 32));
+  const dim3 block(64 * nwm * nwp);
   switch (tile) {
-    case 81: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, NW, 3, RA>), grid, dim3(64 * NW), 0, stream, a); break;
-    case 82: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, NW, 1, RA>), grid, dim3(64 * NW), 0, stream, a); break;
-    case 83: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, NW, 2, RA>), grid, dim3(64 * NW), 0, stream, a); break;
+    case 81: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, 4, 3, RA>), grid, block, 0, stream, a); break;
+    case 82: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, 4, 1, RA>), grid, block, 0, stream, a); break;
+    case 83: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, 4, 2, RA>), grid, block, 0, stream, a); break;
+    case 84: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, 2, 2, RA, 2>), grid, block, 0, stream, a); break;
+    case 85: hipLaunchKernelGGL((conv_v3f_kernel<KH, KW, 2, 2, RA, 2, 1>), grid, block, 0, stream, a); break;
     default: return false;
   }
   return true;

@@ -181,11 +181,11 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   // fp32 activations: the split-bf16 register-staged tiles (conv.hip conv_lds_kernel<..., F32>)
   const bool f32 = segs[0].scalar_type() == at::kFloat;
   const at::ScalarType adt = f32 ? at::kFloat : at::kBFloat16;
-  // tiles 81-83 (conv_v3f.hip): fp32 weight streaming, split fragment-major weights
-  const bool v3f = f32 && tile >= 81 && tile <= 83;
+  // tiles 81-84 (conv_v3f.hip): fp32 weight streaming, split fragment-major weights
+  const bool v3f = f32 && tile >= 81 && tile <= 85;
   if (f32) {
     TORCH_CHECK(tile == 6 || tile == 7 || tile == 8 || (tile >= 38 && tile <= 40) || v3f,
-                "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40, 81-83 only");
+                "conv_fused: fp32 activations run on tiles 6, 7, 8, 38-40, 81-85 only");
     TORCH_CHECK(epi != EPI_FLOW, "conv_fused: fp32 activations: no flow epilogue (csrc/flowhead.hip serves it)");
   }
   L.f32 = f32 ? 1 : 0;
@@ -224,8 +224,8 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   const bool v3 = tile >= 56 && tile <= 68;  // conv_v3.hip: fragment-major weights (ops/conv.py frag_weight)
   if (v3f) {
     for (size_t s = 0; s < segs.size(); ++s)
-      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 81-83 need segment channels % 64 == 0");
-    TORCH_CHECK(epi != EPI_NORM, "conv_fused: tiles 81-83 have no EPI_NORM epilogue");
+      TORCH_CHECK(seg_C[s] % 64 == 0, "conv_fused: tiles 81-85 need segment channels % 64 == 0");
+    TORCH_CHECK(tile != 85 || Ktot == 64, "conv_fused: tile 85 (one halo buffer) needs exactly one 64-channel K chunk");
   }
   if ((tile >= 42 && tile <= 54) || v3 || v3f)
     TORCH_CHECK((KH == 3 && KW == 3) || (KH == 1 && KW == 5) || (KH == 5 && KW == 1),
@@ -258,7 +258,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
               "conv_fused: packed weight K mismatch", f32 && !v3f ? " (fp32: split [wh | wl] weights, 2 x Ktot)" : "");
   if (v3f) {  // [frag(wh) ; frag(wl)]: two halves of round_up(Cout, 32)+ rows each
     TORCH_CHECK(w.size(0) % 64 == 0 && w.size(0) / 2 >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
-                "conv_fused: tiles 81-83 need split fragment-major weights [frag(wh); frag(wl)] (ops/conv.py "
+                "conv_fused: tiles 81-85 need split fragment-major weights [frag(wh); frag(wl)] (ops/conv.py "
                 "frag_weight_split)");
   } else if (v3) {  // fragment-major rows in 32-row blocks; blocks past the weight read as zeros
     TORCH_CHECK(w.size(0) % 32 == 0 && w.size(0) >= (Cout + 31) / 32 * 32 && w.numel() * 2 < (int64_t(1) << 31),
@@ -329,7 +329,7 @@ void conv_impl(const std::vector<Tensor>& segs, at::IntArrayRef seg_off, at::Int
   }
   TORCH_CHECK(epi >= 0 && epi <= EPI_NORM, "conv_fused: unknown epilogue kind");
   if (nx.chs)
-    TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3 && tile != 70,
+    TORCH_CHECK(!(tile >= 42 && tile <= 54) && !v3 && tile != 70 && (!(tile >= 81 && tile <= 85) || f32),
                 "conv_fused: EPI_NORM needs a tile with the shared epilogue (not 42-70)");
   L.chs = nx.chs;
   TORCH_CHECK(rs::conv_launch(L, stream()), "conv_fused: tile ", L.tile, " is not instantiated for a ", KH, "x", KW,

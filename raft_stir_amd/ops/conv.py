@@ -84,8 +84,9 @@ def frag_weight(w: torch.Tensor) -> torch.Tensor:
 
 F32_TILES = (6, 7, 8)
 # csrc/conv_v3f.hip: the fp32 weight-streaming tiles (81 = 3 patch rows,
-# 82 = 1 row for batch-1 grids, 83 = 2 rows), fed by frag_weight_split
-V3F_TILES = (81, 82, 83)
+# 82 = 1 row for batch-1 grids, 83 = 2 rows, 84 = 64 Cout x 4 rows, 85 = 84
+# with one halo buffer for Ktot = 64), fed by frag_weight_split
+V3F_TILES = (81, 82, 83, 84, 85)
 
 
 @torch.no_grad()
@@ -109,7 +110,7 @@ def frag32_eligible(w_split: torch.Tensor, kh: int, kw: int) -> bool:
 _V3F = os.environ.get("RS_V3F", "1") != "0"  # RS_V3F=0: the fp32 engines stay on the register tiles
 
 
-def choose_tile_f32(P: int, cout: int, geo: bool = False, v3f: bool = False, taps: int = 9) -> int:
+def choose_tile_f32(P: int, cout: int, geo: bool = False, v3f: bool = False, taps: int = 9, ktot: int = 0) -> int:
     """Split-bf16 fp32 tile: 64x64 for narrow outputs / small grids, else
     128x64 (128x128 at large pixel counts).  Batch-1 grids (<= 768 64x64
     tiles: STIR 1x64x80, Sintel 1x55x136) take the intra-block split-K
@@ -118,6 +119,8 @@ def choose_tile_f32(P: int, cout: int, geo: bool = False, v3f: bool = False, tap
     if v3f and _V3F and not geo:  # split fragment-major weight available: the weight-streaming tiles
         # (training shape, scripts/bench_v3f.py: 3x3 on 2 patch rows 78-91 us, 1x5 / 5x1 on 3 rows 71-91 us)
         if P >= 16384:
+            if cout <= 64:
+                return 85 if ktot == 64 else 84
             return 83 if taps == 9 else 81
         return 82
     nb64 = -(-P // 64) * -(-cout // 64)
@@ -257,7 +260,7 @@ def conv_fused(segs: List[Tuple[torch.Tensor, int, int]], w, bias, kh, kw, cout,
             tile = tuned_tiles_f32().get(key)
             has32 = getattr(w, "_rs_frag32", None) is not None and all(c % 64 == 0 for c in chans)
             if tile is None or (tile in V3F_TILES and not (has32 and _V3F)):
-                tile = choose_tile_f32(P, cout, v3f=has32, taps=kh * kw)
+                tile = choose_tile_f32(P, cout, v3f=has32, taps=kh * kw, ktot=sum(chans))
         else:
             tile = tuned_tiles().get(key)
             if tile is None or (tile in V3_TILES and wf is None) or (tile == GEMM1_TILE and not gemm1_ok(

@@ -27,7 +27,8 @@ import torch
 import torch.nn as nn
 
 from . import _ext, wpack
-from .conv import EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag_weight, pack_weight, pad_to
+from .conv import (EPI_BIAS, EPI_NORM, choose_tile_f32, conv_fused, frag32_eligible, frag_weight, frag_weight_split,
+                   pack_weight, pad_to)
 
 _ENABLED = os.environ.get("RS_ENC_CONV", "1") != "0"
 _CL = torch.channels_last
@@ -441,6 +442,23 @@ def _split_weight(weight: torch.Tensor) -> torch.Tensor:
         ws[0], [(cin, [(0, cin, 0)])], pad_to(cout, 128), _F32))
 
 
+# stride-1 3x3 fp32 convs (forward and input gradient) on the fp32
+# weight-streaming tiles (csrc/conv_v3f.hip): the split weight is tagged with
+# its [frag(wh); frag(wl)] copy, recomputed at every call from the registry's
+# current split weight (a few small permute kernels; the registry refreshes
+# the split weight in place, so a cached copy could go stale)
+_V3F_ENC = True
+
+
+def _tag_frag32(ws: torch.Tensor, cin: int, cout: int) -> torch.Tensor:
+    # whole output blocks only: 128-output convs on tiles 81-83, 64-output ones
+    # on tile 84 (on the 128-row tiles half the block was wasted: 276 us per
+    # call vs 373 on the register tile 6, gpurun_out/r6s27)
+    if _V3F_ENC and cin % 64 == 0 and cout % 64 == 0 and frag32_eligible(ws, 3, 3):
+        ws._rs_frag32 = frag_weight_split(ws)
+    return ws
+
+
 def eligible_f32(conv: nn.Conv2d, x: torch.Tensor, residual=None) -> bool:
     """fp32 inference conv on the F32 tiles: 3x3 (stride 1 / 2, pad 1) or 1x1
     (stride 1 / 2), channel counts multiples of 32, nothing to differentiate."""
@@ -481,6 +499,7 @@ def conv_f32(conv: nn.Conv2d, x: torch.Tensor, bias: bool = True, scale=None, sh
     if stride == (1, 1) and (kh, kw) == (3, 3):
         out = torch.empty(N, H, W, cout, device=x.device, dtype=torch.float32)
         rn = _nhwc(residual) if residual is not None else None
+        wp = _tag_frag32(wp, cin, cout)
         conv_fused([(xn, 0, cin)], wp, b, 3, 3, cout, EPI_NORM if norm else EPI_BIAS, out, 0,
                    hd=int(bool(relu)), aux1=rn, tile=None, nscale=scale)
         return out.permute(0, 3, 1, 2)
@@ -586,8 +605,8 @@ class _ConvF32(torch.autograd.Function):
             if conv.kernel_size == (3, 3) and conv.stride == (1, 1):
                 N, H, W, cout = dyn.shape
                 dxn = torch.empty(N, H, W, conv.in_channels, device=dy.device, dtype=torch.float32)
-                conv_fused([(dyn, 0, cout)], _split_dgrad_weight(conv.weight), None, 3, 3, conv.in_channels,
-                           EPI_BIAS, dxn, 0, tile=None)
+                wd = _tag_frag32(_split_dgrad_weight(conv.weight), cout, conv.in_channels)
+                conv_fused([(dyn, 0, cout)], wd, None, 3, 3, conv.in_channels, EPI_BIAS, dxn, 0, tile=None)
                 dx = dxn.permute(0, 3, 1, 2)
             else:
                 dx = _conv_geo_dgrad([dyn], [conv.weight], x.shape, tuple(conv.stride), tuple(conv.padding),

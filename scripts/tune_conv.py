@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-F32_CANDIDATES = [6, 7, 8, 38, 39, 40, 81, 82, 83]
+F32_CANDIDATES = [6, 7, 8, 38, 39, 40, 81, 82, 83, 84, 85]
 CANDIDATES = [3, 4, 6, 7, 16, 17, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 42, 43,
               44, 45, 46, 48, 49, 50, 51, 52, 53, 54, 56, 57, 61, 65, 66, 68, 70]  # 56-68: calls that carry a wf weight; 70: 1x1
 

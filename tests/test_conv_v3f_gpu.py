@@ -15,12 +15,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("k", [(3, 3), (1, 5), (5, 1)])
-@pytest.mark.parametrize("tile", V3F_TILES)
+@pytest.mark.parametrize("tile", [t for t in V3F_TILES if t != 85])  # (85: Ktot = 64 only, below)
 @pytest.mark.parametrize("shape", [(2, 13, 37), (1, 9, 70)])
-def test_v3f_matches_fp64_conv(cuda, k, tile, shape):
+@pytest.mark.parametrize("cout", [160, 64])
+def test_v3f_matches_fp64_conv(cuda, k, tile, shape, cout):
     torch.manual_seed(k[0] * 10 + tile)
     B, H, W = shape
-    cout = 160
     x0 = torch.randn(B, H, W, 128, device=cuda)
     x1 = torch.randn(B, H, W, 64, device=cuda)
     w = torch.randn(cout, 192, *k, device=cuda) * 0.05
@@ -71,3 +71,45 @@ def test_v3f_epilogues_match_f32_tile(cuda, epi):
         outs.append((out, out2, out3))
     for x, y in zip(*outs):
         torch.testing.assert_close(y, x, atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("relu,use_res", [(False, False), (True, False), (True, True)])
+def test_v3f_eval_bn_epilogue_matches_f32_tile(cuda, relu, use_res):
+    """EPI_NORM (eval BatchNorm folded: acc * scale + shift, ReLU, + residual):
+    the fp32 inference encoders' stride-1 3x3 convs."""
+    from raft_stir_amd.ops.conv import EPI_NORM
+    torch.manual_seed(3)
+    B, H, W, cin, cout = 2, 21, 45, 64, 96
+    x = torch.randn(B, H, W, cin, device=cuda)
+    w = torch.randn(cout, cin, 3, 3, device=cuda) * 0.05
+    ws = pack_weight_split(w, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
+    ws._rs_frag32 = frag_weight_split(ws)
+    scale = torch.rand(cout, device=cuda) + 0.5
+    shift = torch.randn(cout, device=cuda) * 0.1
+    res = torch.randn(B, H, W, cout, device=cuda) if use_res else None
+    outs = []
+    for tile in (7, 81):
+        out = torch.empty(B, H, W, cout, device=cuda)
+        conv_fused([(x, 0, cin)], ws, shift, 3, 3, cout, EPI_NORM, out, 0, hd=int(relu), aux1=res, tile=tile,
+                   nscale=scale)
+        outs.append(out)
+    torch.testing.assert_close(outs[1], outs[0], atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("k", [(3, 3), (1, 5), (5, 1)])
+def test_v3f_single_buffer_tile(cuda, k):
+    """Tile 85 (one halo buffer, Ktot = 64) against tile 84 and an fp64 conv."""
+    torch.manual_seed(11)
+    B, H, W, cin, cout = 2, 29, 70, 64, 64
+    x = torch.randn(B, H, W, cin, device=cuda)
+    w = torch.randn(cout, cin, *k, device=cuda) * 0.05
+    ws = pack_weight_split(w, [(cin, [(0, cin, 0)])], pad_to(cout, 128))
+    ws._rs_frag32 = frag_weight_split(ws)
+    outs = []
+    for tile in (84, 85):
+        out = torch.empty(B, H, W, cout, device=cuda)
+        conv_fused([(x, 0, cin)], ws, None, k[0], k[1], cout, EPI_BIAS, out, 0, tile=tile)
+        outs.append(out)
+    torch.testing.assert_close(outs[1], outs[0], atol=0, rtol=0)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.double(), padding=(k[0] // 2, k[1] // 2)).permute(0, 2, 3, 1)
+    assert ((outs[1].double() - ref).norm() / ref.norm()).item() < 2e-5
