@@ -41,6 +41,8 @@ lookup / upsampling in their fp32 forms.
 from __future__ import annotations
 
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -50,6 +52,9 @@ from ..ops.conv import (EPI_FLOW, EPI_GRU_Q, EPI_GRU_ZR, EPI_RELU, EPI_SCALE, ch
                         pack_weight_split, pad_to)
 
 _F32_ENGINE = True
+# RAFT-small inference: the flow branch on the side stream as well (RS_SMALL_SIDE=0 to
+# compare; 1.914-1.941 -> 1.848-1.900 ms per 1088x436 pair, profiles/r6/ab_small_side_s30.txt)
+_SMALL_SIDE = os.environ.get("RS_SMALL_SIDE", "1") == "1"
 from ..ops.upsample import convex_upsample
 
 
@@ -254,15 +259,20 @@ class FusedUpdate:
         # of these convs fills only part of the 256 CUs.  Both write disjoint
         # channel ranges of `mot`; joined before the conv that reads it.
         main = torch.cuda.current_stream(coords1.device)
-        side = self.model._side_stream(coords1.device) if (not small and self.model.cfg.overlap_encoders) else None
+        side = (self.model._side_stream(coords1.device)
+                if ((not small or _SMALL_SIDE) and self.model.cfg.overlap_encoders) else None)
         for itr in range(iters):
             want_up = (not test_mode) or itr == iters - 1
             if side is not None:
                 side.wait_stream(main)  # coords1 of the previous iteration
                 with torch.cuda.stream(side):
                     torch.ops.raft_stir.flow_encode(coords1, self.f1_w, self.f1_b, bufs["f1"], 0, hx, self.off_flow)
-                    cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
-                               bufs["mot"], 192, wf=self.convf2.wf)
+                    if small:
+                        cf([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
+                           bufs["mot"], 96, wf=self.convf2.wf)
+                    else:
+                        cf([(bufs["f1"], 0, 128)], self.convf2.w, self.convf2.b, 3, 3, 64, EPI_RELU,
+                           bufs["mot"], 192, wf=self.convf2.wf)
             if st is not None:
                 torch.ops.raft_stir.corr_lookup_into(st.pyr, coords1, st.radius, bufs["corr"])
             else:  # memory-efficient path: correlate the pooled fmap2 pyramid on the fly
@@ -275,8 +285,11 @@ class FusedUpdate:
             if small:
                 cf([(bufs["corr"], 0, cp)], self.convc1.w, self.convc1.b, 1, 1, 96, EPI_RELU,
                            bufs["mot"], 0)
-                cf([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
-                           bufs["mot"], 96, wf=self.convf2.wf)
+                if side is None:
+                    cf([(bufs["f1"], 0, 64)], self.convf2.w, self.convf2.b, 3, 3, 32, EPI_RELU,
+                       bufs["mot"], 96, wf=self.convf2.wf)
+                else:
+                    main.wait_stream(side)
                 cf([(bufs["mot"], 0, 128)], self.conv.w, self.conv.b, 3, 3, 80, EPI_RELU,
                            hx, self.off_mot, wf=self.conv.wf)
             else:
