@@ -53,8 +53,11 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager inference instead of hipGraph")
     ap.add_argument("--train-graph", action="store_true",
                     help="one GPU: replay the whole training step (forward, loss, backward, clip, AdamW) "
-                         "from one hipGraph (runtime/graph.py GraphedTrainStep).  Measured slower than the "
-                         "eager step (357 vs 390 pairs/s, profiles/r4/ab_train_graph_s27.txt), so off by default")
+                         "from one hipGraph (runtime/graph.py GraphedTrainStep).  Full RAFT: no faster than "
+                         "the GPU-bound eager step, so off; RAFT-small (bf16, all-pairs, one GPU): on by "
+                         "default -- its eager step is host-bound (host issue 11.5 ms = GPU 11.5 ms, "
+                         "626-763 pairs/s run to run vs 748-750 replayed, profiles/r6/ab_small_graph_s32.txt)")
+    ap.add_argument("--eager", action="store_true", help="force the eager training step")
     ap.add_argument("--corr-dtype", default="auto", choices=["auto", "float32", "bfloat16"],
                     help="all-pairs pyramid storage; auto = bf16 under bf16 autocast (EPE-drift gate: "
                          "tests/test_model_gpu.py::test_bf16_pyramid_epe_drift)")
@@ -124,7 +127,8 @@ def main():
     if not cpu:
         model = model.to(memory_format=torch.channels_last)
     model.train()
-    use_graph = a.train_graph and not cpu and not a.reference_ops
+    auto_graph = a.small and not a.fp32 and not a.alternate_corr and a.gpus == 1
+    use_graph = (a.train_graph or auto_graph) and not a.eager and not cpu and not a.reference_ops
     if use_graph and info.world_size > 1:
         raise SystemExit("bench.py: --train-graph is one-GPU only (multi-GPU steps run eager under DDP)")
     targs = argparse.Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000)

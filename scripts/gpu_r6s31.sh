@@ -1,0 +1,13 @@
+set -o pipefail
+OUT=gpurun_out/r6s31
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
+cp raft_stir_amd/conv_tuning.json $OUT/conv_tuning.json
+timeout -k 10 900 python -u scripts/tune_conv.py --small --merge --out $OUT/conv_tuning.json > $OUT/tune_small.log 2>&1 || { tail -30 $OUT/tune_small.log; exit 1; }
+tail -2 $OUT/tune_small.log
+for r in 1 2; do
+timeout -k 10 300 python bench.py --small --steps 40 --warmup 5 --infer-reps 40 > $OUT/b_old.$r.log 2>&1 || { tail -20 $OUT/b_old.$r.log; exit 1; }
+tail -1 $OUT/b_old.$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("old table", d["value"], d["ms_per_step"], d["inference"]["ms_per_pair"])'
+RS_CONV_TUNING_FILE=$OUT/conv_tuning.json timeout -k 10 300 python bench.py --small --steps 40 --warmup 5 --infer-reps 40 > $OUT/b_new.$r.log 2>&1 || { tail -20 $OUT/b_new.$r.log; exit 1; }
+tail -1 $OUT/b_new.$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("new table", d["value"], d["ms_per_step"], d["inference"]["ms_per_pair"])'
+done

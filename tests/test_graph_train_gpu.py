@@ -26,7 +26,8 @@ from raft_stir_amd.train.optim import fetch_optimizer
 from raft_stir_amd.runtime.graph import GraphedTrainStep
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
-m_e = RAFT(make_args(mixed_precision=True)).to(dev).to(memory_format=torch.channels_last).train()
+m_e = RAFT(make_args(mixed_precision=True, small=os.environ.get("SMALL") == "1")).to(dev).to(
+    memory_format=torch.channels_last).train()
 m_g = copy.deepcopy(m_e)
 targs = argparse.Namespace(lr=2e-4, wdecay=1e-4, epsilon=1e-8, num_steps=1000)
 loss_fn = lambda p, f, v: sequence_loss(p, f, v, gamma=0.8, sync_metrics=False)[0]
@@ -74,10 +75,11 @@ print("EVALDIFF", float((a - bb).abs().max()), float(bb.abs().max()))
 '''
 
 
-def test_graphed_train_step_tracks_eager(cuda, tmp_path):
+@pytest.mark.parametrize("small", [False, True])  # (RAFT-small: bench.py's default training step)
+def test_graphed_train_step_tracks_eager(cuda, tmp_path, small):
     script = tmp_path / "g.py"
     script.write_text(WORKER)
-    env = dict(os.environ, ROOT=ROOT)
+    env = dict(os.environ, ROOT=ROOT, SMALL="1" if small else "0")
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("LOSSES")][-1]
