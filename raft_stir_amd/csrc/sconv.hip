@@ -90,9 +90,12 @@ __global__ __launch_bounds__(256) void sconv_kernel(SArgs a) {
   const int b = p / (a.Ho * a.Wo), q = p - b * a.Ho * a.Wo;
   const int oy = q / a.Wo, ox = q - oy * a.Wo;
   const float* wg = ws + wave * 8 * K;            // [8 co][K]
-  float acc[8];
+  // even / odd input-channel partial sums per output channel: the 64 FMAs of
+  // an 8-channel step as 32 packed v_pk_fma_f32 (two fp32 FMAs per lane per issue)
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  f2_t acc2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int j = 0; j < 8; ++j) acc2[j] = f2_t{0.f, 0.f};
   const T* x = static_cast<const T*>(a.x);
   for (int ky = 0; ky < a.KH; ++ky) {
     const int iy = oy * a.S + ky - a.P;
@@ -110,18 +113,17 @@ __global__ __launch_bounds__(256) void sconv_kernel(SArgs a) {
           // same address in every lane: LDS broadcast; 32-B aligned (K, Cin, c0 % 8 == 0)
           const float4* wr = reinterpret_cast<const float4*>(wt + j * K + c0);
           const float4 w0 = wr[0], w1 = wr[1];
-          acc[j] = fmaf(v[0], w0.x, acc[j]);
-          acc[j] = fmaf(v[1], w0.y, acc[j]);
-          acc[j] = fmaf(v[2], w0.z, acc[j]);
-          acc[j] = fmaf(v[3], w0.w, acc[j]);
-          acc[j] = fmaf(v[4], w1.x, acc[j]);
-          acc[j] = fmaf(v[5], w1.y, acc[j]);
-          acc[j] = fmaf(v[6], w1.z, acc[j]);
-          acc[j] = fmaf(v[7], w1.w, acc[j]);
+          acc2[j] = __builtin_elementwise_fma(f2_t{v[0], v[1]}, f2_t{w0.x, w0.y}, acc2[j]);
+          acc2[j] = __builtin_elementwise_fma(f2_t{v[2], v[3]}, f2_t{w0.z, w0.w}, acc2[j]);
+          acc2[j] = __builtin_elementwise_fma(f2_t{v[4], v[5]}, f2_t{w1.x, w1.y}, acc2[j]);
+          acc2[j] = __builtin_elementwise_fma(f2_t{v[6], v[7]}, f2_t{w1.z, w1.w}, acc2[j]);
         }
       }
     }
   }
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = acc2[j].x + acc2[j].y;
   const int co = (cg0 + wave) * 8;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {

@@ -77,8 +77,11 @@ __device__ __forceinline__ void ld4<float>(const float* p, float (&v)[4]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 // thread tile: 4 output channels x 8 input channels of one tap (32 accumulators;
-// per pixel one 8-B dY load, one 16-B input load, 32 FMAs)
+// per pixel one 8-B dY load, one 16-B input load, 32 FMAs as 16 packed
+// v_pk_fma_f32 -- two fp32 FMAs per lane per issue)
 template <typename T>
 __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
   __shared__ float red[THREADS * 8];
@@ -97,11 +100,11 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
   float* out = a.part + (size_t)blockIdx.x * OUT;
   for (int g0 = 0; g0 < ng_all; g0 += NG) {
     const int g = g0 + gi;
-    float acc[4][8];
+    f32x2_t acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x2_t{0.f, 0.f};
     int co0 = 0, tap = 0, c8 = 0;
     if (g < ng_all) {
       c8 = g % C8;
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(d[i], v[j], acc[i][j]);
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_elementwise_fma(f32x2_t{d[i], d[i]}, f32x2_t{v[2 * j], v[2 * j + 1]}, acc[i][j]);
         }
       }
     }
@@ -134,7 +138,10 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[t * 8 + j] = acc[i][j];
+      for (int j = 0; j < 4; ++j) {
+        red[t * 8 + 2 * j] = acc[i][j].x;
+        red[t * 8 + 2 * j + 1] = acc[i][j].y;
+      }
       __syncthreads();
       if (sl == 0 && g < ng_all) {
         float s[8];
