@@ -16,6 +16,8 @@
 //  * sub-lane sums combined in LDS in a fixed order, one fp32 partial row per
 //    block; sconv_wgrad_reduce_kernel adds the blocks in a fixed order
 //    (deterministic).
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "common.h"
@@ -79,15 +81,16 @@ __device__ __forceinline__ void ld4<float>(const float* p, float (&v)[4]) {
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-// thread tile: 4 output channels x 8 input channels of one tap (32 accumulators;
-// per pixel one 8-B dY load, one 16-B input load, 32 FMAs as 16 packed
-// v_pk_fma_f32 -- two fp32 FMAs per lane per issue)
-template <typename T>
+// thread tile: CO (4 or 8) output channels x 8 input channels of one tap
+// (8 CO accumulators; per pixel one 2*CO-B dY load, one 16-B input load,
+// 8 CO FMAs as packed v_pk_fma_f32 -- two fp32 FMAs per lane per issue; CO = 8
+// halves the loads per FMA of this load-bound reduction)
+template <typename T, int CO>
 __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
   __shared__ float red[THREADS * 8];
   const int t = threadIdx.x;
-  const int T_ = a.KH * a.KW, C8 = a.Cin / 8, O4 = a.Cout / 4;
-  const int ng_all = O4 * T_ * C8;               // 32-output groups
+  const int T_ = a.KH * a.KW, C8 = a.Cin / 8, O4 = a.Cout / CO;
+  const int ng_all = O4 * T_ * C8;               // 8*CO-output groups
   const int NG = ng_all < THREADS ? ng_all : THREADS;
   const int SL = THREADS / NG;                   // pixel sub-lanes per group
   const int gi = t % NG, sl = t / NG;
@@ -100,9 +103,9 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
   float* out = a.part + (size_t)blockIdx.x * OUT;
   for (int g0 = 0; g0 < ng_all; g0 += NG) {
     const int g = g0 + gi;
-    f32x2_t acc[4][4];
+    f32x2_t acc[CO][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < CO; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x2_t{0.f, 0.f};
     int co0 = 0, tap = 0, c8 = 0;
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
       c8 = g % C8;
       const int ct = g / C8;
       tap = ct % T_;
-      co0 = (ct / T_) * 4;
+      co0 = (ct / T_) * CO;
     }
     if (active && g < ng_all) {
       const int ky = tap / a.KW, kx = tap - ky * a.KW;
@@ -123,11 +126,14 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
         for (int ox = sl; ox < a.Wo; ox += SL) {
           const int ix = ox * a.S + kx - a.P;
           if ((unsigned)ix >= (unsigned)a.Wi) continue;
-          float d[4], v[8];
-          ld4<T>(dyrow + (size_t)ox * a.ystr, d);
+          float d[CO], v[8];
+          if constexpr (CO == 8)
+            ld8<T>(dyrow + (size_t)ox * a.ystr, d);
+          else
+            ld4<T>(dyrow + (size_t)ox * a.ystr, d);
           ld8<T>(xrow + (size_t)ix * a.xstr, v);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < CO; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               acc[i][j] = __builtin_elementwise_fma(f32x2_t{d[i], d[i]}, f32x2_t{v[2 * j], v[2 * j + 1]}, acc[i][j]);
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(THREADS) void sconv_wgrad_kernel(WArgs a) {
     }
     // combine the sub-lanes in order, one output channel (8 values) at a time
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < CO; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         red[t * 8 + 2 * j] = acc[i][j].x;
@@ -216,10 +222,18 @@ int sconv_wgrad_blocks(int B, int Ho, int OUT, int* rows_per_block) {
 void sconv_wgrad_launch(const SconvWgradLaunch& L, int nblk, int rows_per_block, hipStream_t stream) {
   swg::WArgs a{L.x, L.dy, L.xstr, L.ystr, L.Cin, L.Cout, L.B, L.Hi, L.Wi, L.Ho, L.Wo, L.KH, L.KW, L.S, L.P,
                rows_per_block, L.part};
-  if (L.f32)
-    hipLaunchKernelGGL(swg::sconv_wgrad_kernel<float>, dim3(nblk), dim3(swg::THREADS), 0, stream, a);
-  else
-    hipLaunchKernelGGL(swg::sconv_wgrad_kernel<bf16_t>, dim3(nblk), dim3(swg::THREADS), 0, stream, a);
+  static const int co_env = [] {
+    const char* e = getenv("RS_SWG_CO");
+    return e ? atoi(e) : 8;
+  }();
+  const bool co8 = co_env == 8 && L.Cout % 8 == 0;
+  if (L.f32) {
+    if (co8) hipLaunchKernelGGL((swg::sconv_wgrad_kernel<float, 8>), dim3(nblk), dim3(swg::THREADS), 0, stream, a);
+    else hipLaunchKernelGGL((swg::sconv_wgrad_kernel<float, 4>), dim3(nblk), dim3(swg::THREADS), 0, stream, a);
+  } else {
+    if (co8) hipLaunchKernelGGL((swg::sconv_wgrad_kernel<bf16_t, 8>), dim3(nblk), dim3(swg::THREADS), 0, stream, a);
+    else hipLaunchKernelGGL((swg::sconv_wgrad_kernel<bf16_t, 4>), dim3(nblk), dim3(swg::THREADS), 0, stream, a);
+  }
   const int OUT = L.Cout * L.KH * L.KW * L.Cin;
   hipLaunchKernelGGL(swg::sconv_wgrad_reduce_kernel, dim3(cdiv(OUT, swg::RD_O)), dim3(swg::RD_O * swg::RD_L), 0, stream,
                      L.part, nblk, OUT, L.dw);
