@@ -17,6 +17,8 @@
 // x is viewed as (B, P, C) with P = H*W; vectors of 16 bytes along C.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace rs {
 namespace norm {
 
@@ -37,6 +39,7 @@ template <> struct Vec<float> {
   __device__ static void store(float* p, const float* v) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
+  __device__ static float rnd(float v) { return v; }
 };
 template <> struct Vec<bf16_t> {
   static constexpr int N = 8;
@@ -65,6 +68,7 @@ template <> struct Vec<bf16_t> {
     for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
+  __device__ static float rnd(float v) { return bf2f(f2bf(v)); }  // the value store() keeps
 };
 
 struct Args {
@@ -98,6 +102,11 @@ struct Args {
   const float* rs1;
   const float* rs2;
   float* ws2;
+  // staged output gradient (plain residual): the reduction stores the
+  // residual's gradient gout = mask(dy + dy2) to dres in the tensor dtype and
+  // takes its sums over those rounded values; apply_bwd then reads x and dres
+  // only (not dy, dy2, res again) and leaves dres alone
+  int gstage;
 };
 
 // BatchNorm running-statistics update, applied by finalize_kernel<0> for
@@ -153,6 +162,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
     const T* dy = static_cast<const T*>(a.dy) + (size_t)b * a.P * a.C;
     const T* dy2 = a.dy2 ? static_cast<const T*>(a.dy2) + (size_t)b * a.P * a.C : nullptr;
     const T* res = a.res ? static_cast<const T*>(a.res) + (size_t)b * a.P * a.C : nullptr;
+    T* gst = MODE == 1 && a.gstage ? static_cast<T*>(a.dres) + (size_t)b * a.P * a.C : nullptr;
     for (int p = p0 + row; p < p1; p += rows * 4) {
       typename V::raw xq[4], dq[4], rq[4], eq[4];
 #pragma unroll
@@ -195,6 +205,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
             const float y1 = a.relu ? fmaxf(pre, 0.f) : pre;
             float gg = dv[i];
             if (res && (aff ? rv[i] * rsc[i] + rsh[i] : rv[i]) + y1 <= 0.f) gg = 0.f;
+            if (gst) gg = dv[i] = V::rnd(gg);  // dv: the staged values
             if (aff) {  // the residual branch's gradient, before the main branch's ReLU mask
               racc0[i] += gg;
               racc1[i] += gg * ((rv[i] - rmu[i]) * rrs[i]);
@@ -203,6 +214,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
             acc0[i] += gg;
             acc1[i] += gg * xh;
           }
+          if (gst) V::store(gst + (size_t)(p + u * rows) * a.C + col * VN, dv);
         }
       }
     }
@@ -418,11 +430,13 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   }
   const size_t base = (size_t)b * a.P * a.C + col * VN;
   const T* x = static_cast<const T*>(a.x) + base;
-  const T* dy = static_cast<const T*>(a.dy) + base;
-  const T* dy2 = a.dy2 ? static_cast<const T*>(a.dy2) + base : nullptr;
-  const T* res = a.res ? static_cast<const T*>(a.res) + base : nullptr;
+  // staged: dy := the masked residual gradient the reduction left in dres
+  const bool st = a.gstage;
+  const T* dy = static_cast<const T*>(st ? a.dres : a.dy) + base;
+  const T* dy2 = a.dy2 && !st ? static_cast<const T*>(a.dy2) + base : nullptr;
+  const T* res = a.res && !st ? static_cast<const T*>(a.res) + base : nullptr;
   T* dx = static_cast<T*>(a.dx) + base;
-  T* dres = a.dres ? static_cast<T*>(a.dres) + base : nullptr;
+  T* dres = a.dres && !st ? static_cast<T*>(a.dres) + base : nullptr;
   const bool relu = a.relu;
   for (int p = p0 + row; p < p1; p += rows * UNR) {
     typename V::raw xq[UNR], dq[UNR], rq[UNR], eq[UNR];
@@ -553,6 +567,14 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
     a.rmean = rnorm[0]; a.rrstd = rnorm[1]; a.rgamma = rnorm[2]; a.rbeta = rnorm[3];
     a.ws2 = ws2;
   }
+  // plain residual: stage the residual gradient in dres during the reduction
+  // (RS_NORM_GSTAGE=0: recompute it in apply_bwd from dy, dy2 and res)
+  static const bool gstage_on = [] {
+    const char* e = getenv("RS_NORM_GSTAGE");
+    return !(e && e[0] == '0');
+  }();
+  a.gstage = gstage_on && res != nullptr && rnorm == nullptr && dres != nullptr;
+  if (a.gstage) a.dres = dres;
   a.S = norm::pick_splits(B, P, C, bf16 ? 8 : 4);
   dim3 grid(a.S, B);
   if (bf16)
