@@ -526,13 +526,21 @@ std::vector<Tensor> convex_upsample_backward(const Tensor& flow, const Tensor& m
 // All inputs are NHWC-contiguous, viewed as (P, channels).
 int64_t pixels(const Tensor& t) { return t.numel() / t.size(-1); }
 
-// cn: (B,H,W,hd+cd) contiguous; hx: (B,H,W,>=hd) and inp: (B,H,W,cd), contiguous rows, cn's dtype
+// cn: (B,H,W,hd+cd) contiguous; hx: (B,H,W,>=hd) contiguous; inp: (B,H,W,cd)
+// with unit channel stride and evenly strided pixel rows (contiguous, or a
+// channel window of a wider NHWC buffer: the inference engine's hx slots);
+// all of cn's dtype
+bool rows_view(const Tensor& t) {
+  return t.stride(3) == 1 && t.stride(2) >= t.size(3) && t.stride(1) == t.size(2) * t.stride(2) &&
+         t.stride(0) == t.size(1) * t.stride(1);
+}
+
 void context_act(const Tensor& cn, const Tensor& hx, const Tensor& inp, int64_t hd) {
   check_gpu(cn, "cn");
   check_dtype(cn, {at::kFloat, at::kBFloat16}, "cn");
   TORCH_CHECK(cn.dim() == 4 && hx.dim() == 4 && inp.dim() == 4 && cn.is_contiguous() && hx.is_contiguous() &&
-                  inp.is_contiguous() && hx.scalar_type() == cn.scalar_type() && inp.scalar_type() == cn.scalar_type(),
-              "context_act: contiguous NHWC tensors of one dtype");
+                  rows_view(inp) && hx.scalar_type() == cn.scalar_type() && inp.scalar_type() == cn.scalar_type(),
+              "context_act: NHWC tensors of one dtype (inp: evenly strided pixel rows)");
   const int64_t cd = cn.size(3) - hd;
   TORCH_CHECK(hd > 0 && cd > 0 && hx.size(3) >= hd && inp.size(3) == cd && hx.sizes().slice(0, 3) == cn.sizes().slice(0, 3) &&
                   inp.sizes().slice(0, 3) == cn.sizes().slice(0, 3),
@@ -540,7 +548,7 @@ void context_act(const Tensor& cn, const Tensor& hx, const Tensor& inp, int64_t 
   const c10::DeviceGuard guard(cn.device());
   const long P = cn.size(0) * cn.size(1) * cn.size(2);
   rs::ctx_act_launch(is_bf16(cn), cn.data_ptr(), P, (int)hd, (int)cd, hx.data_ptr(), (int)hx.size(3), inp.data_ptr(),
-                     (int)cd, cur_stream());
+                     (int)inp.stride(2), cur_stream());
   RS_CHECK_LAUNCH();
 }
 

@@ -236,6 +236,7 @@ class FusedUpdate:
 
     @torch.no_grad()
     def run(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        """inp None: ``net`` is the context encoder's raw (hd + cd)-channel output."""
         self.refresh()
         B, _, H, W = coords1.shape
         bufs = self._buffers(B, H, W, coords1.device)
@@ -248,8 +249,14 @@ class FusedUpdate:
                 conv_fused(segs, w, b, kh, kw, cout, epi, out, ooff, tile=None, **kw_)  # tuned F32 table / heuristic
         else:
             cf = conv_fused
-        hx[..., :hd].copy_(net.permute(0, 2, 3, 1))
-        hx[..., self.off_inp:self.off_inp + self.cd].copy_(inp.permute(0, 2, 3, 1))
+        if inp is None:
+            # net: the context encoder's raw output -- split + tanh / relu
+            # (reference core/raft.py:108-110) straight into the hx slots, one pass
+            cn = net.permute(0, 2, 3, 1).to(hx.dtype).contiguous()
+            torch.ops.raft_stir.context_act(cn, hx, hx[..., self.off_inp:self.off_inp + self.cd], hd)
+        else:
+            hx[..., :hd].copy_(net.permute(0, 2, 3, 1))
+            hx[..., self.off_inp:self.off_inp + self.cd].copy_(inp.permute(0, 2, 3, 1))
         coords1 = coords1.float().contiguous().clone()
         st = getattr(corr_fn, "state", None)  # None: on-the-fly correlation
         small = self.model.cfg.small

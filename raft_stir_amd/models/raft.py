@@ -66,6 +66,7 @@ class _StreamHandoff(torch.autograd.Function):
 
 _SIDE_STREAMS = {}  # (device index, slot) -> extra HIP stream
 _FUSED_PREP = True  # one-kernel input normalisation into the fnet batch
+_GRID_CACHE: dict = {}  # (h, w, device) -> (1, 2, h, w) pixel-coordinate grid (initialize_flow)
 # per-mechanism switches of the multi-stream schedule (all gated by cfg.overlap_encoders)
 # defer_enc (encoder conv weight gradients on the deferred stream too) is off:
 # paired A/B on one box, 3 x 30 steps: 352 pairs/s on vs 366 off (the third
@@ -183,9 +184,22 @@ class RAFT(nn.Module):
 
     def initialize_flow(self, img):
         N, _, H, W = img.shape
-        c0 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
-        c1 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
-        return c0, c1
+        if img.device.type != "cuda" or torch.jit.is_tracing():
+            c0 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
+            c1 = ref.coords_grid(N, H // 8, W // 8, device=img.device)
+            return c0, c1
+        # one cached (1, 2, h, w) grid per shape, expanded into two fresh
+        # tensors: two copy kernels per forward instead of eight (arange x4,
+        # stack, repeat); not cached while a hipGraph is being captured (its
+        # memory would belong to the graph's pool)
+        key = (H // 8, W // 8, img.device)
+        g = _GRID_CACHE.get(key)
+        if g is None:
+            g = ref.coords_grid(1, H // 8, W // 8, device=img.device)
+            if not torch.cuda.is_current_stream_capturing():
+                _GRID_CACHE[key] = g
+        shape = (N,) + tuple(g.shape[1:])
+        return g.expand(shape).clone(), g.expand(shape).clone()
 
     def upsample_flow(self, flow, mask):
         return convex_upsample(flow, mask)
@@ -299,9 +313,10 @@ class RAFT(nn.Module):
             elif not fused_enc:
                 cnet = self.cnet(image1)
             fused_train = not test_mode and FusedTrainEngine.eligible(self, image1, corr_fn)
-            if fused_train and not self.cfg.small:
-                # the fused engine splits the context features and applies tanh / relu
-                # itself, straight into its buffers (FusedTrainLoop, context_act)
+            fused_inf = not fused_train and FusedUpdate.eligible(self, image1, corr_fn)
+            if (fused_train and not self.cfg.small) or fused_inf:
+                # the fused engines split the context features and apply tanh / relu
+                # themselves, straight into their buffers (context_act)
                 net, inp = cnet, None
             else:
                 net, inp = torch.split(cnet, [hdim, cdim], dim=1)
@@ -330,7 +345,7 @@ class RAFT(nn.Module):
                                    "but this step is not eligible for it (update-block gradients "
                                    "would not be all-reduced)")
 
-            if FusedUpdate.eligible(self, image1, corr_fn):
+            if fused_inf:
                 eng = self._fused_engine()
                 coords1, preds, flow_up = eng.run(net, inp, corr_fn, coords0, coords1, iters, test_mode)
                 if test_mode:
