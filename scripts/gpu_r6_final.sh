@@ -18,3 +18,7 @@ for l in sys.stdin:
     d=json.loads(l); c=d['config']; i=d.get('inference') or {}
     print(c['model'][:12], c.get('train_step'), d['value'], d['ms_per_step'], i.get('fps'), i.get('ms_per_pair'))
 "
+# per-kernel time of the training step and of the inference forward (no counters)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_train -o k -- python bench.py --steps 10 --warmup 3 --no-infer > $OUT/prof_train.log 2>&1 || { tail -20 $OUT/prof_train.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_infer -o k -- python bench.py --steps 1 --warmup 1 --infer-reps 25 > $OUT/prof_infer.log 2>&1 || { tail -20 $OUT/prof_infer.log; exit 1; }
+find $OUT -name '*kernel_stats.csv' | head -5
