@@ -124,8 +124,13 @@ struct Running {
 // --------------------------------------------------------------- reductions
 // MODE 0: (x, x^2).  MODE 1: (g, g * xhat) with g the gradient reaching the
 // pre-activation a = gamma * xhat + beta.
-template <typename T, int MODE>
+// AFF (MODE 1 only): the affine residual's constants and partial set are
+// compiled in only where they are used -- as a run-time branch they held ~50
+// VGPRs through the loop of every backward reduction and kept it at two waves
+// per SIMD.  RU: pixel rows in flight per thread (MODE 0 reads one tensor).
+template <typename T, int MODE, bool AFF = false>
 __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
+  constexpr int RU = MODE == 0 ? 8 : 4;
   using V = Vec<T>;
   constexpr int VN = V::N;
   const int CV = a.C / VN;
@@ -139,7 +144,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
 #pragma unroll
   for (int i = 0; i < VN; ++i) acc0[i] = acc1[i] = racc0[i] = racc1[i] = 0.f;
   const int g = a.G == 1 ? 0 : b;
-  const bool aff = MODE == 1 && a.rmean != nullptr;  // affine residual (+ its own partials)
+  constexpr bool aff = MODE == 1 && AFF;  // affine residual (+ its own partials)
   float mu[VN], rs_[VN], ga[VN], be[VN], rmu[VN], rrs[VN], rsc[VN], rsh[VN];
   if (MODE == 1 && row < rows) {
 #pragma unroll
@@ -163,10 +168,10 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
     const T* dy2 = a.dy2 ? static_cast<const T*>(a.dy2) + (size_t)b * a.P * a.C : nullptr;
     const T* res = a.res ? static_cast<const T*>(a.res) + (size_t)b * a.P * a.C : nullptr;
     T* gst = MODE == 1 && a.gstage ? static_cast<T*>(a.dres) + (size_t)b * a.P * a.C : nullptr;
-    for (int p = p0 + row; p < p1; p += rows * 4) {
-      typename V::raw xq[4], dq[4], rq[4], eq[4];
+    for (int p = p0 + row; p < p1; p += rows * RU) {
+      typename V::raw xq[RU], dq[RU], rq[RU], eq[RU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RU; ++u) {
         const int pp = p + u * rows;
         if (pp < p1) {
           const size_t off = (size_t)pp * a.C + col * VN;
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(THREADS) void reduce_kernel(Args a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RU; ++u) {
         if (p + u * rows >= p1) break;
         float xv[VN];
         V::cvt(xq[u], xv);
@@ -493,8 +498,20 @@ int pick_apply_splits(int B, int P, int C, int vn) {
 // norm_set_reduce_blocks: in-situ A/B of the target (RS_NORM_REDUCE_BLOCKS)
 int g_reduce_target = 512;
 
-int pick_splits(int B, int P, int C, int vn) {
-  const int target = g_reduce_target;
+// block target of the statistics pass (MODE 0), RS_NORM_STATS_BLOCKS to
+// compare: 512 / 1024 / 2048 measured the same alone (18.6 / 18.5 / 19.8 us
+// at 16 x 184 x 248 x 64 with RU = 8), 2048 slightly slower in situ
+// (profiles/r6/ab_norm_reduce_aff_s43.txt)
+int stats_target() {
+  static const int t = [] {
+    const char* e = getenv("RS_NORM_STATS_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 512;
+  }();
+  return t;
+}
+
+int pick_splits(int B, int P, int C, int vn, bool stats = false) {
+  const int target = stats ? stats_target() : g_reduce_target;
   const int rows = THREADS / (C / vn);
   int S = cdiv(target, B);
   S = max(1, min(S, cdiv(P, rows * 8)));
@@ -511,8 +528,8 @@ int grid_elem(size_t nvec) {
 void norm_set_reduce_blocks(int n) { norm::g_reduce_target = n > 0 ? n : 512; }
 
 // ------------------------------------------------------------------ launchers
-int norm_ws_floats(int B, int P, int C, bool bf16) {
-  const int S = norm::pick_splits(B, P, C, bf16 ? 8 : 4);
+int norm_ws_floats(int B, int P, int C, bool bf16, bool stats) {
+  const int S = norm::pick_splits(B, P, C, bf16 ? 8 : 4, stats);
   return B * S * C * 2;
 }
 
@@ -523,7 +540,7 @@ void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, flo
   norm::Args a{};
   a.x = x;
   a.B = B; a.P = P; a.C = C; a.G = G;
-  a.S = norm::pick_splits(B, P, C, bf16 ? 8 : 4);
+  a.S = norm::pick_splits(B, P, C, bf16 ? 8 : 4, true);
   a.ws = ws;
   dim3 grid(a.S, B);
   if (bf16)
@@ -577,10 +594,17 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
   if (a.gstage) a.dres = dres;
   a.S = norm::pick_splits(B, P, C, bf16 ? 8 : 4);
   dim3 grid(a.S, B);
-  if (bf16)
-    hipLaunchKernelGGL((norm::reduce_kernel<bf16_t, 1>), grid, dim3(norm::THREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL((norm::reduce_kernel<float, 1>), grid, dim3(norm::THREADS), 0, s, a);
+  if (bf16) {
+    if (rnorm)
+      hipLaunchKernelGGL((norm::reduce_kernel<bf16_t, 1, true>), grid, dim3(norm::THREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL((norm::reduce_kernel<bf16_t, 1>), grid, dim3(norm::THREADS), 0, s, a);
+  } else {
+    if (rnorm)
+      hipLaunchKernelGGL((norm::reduce_kernel<float, 1, true>), grid, dim3(norm::THREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL((norm::reduce_kernel<float, 1>), grid, dim3(norm::THREADS), 0, s, a);
+  }
   hipLaunchKernelGGL(norm::finalize_kernel<1>, dim3(G, cdiv(C, 8), rnorm ? 2 : 1), dim3(256), 0, s, ws, B, a.S,
                      C, G, 0.f, 0.f, s1, s2, norm::Running{}, ws2, rs1, rs2);
   a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres; a.rs1 = rs1; a.rs2 = rs2;

@@ -7,7 +7,7 @@
 #include <hip/hip_runtime.h>
 
 namespace rs {
-int norm_ws_floats(int B, int P, int C, bool bf16);
+int norm_ws_floats(int B, int P, int C, bool bf16, bool stats);
 void norm_set_reduce_blocks(int n);
 void norm_stats_launch(bool bf16, const void* x, int B, int P, int C, int G, float eps, float* ws,
                        float* mean, float* rstd, float* rm, float* rv, long long* nbt, const float* rbias,
@@ -68,7 +68,7 @@ std::vector<Tensor> norm_stats(const Tensor& x, bool per_sample, double eps, con
   check_param(bias, C, "bias");
   if (nbt) TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "norm_stats: nbt");
   auto fo = x.options().dtype(at::kFloat);
-  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
+  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf, true)}, fo);
   Tensor mean = at::empty({G, C}, fo), rstd = at::empty({G, C}, fo);
   const float unb = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
   rs::norm_stats_launch(bf, x.data_ptr(), B, P, C, G, (float)eps, ws.data_ptr<float>(), mean.data_ptr<float>(),
@@ -159,7 +159,7 @@ std::vector<Tensor> norm_act_backward(const Tensor& dy, const Tensor& x, const T
   const c10::DeviceGuard g(x.device());
   const bool bf = x.scalar_type() == at::kBFloat16;
   auto fo = x.options().dtype(at::kFloat);
-  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf)}, fo);
+  Tensor ws = at::empty({rs::norm_ws_floats(B, P, C, bf, false)}, fo);
   // s1 / s2 are the two halves of one (2, G, C) buffer: the per-channel sums
   // over groups (dbeta, dgamma) are then ONE reduction (ops/norm.py)
   Tensor s12 = at::empty({2, G, C}, fo);
