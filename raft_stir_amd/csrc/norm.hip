@@ -336,7 +336,10 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* ws, int B, i
 // is unrolled UNR deep so that many 16-B loads are in flight per thread.
 constexpr int UNR = 4;
 
-template <typename T>
+// AFF / K: compile-time variants, as for reduce_kernel (registers): apply_bwd
+// K = 0 plain (dy2 / res at run time), 1 affine residual, 2 staged gradient,
+// 3 neither dy2 nor res (x and dy only)
+template <typename T, bool AFF>
 __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
   using V = Vec<T>;
   constexpr int VN = V::N;
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
   const int chunk = cdiv(a.P, a.S);
   const int p0 = blockIdx.x * chunk, p1 = min(a.P, p0 + chunk);
   float sc[VN], sh[VN], rsc[VN], rsh[VN];
-  const bool aff = a.rmean != nullptr;
+  constexpr bool aff = AFF;
 #pragma unroll
   for (int i = 0; i < VN; ++i) {
     const int c = col * VN + i;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(THREADS) void apply_fwd_kernel(Args a) {
   }
 }
 
-template <typename T>
+template <typename T, int K>
 __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   using V = Vec<T>;
   constexpr int VN = V::N;
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   // k1 = gamma*rstd, m1 = s1/N, k2 = gamma*rstd^2*s2/N
   float sc[VN], sh[VN], k0[VN], k2[VN], mu[VN];
   float rsc[VN], rsh[VN], rk0[VN], rk2[VN], rmu[VN];
-  const bool aff = a.rmean != nullptr;
+  constexpr bool aff = K == 1;
 #pragma unroll
   for (int i = 0; i < VN; ++i) {
     const int c = col * VN + i;
@@ -436,10 +439,10 @@ __global__ __launch_bounds__(THREADS) void apply_bwd_kernel(Args a) {
   const size_t base = (size_t)b * a.P * a.C + col * VN;
   const T* x = static_cast<const T*>(a.x) + base;
   // staged: dy := the masked residual gradient the reduction left in dres
-  const bool st = a.gstage;
+  constexpr bool st = K == 2;
   const T* dy = static_cast<const T*>(st ? a.dres : a.dy) + base;
-  const T* dy2 = a.dy2 && !st ? static_cast<const T*>(a.dy2) + base : nullptr;
-  const T* res = a.res && !st ? static_cast<const T*>(a.res) + base : nullptr;
+  const T* dy2 = K != 3 && a.dy2 && !st ? static_cast<const T*>(a.dy2) + base : nullptr;
+  const T* res = K != 3 && a.res && !st ? static_cast<const T*>(a.res) + base : nullptr;
   T* dx = static_cast<T*>(a.dx) + base;
   T* dres = a.dres && !st ? static_cast<T*>(a.dres) + base : nullptr;
   const bool relu = a.relu;
@@ -563,10 +566,18 @@ void norm_fwd_launch(bool bf16, const void* x, const void* res, const float* mea
   if (rnorm) { a.rmean = rnorm[0]; a.rrstd = rnorm[1]; a.rgamma = rnorm[2]; a.rbeta = rnorm[3]; }
   a.B = B; a.P = P; a.C = C; a.G = G; a.relu = relu;
   a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
-  if (bf16)
-    hipLaunchKernelGGL(norm::apply_fwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL(norm::apply_fwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
+  const dim3 grid(a.S, B);
+  if (bf16) {
+    if (rnorm)
+      hipLaunchKernelGGL((norm::apply_fwd_kernel<bf16_t, true>), grid, dim3(norm::THREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL((norm::apply_fwd_kernel<bf16_t, false>), grid, dim3(norm::THREADS), 0, s, a);
+  } else {
+    if (rnorm)
+      hipLaunchKernelGGL((norm::apply_fwd_kernel<float, true>), grid, dim3(norm::THREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL((norm::apply_fwd_kernel<float, false>), grid, dim3(norm::THREADS), 0, s, a);
+  }
 }
 
 // dy2: second upstream gradient (added on the fly) or null.  rnorm: as in
@@ -610,10 +621,24 @@ void norm_bwd_launch(bool bf16, const void* x, const void* dy, const void* res, 
   a.s1 = s1; a.s2 = s2; a.dx = dx; a.dres = dres; a.rs1 = rs1; a.rs2 = rs2;
   a.inv_n = batch_stats ? 1.f / (float)((G == 1 ? (double)B : 1.0) * P) : 0.f;
   a.S = norm::pick_apply_splits(B, P, C, bf16 ? 8 : 4);
+  const dim3 agrid(a.S, B);
+  const int kind = rnorm ? 1 : (a.gstage ? 2 : (!res && !dy2 ? 3 : 0));
+#define RS_NORM_APPLY_BWD(TT)                                                                        \
+  do {                                                                                               \
+    if (kind == 1)                                                                                   \
+      hipLaunchKernelGGL((norm::apply_bwd_kernel<TT, 1>), agrid, dim3(norm::THREADS), 0, s, a);     \
+    else if (kind == 2)                                                                              \
+      hipLaunchKernelGGL((norm::apply_bwd_kernel<TT, 2>), agrid, dim3(norm::THREADS), 0, s, a);     \
+    else if (kind == 3)                                                                              \
+      hipLaunchKernelGGL((norm::apply_bwd_kernel<TT, 3>), agrid, dim3(norm::THREADS), 0, s, a);     \
+    else                                                                                             \
+      hipLaunchKernelGGL((norm::apply_bwd_kernel<TT, 0>), agrid, dim3(norm::THREADS), 0, s, a);     \
+  } while (0)
   if (bf16)
-    hipLaunchKernelGGL(norm::apply_bwd_kernel<bf16_t>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
+    RS_NORM_APPLY_BWD(bf16_t);
   else
-    hipLaunchKernelGGL(norm::apply_bwd_kernel<float>, dim3(a.S, B), dim3(norm::THREADS), 0, s, a);
+    RS_NORM_APPLY_BWD(float);
+#undef RS_NORM_APPLY_BWD
 }
 
 }  // namespace rs
